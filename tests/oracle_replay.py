@@ -1,0 +1,76 @@
+"""Replay helpers: drive the batched CPU oracle over the golden episodes (all episodes of
+a fixture as parallel envs) and collect per-step outputs aligned with the fixture."""
+from __future__ import annotations
+
+import numpy as np
+
+from oracle import batched as ob
+
+
+def replay_merge(g, autoreset=ob.AUTORESET_NONE):
+    n_ep = len(g["length"])
+    N = int(g["num_ac"])
+    T = g["actions"].shape[1]
+    o = ob.MergeOracle(n_ep, num_ac=N, autoreset=autoreset, compute_cd=False)
+    r0 = o.reset(spawn=g["spawn"])
+    out = {"obs0": r0["obs"], "obs": [], "reward": [], "terminated": [], "truncated": [],
+           "topk": [], "intr": [], "state": [], "info": []}
+    for t in range(T):
+        r = o.step(g["actions"][:, t])
+        out["obs"].append(r["obs"]); out["reward"].append(r["reward"])
+        out["terminated"].append(r["terminated"]); out["truncated"].append(r["truncated"])
+        out["topk"].append(r["topk"])
+        out["intr"].append(np.stack([(r["intr_mask"] >> np.uint64(i + 1)) & np.uint64(1)
+                                     for i in range(N - 1)], 1).astype(np.int8))
+        out["state"].append(np.stack([o.st.lat, o.st.lon, o.st.alt, o.st.hdg, o.st.tas,
+                                      o.st.cas, o.st.vs], 1))
+        inf = o.info()
+        out["info"].append(np.stack([inf["total_reward"], inf["faf_reach"],
+                                     inf["average_drift"], inf["total_intrusions"]], 1))
+    return {k: (np.stack(v, 1) if k != "obs0" else v) for k, v in out.items()}
+
+
+def replay_vertical(g, autoreset=ob.AUTORESET_NONE):
+    n_ep = len(g["length"])
+    N = int(g["num_ac"])
+    T = g["actions"].shape[1]
+    o = ob.VerticalOracle(n_ep, num_ac=N, autoreset=autoreset, compute_cd=False)
+    r0 = o.reset(spawn=g["spawn"])
+    out = {"obs0": r0["obs"], "obs": [], "reward": [], "terminated": [], "truncated": [],
+           "intr": [], "state": [], "info": []}
+    for t in range(T):
+        r = o.step(g["actions"][:, t])
+        out["obs"].append(r["obs"]); out["reward"].append(r["reward"])
+        out["terminated"].append(r["terminated"]); out["truncated"].append(r["truncated"])
+        out["intr"].append(np.stack([(r["intr_mask"] >> np.uint64(i + 1)) & np.uint64(1)
+                                     for i in range(N - 1)], 1).astype(np.int8))
+        out["state"].append(np.stack([o.st.lat, o.st.lon, o.st.alt, o.st.hdg, o.st.tas,
+                                      o.st.cas, o.st.vs], 1))
+        inf = o.info()
+        out["info"].append(np.stack([inf["total_reward"], inf["total_intrusions"],
+                                     inf["final_altitude"]], 1))
+    return {k: (np.stack(v, 1) if k != "obs0" else v) for k, v in out.items()}
+
+
+def replay_descent(g, autoreset=ob.AUTORESET_NONE):
+    n_ep = len(g["length"])
+    T = g["actions"].shape[1]
+    o = ob.DescentOracle(n_ep, autoreset=autoreset)
+    r0 = o.reset(spawn=g["spawn"])
+    out = {"obs0": r0["obs"], "obs": [], "reward": [], "terminated": [], "truncated": [],
+           "state": [], "info": []}
+    for t in range(T):
+        r = o.step(g["actions"][:, t])
+        out["obs"].append(r["obs"]); out["reward"].append(r["reward"])
+        out["terminated"].append(r["terminated"]); out["truncated"].append(r["truncated"])
+        out["state"].append(np.stack([o.st.lat, o.st.lon, o.st.alt, o.st.hdg, o.st.tas,
+                                      o.st.cas, o.st.vs], 1))
+        inf = o.info()
+        out["info"].append(np.stack([inf["total_reward"], inf["final_altitude"]], 1))
+    return {k: (np.stack(v, 1) if k != "obs0" else v) for k, v in out.items()}
+
+
+def step_mask(g):
+    """[n_ep, T] bool: steps inside each recorded episode."""
+    T = g["actions"].shape[1]
+    return np.arange(T)[None, :] < g["length"][:, None]
