@@ -1,0 +1,133 @@
+"""ctypes binding of libbsg.so (include/bsg.h).
+
+The product path: every env step of ``bluesky_gym`` goes through these entry points.
+There is no CPU fallback -- if the HIP library is missing or no HIP device is present,
+construction raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("BSG_LIBRARY", os.path.join(_HERE, "_lib", "libbsg.so"))
+
+ABI_VERSION = 1
+MAX_ROUTE = 4
+
+ENV_MERGE, ENV_VERTICAL_CR, ENV_DESCENT = 0, 1, 2
+AUTORESET_NONE, AUTORESET_NEXT_STEP, AUTORESET_SAME_STEP = 0, 1, 2
+
+E_CODES = {-1: "BSG_E_INVALID_ARG", -2: "BSG_E_HIP", -3: "BSG_E_STATE", -4: "BSG_E_UNSUPPORTED"}
+
+_dp = C.POINTER(C.c_double)
+_fp = C.POINTER(C.c_float)
+_i32p = C.POINTER(C.c_int32)
+_u32p = C.POINTER(C.c_uint32)
+_u8p = C.POINTER(C.c_uint8)
+_u64p = C.POINTER(C.c_uint64)
+
+
+class BsgConfig(C.Structure):
+    _fields_ = [
+        ("abi_version", C.c_int32),
+        ("env_kind", C.c_int32),
+        ("num_envs", C.c_int32),
+        ("num_ac", C.c_int32),
+        ("num_ac_state", C.c_int32),
+        ("action_frequency", C.c_int32),
+        ("simdt", C.c_double),
+        ("max_episode_steps", C.c_int32),
+        ("autoreset_mode", C.c_int32),
+        ("compute_cd", C.c_int32),
+        ("device", C.c_int32),
+        ("seed", C.c_uint64),
+        ("route_len", C.c_int32),
+        ("_pad0", C.c_int32),
+        ("route_lat", C.c_double * MAX_ROUTE),
+        ("route_lon", C.c_double * MAX_ROUTE),
+        ("route_next_qdr", C.c_double * MAX_ROUTE),
+        ("wpt_lat", C.c_double * 2),
+        ("wpt_lon", C.c_double * 2),
+    ]
+
+
+# (name, ctype pointer) in include/bsg.h order
+BUFFER_FIELDS = [
+    ("lat", _dp), ("lon", _dp), ("alt", _dp), ("hdg", _dp), ("tas", _dp), ("cas", _dp),
+    ("vs", _dp), ("ax", _dp), ("ap_trk", _dp), ("selspd", _dp), ("selalt", _dp),
+    ("selvs", _dp), ("nav", _i32p),
+    ("step_count", _i32p), ("flags", _i32p), ("episode", _u32p), ("wpt_reach", _i32p),
+    ("faf_reached", _i32p), ("total_intrusions", _i32p), ("total_reward", _dp),
+    ("drift_sum", _dp), ("target_alt", _dp), ("final_altitude", _dp),
+    ("obs", _fp), ("final_obs", _fp), ("reward", _fp), ("terminated", _u8p),
+    ("truncated", _u8p), ("topk", _i32p), ("intr_mask", _u64p), ("conf_mask", _u64p),
+    ("los_mask", _u64p), ("tcpamax", _fp), ("min_sep", _fp), ("ep_info", _dp),
+]
+
+
+class BsgBuffers(C.Structure):
+    _fields_ = [(n, t) for n, t in BUFFER_FIELDS]
+
+
+EXPORTED_SYMBOLS = (
+    "bsg_abi_version", "bsg_last_error", "bsg_obs_dim", "bsg_action_dim", "bsg_spawn_width",
+    "bsg_create", "bsg_destroy", "bsg_bind", "bsg_reset", "bsg_step", "bsg_set_timing",
+    "bsg_step_timing",
+)
+
+_lib = None
+
+
+class BsgError(RuntimeError):
+    pass
+
+
+def load_library(path: str | None = None):
+    """Load libbsg.so once and declare every signature of include/bsg.h."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise BsgError(f"libbsg.so not found at {p}: build it with "
+                       f"`python -c 'import __graft_entry__ as g; g.build()'` or `make -C "
+                       f"bluesky-gym-hallucination_amd/csrc`")
+    lib = C.CDLL(p)
+    lib.bsg_abi_version.restype = C.c_int32
+    lib.bsg_abi_version.argtypes = []
+    lib.bsg_last_error.restype = C.c_char_p
+    lib.bsg_last_error.argtypes = []
+    for fn in ("bsg_obs_dim",):
+        getattr(lib, fn).restype = C.c_int32
+        getattr(lib, fn).argtypes = [C.c_int32, C.c_int32, C.c_int32]
+    lib.bsg_action_dim.restype = C.c_int32
+    lib.bsg_action_dim.argtypes = [C.c_int32]
+    lib.bsg_spawn_width.restype = C.c_int32
+    lib.bsg_spawn_width.argtypes = [C.c_int32, C.c_int32]
+    lib.bsg_create.restype = C.c_int32
+    lib.bsg_create.argtypes = [C.POINTER(BsgConfig), C.POINTER(C.c_void_p)]
+    lib.bsg_destroy.restype = C.c_int32
+    lib.bsg_destroy.argtypes = [C.c_void_p]
+    lib.bsg_bind.restype = C.c_int32
+    lib.bsg_bind.argtypes = [C.c_void_p, C.POINTER(BsgBuffers)]
+    lib.bsg_reset.restype = C.c_int32
+    lib.bsg_reset.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+    lib.bsg_step.restype = C.c_int32
+    lib.bsg_step.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+    lib.bsg_set_timing.restype = C.c_int32
+    lib.bsg_set_timing.argtypes = [C.c_void_p, C.c_int32]
+    lib.bsg_step_timing.restype = C.c_int32
+    lib.bsg_step_timing.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_int32)]
+    if lib.bsg_abi_version() != ABI_VERSION:
+        raise BsgError(f"libbsg ABI {lib.bsg_abi_version()} != expected {ABI_VERSION}")
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        lib = load_library()
+        msg = lib.bsg_last_error().decode(errors="replace")
+        raise BsgError(f"{what} failed ({E_CODES.get(rc, rc)}): {msg}")

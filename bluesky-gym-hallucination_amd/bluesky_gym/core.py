@@ -1,0 +1,154 @@
+"""DeviceBatch: E independent envs of one kind as device-resident SoA tensors, stepped by
+libbsg.so.  PyTorch-ROCm provides device memory and the stream; all arithmetic runs in
+the HIP kernels (csrc/bsg_kernels.hip).  There is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import torch
+
+from . import _native as nat
+from .config import EnvKindConfig
+
+F64_STATE = ("lat", "lon", "alt", "hdg", "tas", "cas", "vs", "ax",
+             "ap_trk", "selspd", "selalt", "selvs")
+I32_ENV = ("step_count", "flags", "wpt_reach", "faf_reached", "total_intrusions")
+F64_ENV = ("total_reward", "drift_sum", "target_alt", "final_altitude")
+
+
+class DeviceBatch:
+    def __init__(self, cfg: EnvKindConfig, num_envs: int, *, autoreset=nat.AUTORESET_NEXT_STEP,
+                 compute_cd=True, seed=0, device=None):
+        if not torch.cuda.is_available():
+            raise nat.BsgError("bluesky_gym needs a HIP device (MI355X); none is visible")
+        self.lib = nat.load_library()
+        self.cfg = cfg
+        self.E = int(num_envs)
+        self.N = cfg.num_ac
+        self.K = cfg.num_ac_state
+        self.device = torch.device("cuda", torch.cuda.current_device() if device is None
+                                   else torch.device(device).index or 0)
+        self.autoreset = autoreset
+        self.compute_cd = bool(compute_cd) and cfg.kind != nat.ENV_DESCENT
+        self.obs_dim = self.lib.bsg_obs_dim(cfg.kind, cfg.num_ac, cfg.num_ac_state)
+        if self.obs_dim < 0:
+            raise nat.BsgError(f"invalid env config {cfg}")
+        self.act_dim = self.lib.bsg_action_dim(cfg.kind)
+        self.spawn_width = self.lib.bsg_spawn_width(cfg.kind, cfg.num_ac)
+        ccfg = cfg.to_c(self.E, autoreset, self.compute_cd, seed, self.device.index)
+        ctx = C.c_void_p()
+        nat.check(self.lib.bsg_create(C.byref(ccfg), C.byref(ctx)), "bsg_create")
+        self._ctx = ctx
+        self._alloc()
+        self._bind()
+
+    # ------------------------------------------------------------------ buffers
+    def _alloc(self):
+        d, E, N = self.device, self.E, self.N
+        z = lambda shape, dt: torch.zeros(shape, dtype=dt, device=d)
+        self.state = {k: z((E, N), torch.float64) for k in F64_STATE}
+        self.state["nav"] = z((E, N), torch.int32)
+        self.envs = {k: z((E,), torch.int32) for k in I32_ENV}
+        self.envs["episode"] = z((E,), torch.int32)     # uint32 on the device side
+        self.envs.update({k: z((E,), torch.float64) for k in F64_ENV})
+        self.obs = z((E, self.obs_dim), torch.float32)
+        self.final_obs = z((E, self.obs_dim), torch.float32) \
+            if self.autoreset == nat.AUTORESET_SAME_STEP else None
+        self.reward = z((E,), torch.float32)
+        self.terminated = z((E,), torch.uint8)
+        self.truncated = z((E,), torch.uint8)
+        self.topk = z((E, max(self.K, 1)), torch.int32) if self.cfg.kind == nat.ENV_MERGE else None
+        self.intr_mask = z((E,), torch.int64)
+        self.ep_info = z((E, 4), torch.float64)
+        if self.compute_cd:
+            self.conf_mask = z((E, N), torch.int64)
+            self.los_mask = z((E, N), torch.int64)
+            self.tcpamax = z((E, N), torch.float32)
+            self.min_sep = z((E,), torch.float32)
+        else:
+            self.conf_mask = self.los_mask = self.tcpamax = self.min_sep = None
+
+    def _bind(self):
+        b = nat.BsgBuffers()
+        src = dict(self.state)
+        src.update(self.envs)
+        src.update(obs=self.obs, final_obs=self.final_obs, reward=self.reward,
+                   terminated=self.terminated, truncated=self.truncated, topk=self.topk,
+                   intr_mask=self.intr_mask, conf_mask=self.conf_mask, los_mask=self.los_mask,
+                   tcpamax=self.tcpamax, min_sep=self.min_sep, ep_info=self.ep_info)
+        for name, ptype in nat.BUFFER_FIELDS:
+            t = src.get(name)
+            setattr(b, name, C.cast(C.c_void_p(t.data_ptr()), ptype) if t is not None
+                    else ptype())
+        self._bufs = b
+        nat.check(self.lib.bsg_bind(self._ctx, C.byref(b)), "bsg_bind")
+
+    def _stream(self):
+        return C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    # ------------------------------------------------------------------ API
+    def reset(self, env_mask: torch.Tensor | None = None, spawn: torch.Tensor | None = None):
+        """Env.reset for the envs in env_mask (u8/bool [E] on device; None = all).
+        spawn: f64 [E, spawn_width] on device (parity mode) or None (device Philox)."""
+        m = None
+        if env_mask is not None:
+            m = env_mask.to(device=self.device, dtype=torch.uint8).contiguous()
+        sp = self._spawn_arg(spawn)
+        nat.check(self.lib.bsg_reset(self._ctx, C.c_void_p(m.data_ptr()) if m is not None else None,
+                                     C.c_void_p(sp.data_ptr()) if sp is not None else None,
+                                     self._stream()), "bsg_reset")
+        self._keep = (m, sp)
+        return self.obs
+
+    def step(self, actions: torch.Tensor, spawn: torch.Tensor | None = None):
+        """One RL step of every env.  actions: [E, act_dim] (any float dtype/device; kept
+        as f64 on device).  Returns (obs, reward, terminated, truncated) device views."""
+        a = actions
+        if a.dtype != torch.float64 or a.device != self.device or not a.is_contiguous():
+            a = a.to(device=self.device, dtype=torch.float64).contiguous()
+        if a.shape != (self.E, self.act_dim):
+            a = a.reshape(self.E, self.act_dim)
+        sp = self._spawn_arg(spawn)
+        nat.check(self.lib.bsg_step(self._ctx, C.c_void_p(a.data_ptr()),
+                                    C.c_void_p(sp.data_ptr()) if sp is not None else None,
+                                    self._stream()), "bsg_step")
+        self._keep = (a, sp)
+        return self.obs, self.reward, self.terminated, self.truncated
+
+    def _spawn_arg(self, spawn):
+        if spawn is None:
+            return None
+        sp = spawn.to(device=self.device, dtype=torch.float64).contiguous()
+        if sp.shape != (self.E, self.spawn_width):
+            raise nat.BsgError(f"spawn must be [{self.E}, {self.spawn_width}], got {tuple(sp.shape)}")
+        return sp
+
+    def set_timing(self, enable: bool):
+        nat.check(self.lib.bsg_set_timing(self._ctx, int(enable)), "bsg_set_timing")
+
+    def step_timing(self):
+        """(total kernel ms, launches) since the last call (HIP events on the launch stream)."""
+        ms = C.c_double()
+        n = C.c_int32()
+        nat.check(self.lib.bsg_step_timing(self._ctx, C.byref(ms), C.byref(n)), "bsg_step_timing")
+        return ms.value, n.value
+
+    def info(self):
+        """Per-env running info (device tensors)."""
+        return dict(total_reward=self.envs["total_reward"],
+                    total_intrusions=self.envs["total_intrusions"],
+                    faf_reach=self.envs["faf_reached"],
+                    drift_sum=self.envs["drift_sum"], step_count=self.envs["step_count"],
+                    final_altitude=self.envs["final_altitude"])
+
+    def close(self):
+        if getattr(self, "_ctx", None) is not None and self._ctx.value:
+            self.lib.bsg_destroy(self._ctx)
+            self._ctx = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

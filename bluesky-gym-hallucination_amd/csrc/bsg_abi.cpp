@@ -1,0 +1,244 @@
+// bsg_abi.cpp -- extern "C" boundary of libbsg.so (declared in include/bsg.h).
+//
+// Validation, thread-local error reporting and launch plumbing only; all arithmetic
+// lives in bsg_kernels.hip.  No C++ exception crosses the ABI.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/bsg.h"
+#include "bsg_internal.h"
+
+struct bsg_ctx {
+  bsg_config cfg;
+  bsg_buffers bufs;
+  bool bound = false;
+  int obs_dim = 0;
+  int spawn_width = 0;
+  bsg::Route route{};
+  // optional per-launch timing (bsg_set_timing)
+  bool timing = false;
+  std::vector<hipEvent_t> ev_pool;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> pending;
+};
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, const char* a = "", long long b = 0) {
+  char buf[512];
+  std::snprintf(buf, sizeof(buf), fmt, a, b);
+  g_err = buf;
+  return code;
+}
+
+int hip_fail(hipError_t e, const char* where) {
+  g_err = std::string(where) + ": " + hipGetErrorString(e);
+  return BSG_E_HIP;
+}
+
+hipEvent_t take_event(bsg_ctx* c) {
+  if (!c->ev_pool.empty()) {
+    hipEvent_t e = c->ev_pool.back();
+    c->ev_pool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  if (hipEventCreate(&e) != hipSuccess) return nullptr;
+  return e;
+}
+
+bsg::KParams make_params(const bsg_ctx* c, int mode) {
+  bsg::KParams p;
+  std::memset(&p, 0, sizeof(p));
+  p.cfg = c->cfg;
+  p.route = c->route;
+  p.b = c->bufs;
+  p.mode = mode;
+  p.E = c->cfg.num_envs;
+  p.N = c->cfg.num_ac;
+  p.K = c->cfg.num_ac_state;
+  p.obs_dim = c->obs_dim;
+  p.spawn_width = c->spawn_width;
+  p.seed = c->cfg.seed;
+  return p;
+}
+
+int launch(bsg_ctx* c, const bsg::KParams& p, void* stream) {
+  hipError_t e = hipSetDevice(c->cfg.device);
+  if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  hipEvent_t t0 = nullptr, t1 = nullptr;
+  if (c->timing) {
+    t0 = take_event(c);
+    t1 = take_event(c);
+    if (!t0 || !t1) return fail(BSG_E_HIP, "hipEventCreate failed%s%lld");
+    if ((e = hipEventRecord(t0, st)) != hipSuccess) return hip_fail(e, "hipEventRecord");
+  }
+  e = bsg::launch_step(p, st);
+  if (e != hipSuccess) return hip_fail(e, "kernel launch");
+  if (c->timing) {
+    if ((e = hipEventRecord(t1, st)) != hipSuccess) return hip_fail(e, "hipEventRecord");
+    c->pending.emplace_back(t0, t1);
+  }
+  return BSG_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int32_t bsg_abi_version(void) { return BSG_ABI_VERSION; }
+
+const char* bsg_last_error(void) { return g_err.c_str(); }
+
+int32_t bsg_obs_dim(int32_t kind, int32_t num_ac, int32_t k) {
+  switch (kind) {
+    case BSG_ENV_MERGE: return (num_ac >= 2 && k >= 1 && k <= num_ac - 1) ? 5 + 7 * k : BSG_E_INVALID_ARG;
+    case BSG_ENV_VERTICAL_CR: return num_ac >= 2 ? 4 + 7 * (num_ac - 1) : BSG_E_INVALID_ARG;
+    case BSG_ENV_DESCENT: return num_ac == 1 ? 4 : BSG_E_INVALID_ARG;
+    default: return BSG_E_INVALID_ARG;
+  }
+}
+
+int32_t bsg_action_dim(int32_t kind) {
+  switch (kind) {
+    case BSG_ENV_MERGE: return 2;
+    case BSG_ENV_VERTICAL_CR:
+    case BSG_ENV_DESCENT: return 1;
+    default: return BSG_E_INVALID_ARG;
+  }
+}
+
+int32_t bsg_spawn_width(int32_t kind, int32_t num_ac) {
+  switch (kind) {
+    case BSG_ENV_MERGE: return 2 * num_ac;
+    case BSG_ENV_VERTICAL_CR: return 2 + 4 * (num_ac - 1);
+    case BSG_ENV_DESCENT: return 2;
+    default: return BSG_E_INVALID_ARG;
+  }
+}
+
+int32_t bsg_create(const bsg_config* cfg, bsg_ctx** out) {
+  if (!cfg || !out) return fail(BSG_E_INVALID_ARG, "bsg_create: null argument%s%lld");
+  *out = nullptr;
+  if (cfg->abi_version != BSG_ABI_VERSION)
+    return fail(BSG_E_INVALID_ARG, "bsg_create: abi_version mismatch%s (got %lld)", "",
+                cfg->abi_version);
+  if (cfg->num_envs <= 0) return fail(BSG_E_INVALID_ARG, "bsg_create: num_envs must be > 0%s%lld");
+  if (cfg->num_ac < 1 || cfg->num_ac > BSG_MAX_AC)
+    return fail(BSG_E_INVALID_ARG, "bsg_create: num_ac must be in [1, 64]%s (got %lld)", "", cfg->num_ac);
+  const int od = bsg_obs_dim(cfg->env_kind, cfg->num_ac, cfg->num_ac_state);
+  if (od < 0) return fail(BSG_E_INVALID_ARG, "bsg_create: invalid env_kind/num_ac/num_ac_state%s%lld");
+  if (cfg->action_frequency < 0) return fail(BSG_E_INVALID_ARG, "bsg_create: action_frequency < 0%s%lld");
+  if (!(cfg->simdt > 0.0)) return fail(BSG_E_INVALID_ARG, "bsg_create: simdt must be > 0%s%lld");
+  if (cfg->autoreset_mode < 0 || cfg->autoreset_mode > 2)
+    return fail(BSG_E_INVALID_ARG, "bsg_create: invalid autoreset_mode%s%lld");
+  if (cfg->route_len < 0 || cfg->route_len > BSG_MAX_ROUTE)
+    return fail(BSG_E_INVALID_ARG, "bsg_create: route_len out of range%s%lld");
+  if (cfg->env_kind == BSG_ENV_MERGE && cfg->route_len < 1)
+    return fail(BSG_E_INVALID_ARG, "bsg_create: Merge needs the FIX/RWY route%s%lld");
+  int ndev = 0;
+  hipError_t e = hipGetDeviceCount(&ndev);
+  if (e != hipSuccess) return hip_fail(e, "hipGetDeviceCount");
+  if (cfg->device < 0 || cfg->device >= ndev)
+    return fail(BSG_E_INVALID_ARG, "bsg_create: device ordinal out of range%s (%lld)", "", cfg->device);
+  bsg_ctx* c = new (std::nothrow) bsg_ctx();
+  if (!c) return fail(BSG_E_STATE, "bsg_create: out of host memory%s%lld");
+  c->cfg = *cfg;
+  c->obs_dim = od;
+  c->spawn_width = bsg_spawn_width(cfg->env_kind, cfg->num_ac);
+  c->route.len = cfg->route_len;
+  for (int k = 0; k < BSG_MAX_ROUTE; ++k) {
+    c->route.lat[k] = cfg->route_lat[k];
+    c->route.lon[k] = cfg->route_lon[k];
+    c->route.next_qdr[k] = cfg->route_next_qdr[k];
+  }
+  *out = c;
+  return BSG_OK;
+}
+
+int32_t bsg_destroy(bsg_ctx* c) {
+  if (!c) return BSG_OK;
+  for (auto& pr : c->pending) {
+    (void)hipEventDestroy(pr.first);
+    (void)hipEventDestroy(pr.second);
+  }
+  for (auto ev : c->ev_pool) (void)hipEventDestroy(ev);
+  delete c;
+  return BSG_OK;
+}
+
+int32_t bsg_bind(bsg_ctx* c, const bsg_buffers* b) {
+  if (!c || !b) return fail(BSG_E_INVALID_ARG, "bsg_bind: null argument%s%lld");
+  const void* required[] = {b->lat, b->lon, b->alt, b->hdg, b->tas, b->cas, b->vs, b->ax,
+                            b->ap_trk, b->selspd, b->selalt, b->selvs, b->nav,
+                            b->step_count, b->flags, b->episode, b->wpt_reach, b->faf_reached,
+                            b->total_intrusions, b->total_reward, b->drift_sum, b->target_alt,
+                            b->final_altitude, b->obs, b->reward, b->terminated, b->truncated};
+  for (size_t i = 0; i < sizeof(required) / sizeof(required[0]); ++i)
+    if (!required[i]) return fail(BSG_E_INVALID_ARG, "bsg_bind: required buffer #%s%lld is NULL", "", (long long)i);
+  if (c->cfg.env_kind == BSG_ENV_MERGE && !b->topk)
+    return fail(BSG_E_INVALID_ARG, "bsg_bind: Merge needs topk%s%lld");
+  if (c->cfg.autoreset_mode == BSG_AUTORESET_SAME_STEP && !b->final_obs)
+    return fail(BSG_E_INVALID_ARG, "bsg_bind: SAME_STEP autoreset needs final_obs%s%lld");
+  if (c->cfg.compute_cd && c->cfg.env_kind != BSG_ENV_DESCENT &&
+      (!b->conf_mask || !b->los_mask || !b->tcpamax || !b->min_sep))
+    return fail(BSG_E_INVALID_ARG, "bsg_bind: compute_cd needs conf_mask/los_mask/tcpamax/min_sep%s%lld");
+  c->bufs = *b;
+  c->bound = true;
+  return BSG_OK;
+}
+
+int32_t bsg_reset(bsg_ctx* c, const uint8_t* env_mask, const double* spawn, void* stream) {
+  if (!c) return fail(BSG_E_INVALID_ARG, "bsg_reset: null ctx%s%lld");
+  if (!c->bound) return fail(BSG_E_STATE, "bsg_reset: buffers not bound%s%lld");
+  bsg::KParams p = make_params(c, bsg::MODE_RESET);
+  p.env_mask = env_mask;
+  p.spawn = spawn;
+  return launch(c, p, stream);
+}
+
+int32_t bsg_step(bsg_ctx* c, const double* actions, const double* spawn, void* stream) {
+  if (!c) return fail(BSG_E_INVALID_ARG, "bsg_step: null ctx%s%lld");
+  if (!c->bound) return fail(BSG_E_STATE, "bsg_step: buffers not bound%s%lld");
+  if (!actions) return fail(BSG_E_INVALID_ARG, "bsg_step: actions is NULL%s%lld");
+  bsg::KParams p = make_params(c, bsg::MODE_STEP);
+  p.actions = actions;
+  p.spawn = spawn;
+  return launch(c, p, stream);
+}
+
+int32_t bsg_set_timing(bsg_ctx* c, int32_t enable) {
+  if (!c) return fail(BSG_E_INVALID_ARG, "bsg_set_timing: null ctx%s%lld");
+  c->timing = enable != 0;
+  return BSG_OK;
+}
+
+int32_t bsg_step_timing(bsg_ctx* c, double* total_ms, int32_t* launches) {
+  if (!c || !total_ms || !launches) return fail(BSG_E_INVALID_ARG, "bsg_step_timing: null argument%s%lld");
+  double tot = 0.0;
+  int n = 0;
+  for (auto& pr : c->pending) {
+    hipError_t e = hipEventSynchronize(pr.second);
+    if (e != hipSuccess) return hip_fail(e, "hipEventSynchronize");
+    float ms = 0.f;
+    e = hipEventElapsedTime(&ms, pr.first, pr.second);
+    if (e != hipSuccess) return hip_fail(e, "hipEventElapsedTime");
+    tot += ms;
+    ++n;
+    c->ev_pool.push_back(pr.first);
+    c->ev_pool.push_back(pr.second);
+  }
+  c->pending.clear();
+  *total_ms = tot;
+  *launches = n;
+  return BSG_OK;
+}
+
+}  // extern "C"

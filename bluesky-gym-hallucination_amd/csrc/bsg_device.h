@@ -1,0 +1,246 @@
+// bsg_device.h -- fp64 device math of the BlueSky subset for gfx950.
+//
+// Every function restates, in the same IEEE operation order, the NumPy code of
+// oracle/bluesky_subset.py (itself a restatement of bluesky-simulator 1.0.3:
+// bluesky/tools/aero.py, bluesky/tools/geo.py, bluesky/traffic/*.py; frozen in
+// docs/BLUESKY_SUBSET_SPEC.md).  Build with -ffp-contract=off: NumPy never fuses a
+// multiply-add, so neither may we.  Transcendentals come from the device libm (ocml);
+// they may differ from NumPy's by an ulp, which is why fp outputs are compared with a
+// tolerance while every boolean/index output is compared bit for bit.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace bsg {
+
+// ---- constants (bluesky.tools.aero; oracle/bluesky_subset.py) -----------------------
+constexpr double kPi = 3.141592653589793238462643383279502884;
+constexpr double kD2R = kPi / 180.0;   // np.radians / np.deg2rad multiply by this
+constexpr double kR2D = 180.0 / kPi;   // np.degrees
+constexpr double Rearth = 6371000.0;
+constexpr double NM = 1852.0;
+constexpr double FT = 0.3048;
+constexpr double KTS = 0.514444;
+constexpr double FPM = 0.00508;
+constexpr double G0 = 9.80665;
+constexpr double RGAS = 287.05287;
+constexpr double GAMMA = 1.40;
+constexpr double P0 = 101325.0;
+constexpr double RHO0 = 1.225;
+constexpr double TSTRAT = 216.65;
+
+// frozen A320 envelope / autopilot defaults (docs/BLUESKY_SUBSET_SPEC.md §A.3)
+constexpr double TAN_BANKDEF = 0.4663076581549986;    // tan(radians(25)), frozen literal
+constexpr double APVSDEF = 1500.0 * FPM;
+constexpr double EPS_SPD = 0.01;
+constexpr double AXMAX = 0.5;
+constexpr double VMIN_CAS = 140.0 * KTS;
+constexpr double VMAX_CAS = 350.0 * KTS;
+constexpr double MMO = 0.82;
+constexpr double HMAX = 39800.0 * FT;
+constexpr double VSMAX = 4000.0 * FPM;
+constexpr double VSMIN = -4000.0 * FPM;
+constexpr double RPZ = 5.0 * NM;
+constexpr double HPZ = 1000.0 * FT;
+constexpr double DTLOOKAHEAD = 300.0;
+
+__device__ __forceinline__ double sgn(double x) { return (double)((x > 0.0) - (x < 0.0)); }
+
+// np.remainder / Python float % (numpy npy_divmod): fmod, then move toward b's sign.
+__device__ __forceinline__ double pymod(double a, double b) {
+  double mod = fmod(a, b);
+  if (mod != 0.0) {
+    if ((b < 0.0) != (mod < 0.0)) mod += b;
+  } else {
+    mod = copysign(0.0, b);
+  }
+  return mod;
+}
+
+// np.maximum / np.minimum on finite inputs
+__device__ __forceinline__ double npmax(double a, double b) { return (a >= b || a != a) ? a : b; }
+__device__ __forceinline__ double npmin(double a, double b) { return (a <= b || a != a) ? a : b; }
+
+__device__ __forceinline__ double degto180(double a) { return pymod(a + 180.0, 360.0) - 180.0; }
+
+// functions.py:4-22 bound_angle_positive_negative_180 (single wrap)
+__device__ __forceinline__ double bound180(double a) {
+  return a > 180.0 ? -(360.0 - a) : (a < -180.0 ? 360.0 + a : a);
+}
+
+// ---- aero -----------------------------------------------------------------------
+struct Atmos { double p, rho, T; };
+
+__device__ __forceinline__ Atmos vatmos(double h) {
+  Atmos a;
+  a.T = npmax(288.15 - 0.0065 * h, TSTRAT);
+  double rhotrop = 1.225 * pow(a.T / 288.15, 4.256848030018761);
+  double dhstrat = npmax(0.0, h - 11000.0);
+  a.rho = rhotrop * exp(-dhstrat / 6341.552161);
+  a.p = a.rho * RGAS * a.T;
+  return a;
+}
+
+__device__ __forceinline__ double tas2cas_at(double tas, const Atmos& a) {
+  double qdyn = a.p * (pow(1.0 + a.rho * tas * tas / (7.0 * a.p), 3.5) - 1.0);
+  double cas = sqrt(7.0 * P0 / RHO0 * (pow(qdyn / P0 + 1.0, 2.0 / 7.0) - 1.0));
+  return tas < 0 ? -1 * cas : cas;
+}
+
+__device__ __forceinline__ double cas2tas_at(double cas, const Atmos& a) {
+  double qdyn = P0 * (pow(1.0 + RHO0 * cas * cas / (7.0 * P0), 3.5) - 1.0);
+  double tas = sqrt(7.0 * a.p / a.rho * (pow(1.0 + qdyn / a.p, 2.0 / 7.0) - 1.0));
+  return cas < 0 ? -1 * tas : tas;
+}
+
+__device__ __forceinline__ double sound_at(const Atmos& a) { return sqrt(GAMMA * RGAS * a.T); }
+
+// vcasormach2tas: |spd| < 2 -> Mach, else CAS
+__device__ __forceinline__ double casormach2tas_at(double spd, const Atmos& a) {
+  return fabs(spd) < 2.0 ? spd * sound_at(a) : cas2tas_at(spd, a);
+}
+
+// vcasormach (Traffic.cre): returns tas, cas
+__device__ __forceinline__ void casormach_at(double spd, const Atmos& a, double* tas, double* cas) {
+  bool ismach = (0.1 < spd) && (spd < 2.0);
+  if (ismach) {
+    *tas = spd * sound_at(a);
+    *cas = tas2cas_at(*tas, a);
+  } else {
+    *tas = cas2tas_at(spd, a);
+    *cas = spd;
+  }
+}
+
+// ---- geo ---------------------------------------------------------------------------
+// kwikqdrdist (qdr in [0,360), dist NM)
+__device__ __forceinline__ void kwikqdrdist(double lata, double lona, double latb, double lonb,
+                                            double* qdr, double* dist) {
+  double dlat = (latb - lata) * kD2R;
+  double dlon = (pymod((lonb - lona) + 180.0, 360.0) - 180.0) * kD2R;
+  double cavelat = cos(((lata + latb) * kD2R) * 0.5);
+  double dangle = sqrt(dlat * dlat + dlon * dlon * cavelat * cavelat);
+  *dist = 6371000.0 * dangle / NM;
+  *qdr = pymod(atan2(dlon * cavelat, dlat) * kR2D, 360.0);
+}
+
+__device__ __forceinline__ double kwikdist(double lata, double lona, double latb, double lonb) {
+  double dlat = (latb - lata) * kD2R;
+  double dlon = (pymod((lonb - lona) + 180.0, 360.0) - 180.0) * kD2R;
+  double cavelat = cos(((lata + latb) * kD2R) * 0.5);
+  double dangle = sqrt(dlat * dlat + dlon * dlon * cavelat * cavelat);
+  return 6371000.0 * dangle / NM;
+}
+
+// kwikdist_matrix element (operation order of the matrix form, merge_env.py:195)
+__device__ __forceinline__ double kwikdist_mat(double lata, double lona, double latb, double lonb) {
+  double dlat = (latb - lata) * kD2R;
+  double dlon = (pymod((lonb - lona) + 180.0, 360.0) - 180.0) * kD2R;
+  double cavelat = cos(((latb + lata) * kD2R) * 0.5);
+  double dangle = sqrt(dlat * dlat + (dlon * dlon) * (cavelat * cavelat));
+  return 6371000.0 * dangle / NM;
+}
+
+// kwikqdrdist_matrix element (StateBased.detect), [i][j] = from a=i to b=j
+__device__ __forceinline__ void kwikqdrdist_mat(double lata, double lona, double latb, double lonb,
+                                                double* qdr, double* dist) {
+  double dlat = (latb - lata) * kD2R;
+  double dlon = (pymod((lonb - lona) + 180.0, 360.0) - 180.0) * kD2R;
+  double cavelat = cos(((lata + latb) * kD2R) * 0.5);
+  double dangle = sqrt(dlat * dlat + (dlon * dlon) * (cavelat * cavelat));
+  *dist = 6371000.0 * dangle / NM;
+  *qdr = pymod(atan2(dlon * cavelat, dlat) * kR2D, 360.0);
+}
+
+__device__ __forceinline__ void kwikpos(double latd1, double lond1, double qdr, double dist,
+                                        double* lat2, double* lon2) {
+  double dx = dist * sin(qdr * kD2R);
+  double dy = dist * cos(qdr * kD2R);
+  double dlat = dy / 60.0;
+  double dlon = dx / npmax(0.01, 60.0 * cos(latd1 * kD2R));
+  *lat2 = latd1 + dlat;
+  *lon2 = pymod((lond1 + dlon) + 180.0, 360.0) - 180.0;
+}
+
+__device__ __forceinline__ double rwgs84(double latd) {
+  double lat = latd * kD2R;
+  const double a = 6378137.0;
+  const double b = 6356752.314245;
+  double coslat = cos(lat);
+  double sinlat = sin(lat);
+  double an = a * a * coslat;
+  double bn = b * b * sinlat;
+  double ad = a * coslat;
+  double bd = b * sinlat;
+  return sqrt((an * an + bn * bn) / (ad * ad + bd * bd));
+}
+
+// geo.qdrdist (WGS84): qdr in (-180,180], dist NM
+__device__ __forceinline__ void qdrdist(double latd1, double lond1, double latd2, double lond2,
+                                        double* qdr, double* distnm) {
+  bool sw = (latd1 * latd2 >= 0.0);
+  double r;
+  if (sw) {
+    r = rwgs84(0.5 * (latd1 + latd2));
+  } else {
+    const double a = 6378137.0;
+    double r1 = rwgs84(latd1);
+    double r2 = rwgs84(latd2);
+    r = 0.5 * (fabs(latd1) * (r1 + a) + fabs(latd2) * (r2 + a)) /
+        npmax(0.000001, fabs(latd1) + fabs(latd2));
+  }
+  double lat1 = latd1 * kD2R, lon1 = lond1 * kD2R;
+  double lat2 = latd2 * kD2R, lon2 = lond2 * kD2R;
+  double coslat1 = cos(lat1), coslat2 = cos(lat2);
+  double sinlat1 = sin(lat1), sinlat2 = sin(lat2);
+  double cosdlon = cos(lon2 - lon1);
+  double d = r * acos(coslat1 * coslat2 * cosdlon + sinlat1 * sinlat2);
+  *qdr = atan2(sin(lon2 - lon1) * coslat2, coslat1 * sinlat2 - sinlat1 * coslat2 * cosdlon) * kR2D;
+  *distnm = d / NM;
+}
+
+// functions.py:24-42 get_point_at_distance (R = 6371 km)
+__device__ __forceinline__ void get_point_at_distance(double lat1d, double lon1d, double d,
+                                                      double bearing, double* lat2d, double* lon2d) {
+  const double R = 6371.0;
+  double lat1 = lat1d * kD2R;
+  double lon1 = lon1d * kD2R;
+  double a = bearing * kD2R;
+  double lat2 = asin(sin(lat1) * cos(d / R) + cos(lat1) * sin(d / R) * cos(a));
+  double lon2 = lon1 + atan2(sin(a) * sin(d / R) * cos(lat1), cos(d / R) - sin(lat1) * sin(lat2));
+  *lat2d = lat2 * kR2D;
+  *lon2d = lon2 * kR2D;
+}
+
+// ---- Philox4x32-10 (oracle/philox.py) ---------------------------------------------------
+struct U4 { uint32_t x, y, z, w; };
+
+__device__ __forceinline__ U4 philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
+                                            uint64_t seed) {
+  uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
+    uint32_t hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
+    uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+    c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+    k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+  }
+  return U4{c0, c1, c2, c3};
+}
+
+__device__ __forceinline__ double u01_53(uint32_t lo, uint32_t hi) {
+  uint64_t x = ((uint64_t)hi << 32) | lo;
+  return (double)(x >> 11) * (1.0 / 9007199254740992.0);
+}
+
+__device__ __forceinline__ int64_t randint_u32(uint32_t x, int64_t lo, int64_t hi) {
+  return lo + (((int64_t)x * (hi - lo)) >> 32);
+}
+
+constexpr uint32_t TAG_MERGE = 0x4D455247u;
+constexpr uint32_t TAG_VERT = 0x56455254u;
+constexpr uint32_t TAG_DESC = 0x44455343u;
+
+}  // namespace bsg

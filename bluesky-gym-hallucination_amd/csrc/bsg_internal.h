@@ -1,0 +1,34 @@
+// bsg_internal.h -- launch parameters shared by the C ABI (bsg_abi.cpp) and the kernels.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "../../include/bsg.h"
+
+namespace bsg {
+
+using Buffers = bsg_buffers;
+
+enum { MODE_STEP = 0, MODE_RESET = 1 };
+
+struct Route {
+  int len;
+  double lat[BSG_MAX_ROUTE], lon[BSG_MAX_ROUTE], next_qdr[BSG_MAX_ROUTE];
+};
+
+// Passed by value to every launch (kernarg segment).
+struct KParams {
+  bsg_config cfg;
+  Route route;
+  Buffers b;
+  int mode;
+  int E, N, K, obs_dim, spawn_width;
+  uint64_t seed;
+  const double* actions;     // [E, A]
+  const double* spawn;       // [E, spawn_width] or nullptr (Philox)
+  const uint8_t* env_mask;   // [E] or nullptr (all)  -- reset mode only
+};
+
+hipError_t launch_step(const KParams& p, hipStream_t stream);
+
+}  // namespace bsg

@@ -1,0 +1,160 @@
+/*
+ * bsg.h -- C ABI of libbsg.so, the MI355X-native vectorised BlueSky-Gym step path.
+ *
+ * Drop-in boundary: the reference exposes one Gymnasium env per process
+ * (bluesky_gym/envs/merge_env.py:48, vertical_cr_env.py:47, descent_env.py:32) whose
+ * reset()/step() drive a process-global BlueSky singleton.  This library replaces that
+ * pair with a device-resident structure-of-arrays batch of E envs, stepped by one HIP
+ * launch per RL step.  The Python host mirror (bluesky_gym/_native.py, ctypes) binds
+ * exactly these symbols; INTEGRATION.md shows the binding.
+ *
+ * Conventions
+ *   - Caller owns ALL memory.  Every pointer in bsg_buffers is a device pointer
+ *     (hipMalloc / torch.cuda tensor).  The library stores them non-owning.
+ *   - All launches are asynchronous on the caller's stream (hipStream_t passed as void*);
+ *     no call synchronises the device.
+ *   - Return 0 on success, a negative BSG_E_* code otherwise; bsg_last_error() gives the
+ *     thread-local message.  No C++ exception crosses the ABI.
+ *   - Aircraft arrays are [num_envs][num_ac] row-major (env-major); aircraft 0 of each
+ *     env is the ownship ('KL001'), 1..num_ac-1 the intruders ('INT{i}' / creconfs).
+ */
+#ifndef BSG_H_
+#define BSG_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BSG_ABI_VERSION 1
+#define BSG_MAX_AC 64          /* aircraft per env (one wavefront) */
+#define BSG_MAX_ROUTE 4
+
+enum {
+  BSG_OK = 0,
+  BSG_E_INVALID_ARG = -1,
+  BSG_E_HIP = -2,
+  BSG_E_STATE = -3,
+  BSG_E_UNSUPPORTED = -4
+};
+
+enum { BSG_ENV_MERGE = 0, BSG_ENV_VERTICAL_CR = 1, BSG_ENV_DESCENT = 2 };
+
+/* Vector-env autoreset conventions:
+ *   NEXT_STEP: Gymnasium >= 1.0 VectorEnv default -- the step AFTER a done step resets
+ *              the env (action ignored, reward 0, terminated/truncated false).
+ *   SAME_STEP: SB3 VecEnv -- a done env is reset inside the same step; the terminal
+ *              observation is written to final_obs, obs holds the reset observation. */
+enum { BSG_AUTORESET_NONE = 0, BSG_AUTORESET_NEXT_STEP = 1, BSG_AUTORESET_SAME_STEP = 2 };
+
+typedef struct bsg_config {
+  int32_t abi_version;       /* = BSG_ABI_VERSION */
+  int32_t env_kind;          /* BSG_ENV_* */
+  int32_t num_envs;          /* E */
+  int32_t num_ac;            /* N aircraft per env incl. ownship (merge_env.py:37 NUM_AC;
+                                vertical: 1 + NUM_INTRUDERS, vertical_cr_env.py:45; descent: 1) */
+  int32_t num_ac_state;      /* K nearest intruders in the Merge obs (merge_env.py:38) */
+  int32_t action_frequency;  /* substeps per RL step (merge_env.py:35; vertical_cr_env.py:43) */
+  double simdt;              /* s per substep ('DT 5' merge_env.py:86; 'DT 1' vertical_cr_env.py:95) */
+  int32_t max_episode_steps; /* TimeLimit (bluesky_gym/__init__.py:9,27,45); 0 = none */
+  int32_t autoreset_mode;    /* BSG_AUTORESET_* */
+  int32_t compute_cd;        /* 1: StateBased all-pairs CPA outputs every step */
+  int32_t device;            /* HIP device ordinal */
+  uint64_t seed;             /* Philox key for device-side spawns */
+  int32_t route_len;         /* Merge intruder route (ADDWPT FIX; DEST RWY, merge_env.py:155-156) */
+  int32_t _pad0;
+  double route_lat[BSG_MAX_ROUTE];
+  double route_lon[BSG_MAX_ROUTE];
+  double route_next_qdr[BSG_MAX_ROUTE]; /* qdrdist bearing wp k -> k+1; -999 for the last */
+  double wpt_lat[2];         /* Merge drift targets: FIX, RWY (merge_env.py:98-101) */
+  double wpt_lon[2];
+} bsg_config;
+
+typedef struct bsg_buffers {
+  /* ---- aircraft state, fp64 [E*N] (bs.traf.* arrays) ---------------------------- */
+  double *lat, *lon, *alt, *hdg, *tas, *cas, *vs, *ax;
+  double *ap_trk, *selspd, *selalt, *selvs;   /* autopilot targets */
+  int32_t *nav;                               /* bit0 swlnav, bits 8..15 active waypoint */
+  /* ---- per-env state [E] ----------------------------------------------------------- */
+  int32_t *step_count;       /* TimeLimit elapsed steps */
+  int32_t *flags;            /* bit0: reset pending (NEXT_STEP autoreset) */
+  uint32_t *episode;         /* episode counter (Philox counter word) */
+  int32_t *wpt_reach;        /* merge_env.py:97 */
+  int32_t *faf_reached;      /* merge_env.py:92 (info faf_reach) */
+  int32_t *total_intrusions; /* info */
+  double *total_reward;      /* info */
+  double *drift_sum;         /* info average_drift numerator (count = step_count) */
+  double *target_alt;        /* vertical/descent target altitude (m) */
+  double *final_altitude;    /* vertical/descent info */
+  /* ---- outputs --------------------------------------------------------------------- */
+  float *obs;                /* [E, obs_dim] sorted-key flatten (gymnasium spaces.Dict order) */
+  float *final_obs;          /* [E, obs_dim] terminal obs (SAME_STEP only; else may be NULL) */
+  float *reward;             /* [E] */
+  uint8_t *terminated;       /* [E] */
+  uint8_t *truncated;        /* [E] */
+  int32_t *topk;             /* [E, K] aircraft index of the K nearest intruders (Merge) */
+  uint64_t *intr_mask;       /* [E] bit i: ownship-aircraft i intrusion this step */
+  uint64_t *conf_mask;       /* [E, N] StateBased swconfl, bit j of row i (compute_cd) */
+  uint64_t *los_mask;        /* [E, N] StateBased swlos, bit j of row i (compute_cd) */
+  float *tcpamax;            /* [E, N] StateBased tcpamax (compute_cd) */
+  float *min_sep;            /* [E] min pairwise horizontal distance, m (compute_cd) */
+  double *ep_info;           /* [E, 4] written when an episode ends: total_reward,
+                                total_intrusions, faf_reach | final_altitude,
+                                average_drift (Merge) -- the info dict at done
+                                (merge_env.py:238-244, vertical_cr_env.py:203-211) */
+} bsg_buffers;
+
+typedef struct bsg_ctx bsg_ctx;
+
+/* ABI version of the loaded library. */
+int32_t bsg_abi_version(void);
+
+/* Thread-local message of the last failing call ("" if none). */
+const char* bsg_last_error(void);
+
+/* Flat observation length for an env kind (sum of the Box sizes of the reference
+ * observation_space: merge_env.py:59-74 -> 5+7K; vertical_cr_env.py:67-83 -> 4+7(N-1);
+ * descent_env.py:53-60 -> 4). Negative on invalid input. */
+int32_t bsg_obs_dim(int32_t env_kind, int32_t num_ac, int32_t num_ac_state);
+
+/* Action width (merge_env.py:76 -> 2; vertical_cr_env.py:85 / descent_env.py:62 -> 1). */
+int32_t bsg_action_dim(int32_t env_kind);
+
+/* Doubles per env of host-supplied spawn parameters for bsg_reset / bsg_step:
+ *   Merge    [2N]      : (bearing deg, distance km) for aircraft 0..N-1, the
+ *                        random.uniform draws of merge_env.py:115-116,150-151
+ *   Vertical [2+4(N-1)]: alt_init, target_alt, then (dpsi, cpa, tlosh, dH) per intruder,
+ *                        the np.random draws of vertical_cr_env.py:188-195,267-268
+ *   Descent  [2]       : alt_init, target_alt (descent_env.py:170-171) */
+int32_t bsg_spawn_width(int32_t env_kind, int32_t num_ac);
+
+/* Replaces: gym.make(id) -> Env.__init__ (merge_env.py:54-101): validates the config
+ * and binds a device.  No device memory is allocated. */
+int32_t bsg_create(const bsg_config* cfg, bsg_ctx** out);
+int32_t bsg_destroy(bsg_ctx* ctx);
+
+/* Attach the caller-owned device buffers (non-owning). */
+int32_t bsg_bind(bsg_ctx* ctx, const bsg_buffers* bufs);
+
+/* Replaces: Env.reset() (merge_env.py:103-130 + _gen_aircraft :148-158;
+ * vertical_cr_env.py:258-281 + _generate_conflicts :183-200; descent_env.py:162-182).
+ * env_mask: device u8 [E] (NULL = all envs).  spawn: device f64 [E, spawn_width]
+ * (NULL = Philox draw keyed by (seed, env, episode)).  Writes obs. */
+int32_t bsg_reset(bsg_ctx* ctx, const uint8_t* env_mask, const double* spawn, void* stream);
+
+/* Replaces: Env.step(action) + TimeLimit (merge_env.py:132-146; vertical_cr_env.py:283-305;
+ * descent_env.py:184-206).  actions: device f64 [E, action_dim].  spawn: optional
+ * device f64 [E, spawn_width] used by autoresets in this step (NULL = Philox). */
+int32_t bsg_step(bsg_ctx* ctx, const double* actions, const double* spawn, void* stream);
+
+/* Kernel-time instrumentation: record a HIP event pair around each step launch on the
+ * launch stream; bsg_last_step_ms() returns the elapsed time of the most recent
+ * completed pair (synchronises on that event only).  enable=0 turns it off. */
+int32_t bsg_set_timing(bsg_ctx* ctx, int32_t enable);
+int32_t bsg_step_timing(bsg_ctx* ctx, double* total_ms, int32_t* launches);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* BSG_H_ */

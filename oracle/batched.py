@@ -117,6 +117,7 @@ class _Base:
         self.needs_reset = np.zeros(self.E, bool)
         self.total_reward = np.zeros(self.E, np.float64)
         self.total_intrusions = np.zeros(self.E, np.int32)
+        self.env_ids = np.arange(self.E)     # global env ids (Philox counter word 0)
 
     # -------- spawn parameters (host-supplied = parity mode; None = device Philox) -----
     def device_spawn_params(self, env_ids, episodes):
@@ -131,8 +132,9 @@ class _Base:
             return self.observe()
         if spawn is None:
             spawn = np.zeros((self.E, self.spawn_width()), np.float64)
-            spawn[ids] = self.device_spawn_params(ids, self.episode[ids])
+            spawn[ids] = self.device_spawn_params(self.env_ids[ids], self.episode[ids])
         self._reset_ids(ids, np.asarray(spawn, np.float64))
+        self.episode[ids] += 1          # every reset consumes one Philox episode counter
         self.step_count[ids] = 0
         self.needs_reset[ids] = False
         self.total_reward[ids] = 0.0
@@ -173,12 +175,13 @@ class _Base:
         if was_reset.any():
             ro = self.reset(was_reset, spawn)
             obs[was_reset] = ro["obs"][was_reset]
+            if "cd" in res:
+                # a NEXT_STEP reset step reports conflict detection on the fresh state
+                self._cd_into(res, was_reset)
         if self.autoreset == AUTORESET_NEXT_STEP:
             self.needs_reset = done.copy()
-            self.episode[done] += 1
         elif self.autoreset == AUTORESET_SAME_STEP and done.any():
             final_obs = obs.copy()
-            self.episode[done] += 1
             ro = self.reset(done, spawn)
             obs[done] = ro["obs"][done]
         out = dict(res)
@@ -592,6 +595,17 @@ class DescentOracle(_VertBase):
     def info(self):
         return {"total_reward": self.total_reward.copy(),
                 "final_altitude": self.final_altitude.copy()}
+
+
+def _cd_fill(o, res, mask):
+    st = o.st
+    cd = bsx.statebased_detect(st.lat, st.lon, st.alt, st.hdg, st.tas, st.vs)
+    res["conf_mask"] = np.where(mask[:, None], _rows_to_u64(cd["swconfl"]), res["conf_mask"])
+    res["los_mask"] = np.where(mask[:, None], _rows_to_u64(cd["swlos"]), res["los_mask"])
+    res["tcpamax"] = np.where(mask[:, None], cd["tcpamax"], res["tcpamax"])
+
+
+_Base._cd_into = lambda self, res, mask: _cd_fill(self, res, mask)
 
 
 def _rows_to_u64(m):

@@ -52,6 +52,7 @@ Tstrat = 216.65         # K
 
 # Frozen A320 envelope and autopilot defaults (docs/BLUESKY_SUBSET_SPEC.md §A.3)
 BANKDEF = math.radians(25.0)          # ap.bankdef
+TAN_BANKDEF = 0.4663076581549986      # tan(BANKDEF), frozen literal shared with the device code
 APVSDEF = 1500.0 * fpm                # ap.apvsdef  (m/s)
 EPS_SPD = 0.01                        # traf.eps
 AXMAX = 0.5                           # perf.axmax  (m/s2), airborne
@@ -314,7 +315,7 @@ def traffic_update(st, dt, route_lat, route_lon, route_next_qdr):
         # ActiveWaypoint.reached: fly-by turn distance, or "too close and passing"
         nq = np.asarray(route_next_qdr)[np.clip(st.actwp, 0, nwp - 1)]
         next_qdr = np.where(nq < -900.0, qdr, nq)
-        turnrad = st.tas * st.tas / (np.maximum(0.01, np.tan(BANKDEF)) * g0)
+        turnrad = st.tas * st.tas / (np.maximum(0.01, TAN_BANKDEF) * g0)
         turndist = np.abs(turnrad * np.tan(np.radians(
             0.5 * np.abs(degto180(pymod(qdr, 360.0) - pymod(next_qdr, 360.0))))))
         close2wp = dist / (np.maximum(0.0001, np.abs(st.gs))) < 4.0
@@ -346,7 +347,7 @@ def traffic_update(st, dt, route_lat, route_lon, route_next_qdr):
     st.ax = need_ax * np.sign(delta_spd) * AXMAX
     st.tas = np.where(need_ax, st.tas + st.ax * dt, tas_cmd)
     st.cas = vtas2cas(st.tas, st.alt)
-    turnrate = np.degrees(g0 * np.tan(BANKDEF) / np.maximum(st.tas, EPS_SPD))
+    turnrate = np.degrees(g0 * TAN_BANKDEF / np.maximum(st.tas, EPS_SPD))
     delhdg = pymod(hdg_cmd - st.hdg + 180.0, 360.0) - 180.0
     swhdgsel = np.abs(delhdg) > np.abs(dt * turnrate)
     st.hdg = pymod(np.where(swhdgsel, st.hdg + dt * turnrate * np.sign(delhdg), hdg_cmd), 360.0)

@@ -1,0 +1,220 @@
+"""GPU parity: libbsg.so (HIP, gfx950) against the CPU oracle and the golden vectors.
+
+Bar (BASELINE.json north_star): bit-exact for booleans and indices (terminated,
+truncated, top-K intruder indices, intrusion masks, StateBased conflict / LoS masks);
+fp32 observations and rewards within |gpu - ref| <= 1e-5 + 1e-5 * |ref|.
+"""
+import numpy as np
+import pytest
+import torch
+
+import oracle_replay as rp
+from oracle import batched as ob
+
+pytestmark = pytest.mark.gpu
+
+ATOL = 1e-5
+RTOL = 1e-5
+GOLD = __import__("os").path.join(__import__("os").path.dirname(__file__), "golden")
+
+
+# tcpa of an exactly parallel, equal-speed pair is ill-conditioned: its relative velocity
+# is rounding noise (|dv| ~ 1e-13 m/s), StateBased floors dv2 at 1e-6 and tcpa becomes
+# noise of order |dv|*dist/1e-6 <= ~0.1 s (creconfs intruders with equal dpsi hit this).
+# The conflict / LoS masks of such pairs are robust and stay bit-exact.
+TCPA_ATOL = 0.1
+
+
+def close(a, b, what, atol=ATOL):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    err = np.abs(a - b) - (atol + RTOL * np.abs(b))
+    assert np.all(np.isfinite(a)), what + ": non-finite"
+    assert err.max(initial=-1) <= 0, f"{what}: max excess {err.max()} at {np.unravel_index(err.argmax(), err.shape)}"
+
+
+def bits(mask_u64, n):
+    m = np.asarray(mask_u64).astype(np.uint64)
+    return np.stack([(m >> np.uint64(i)) & np.uint64(1) for i in range(n)], -1).astype(np.int8)
+
+
+@pytest.fixture(scope="module")
+def bg():
+    from bluesky_gym import core, config, _native
+    return core, config, _native
+
+
+def load(name):
+    return dict(np.load(f"{GOLD}/{name}.npz"))
+
+
+@pytest.mark.parametrize("name", ["merge_N8", "merge_N16", "merge_N20", "merge_N32"])
+def test_merge_golden_on_gpu(bg, name):
+    core, config, nat = bg
+    g = load(name)
+    n_ep, T = g["actions"].shape[:2]
+    N = int(g["num_ac"])
+    b = core.DeviceBatch(config.merge_config(num_ac=N), n_ep, autoreset=nat.AUTORESET_NONE,
+                         compute_cd=True)
+    obs0 = b.reset(spawn=torch.from_numpy(g["spawn"])).cpu().numpy()
+    close(obs0, g["obs0"], "reset obs")
+    m = rp.step_mask(g)
+    act = torch.from_numpy(g["actions"]).cuda()
+    for t in range(T):
+        obs, rew, term, trunc = b.step(act[:, t])
+        live = m[:, t]
+        if not live.any():
+            break
+        close(obs.cpu().numpy()[live], g["obs"][live, t], f"obs t={t}")
+        close(rew.cpu().numpy()[live], g["reward"][live, t], f"reward t={t}")
+        assert np.array_equal(term.cpu().numpy()[live], g["terminated"][live, t].astype(np.uint8)), t
+        assert np.array_equal(trunc.cpu().numpy()[live], g["truncated"][live, t].astype(np.uint8)), t
+        assert np.array_equal(b.topk.cpu().numpy()[live], g["topk"][live, t]), t
+        ib = bits(b.intr_mask.cpu().numpy(), N)[:, 1:]
+        assert np.array_equal(ib[live], g["intr"][live, t]), t
+
+
+@pytest.mark.parametrize("name", ["vertical_N6", "vertical_N32"])
+def test_vertical_golden_on_gpu(bg, name):
+    core, config, nat = bg
+    g = load(name)
+    n_ep, T = g["actions"].shape[:2]
+    N = int(g["num_ac"])
+    b = core.DeviceBatch(config.vertical_config(num_intruders=N - 1), n_ep,
+                         autoreset=nat.AUTORESET_NONE, compute_cd=True)
+    obs0 = b.reset(spawn=torch.from_numpy(g["spawn"])).cpu().numpy()
+    close(obs0, g["obs0"], "reset obs")
+    m = rp.step_mask(g)
+    act = torch.from_numpy(g["actions"]).cuda()
+    for t in range(T):
+        obs, rew, term, trunc = b.step(act[:, t])
+        live = m[:, t]
+        if not live.any():
+            break
+        close(obs.cpu().numpy()[live], g["obs"][live, t], f"obs t={t}")
+        close(rew.cpu().numpy()[live], g["reward"][live, t], f"reward t={t}")
+        assert np.array_equal(term.cpu().numpy()[live], g["terminated"][live, t].astype(np.uint8)), t
+        nt = live & (g["terminated"][:, t] == 0)
+        ib = bits(b.intr_mask.cpu().numpy(), N)[:, 1:]
+        assert np.array_equal(ib[nt], g["intr"][nt, t]), t
+
+
+def test_descent_golden_on_gpu(bg):
+    core, config, nat = bg
+    g = load("descent")
+    n_ep, T = g["actions"].shape[:2]
+    b = core.DeviceBatch(config.descent_config(), n_ep, autoreset=nat.AUTORESET_NONE)
+    obs0 = b.reset(spawn=torch.from_numpy(g["spawn"])).cpu().numpy()
+    close(obs0, g["obs0"], "reset obs")
+    m = rp.step_mask(g)
+    act = torch.from_numpy(g["actions"]).cuda()
+    for t in range(T):
+        obs, rew, term, trunc = b.step(act[:, t])
+        live = m[:, t]
+        if not live.any():
+            break
+        close(obs.cpu().numpy()[live], g["obs"][live, t], f"obs t={t}")
+        close(rew.cpu().numpy()[live], g["reward"][live, t], f"reward t={t}")
+        assert np.array_equal(term.cpu().numpy()[live], g["terminated"][live, t].astype(np.uint8)), t
+
+
+def _compare_step(b, r, N, kind, t):
+    close(b.obs.cpu().numpy(), r["obs"], f"obs t={t}")
+    close(b.reward.cpu().numpy(), r["reward"], f"reward t={t}")
+    assert np.array_equal(b.terminated.cpu().numpy().astype(bool), r["terminated"]), t
+    assert np.array_equal(b.truncated.cpu().numpy().astype(bool), r["truncated"]), t
+    if kind != "descent":
+        live = ~r["was_reset"]
+        gi = b.intr_mask.cpu().numpy().astype(np.uint64)
+        assert np.array_equal(gi[live], r["intr_mask"][live]), t
+        assert np.array_equal(b.conf_mask.cpu().numpy().astype(np.uint64), r["conf_mask"]), t
+        assert np.array_equal(b.los_mask.cpu().numpy().astype(np.uint64), r["los_mask"]), t
+        close(b.tcpamax.cpu().numpy(), r["tcpamax"], f"tcpamax t={t}", atol=TCPA_ATOL)
+    if kind == "merge":
+        live = ~r["was_reset"]
+        assert np.array_equal(b.topk.cpu().numpy()[live], r["topk"][live]), t
+
+
+@pytest.mark.parametrize("autoreset", [ob.AUTORESET_NEXT_STEP, ob.AUTORESET_SAME_STEP])
+def test_merge_batch_autoreset_parity(bg, autoreset):
+    """256 envs x 32 aircraft, device Philox spawns, random actions, 120 steps (two full
+    TimeLimit episodes plus early terminations): every output vs the oracle."""
+    core, config, nat = bg
+    E, N, T = 256, 32, 120
+    seed = 1234
+    b = core.DeviceBatch(config.merge_config(num_ac=N), E, autoreset=autoreset,
+                         compute_cd=True, seed=seed)
+    o = ob.MergeOracle(E, num_ac=N, autoreset=autoreset, seed=seed, compute_cd=True)
+    close(b.reset().cpu().numpy(), o.reset()["obs"], "reset obs")
+    rng = np.random.default_rng(7)
+    for t in range(T):
+        a = rng.uniform(-1, 1, (E, 2))
+        b.step(torch.from_numpy(a))
+        r = o.step(a)
+        _compare_step(b, r, N, "merge", t)
+        if autoreset == ob.AUTORESET_SAME_STEP and r["final_obs"] is not None:
+            d = r["terminated"] | r["truncated"]
+            close(b.final_obs.cpu().numpy()[d], r["final_obs"][d], f"final_obs t={t}")
+
+
+@pytest.mark.parametrize("N", [6, 32])
+def test_vertical_batch_autoreset_parity(bg, N):
+    core, config, nat = bg
+    E, T = 128, 100
+    b = core.DeviceBatch(config.vertical_config(num_intruders=N - 1), E, compute_cd=True, seed=99)
+    o = ob.VerticalOracle(E, num_ac=N, seed=99, compute_cd=True)
+    close(b.reset().cpu().numpy(), o.reset()["obs"], "reset obs")
+    rng = np.random.default_rng(3)
+    for t in range(T):
+        a = rng.uniform(-1, 1, (E, 1))
+        b.step(torch.from_numpy(a))
+        r = o.step(a)
+        _compare_step(b, r, N, "vertical", t)
+
+
+def test_descent_batch_autoreset_parity(bg):
+    core, config, nat = bg
+    E, T = 512, 100
+    b = core.DeviceBatch(config.descent_config(), E, seed=5)
+    o = ob.DescentOracle(E, seed=5)
+    close(b.reset().cpu().numpy(), o.reset()["obs"], "reset obs")
+    rng = np.random.default_rng(11)
+    for t in range(T):
+        a = rng.uniform(-1, 1, (E, 1))
+        b.step(torch.from_numpy(a))
+        r = o.step(a)
+        _compare_step(b, r, 1, "descent", t)
+
+
+def test_merge_full_size_subset_parity(bg):
+    """BASELINE workload (4096 envs x 32 aircraft): run the full batch on the GPU and
+    check a strided subset of 64 envs against the oracle (envs are independent, so the
+    subset oracle with the same global env ids sees identical spawns)."""
+    core, config, nat = bg
+    E, N, T = 4096, 32, 60
+    b = core.DeviceBatch(config.merge_config(num_ac=N), E, compute_cd=True, seed=42)
+    ids = np.arange(0, E, 64)
+    o = ob.MergeOracle(len(ids), num_ac=N, seed=42, compute_cd=True)
+    o.env_ids = ids
+    close(b.reset().cpu().numpy()[ids], o.reset()["obs"], "reset obs")
+    rng = np.random.default_rng(1)
+    for t in range(T):
+        a = rng.uniform(-1, 1, (E, 2))
+        b.step(torch.from_numpy(a))
+        r = o.step(a[ids])
+        close(b.obs.cpu().numpy()[ids], r["obs"], f"obs t={t}")
+        assert np.array_equal(b.terminated.cpu().numpy()[ids].astype(bool), r["terminated"])
+        assert np.array_equal(b.conf_mask.cpu().numpy()[ids].astype(np.uint64), r["conf_mask"])
+    # size-independent properties over the whole batch
+    obs = b.obs.cpu().numpy()
+    assert np.isfinite(obs).all()
+    tk = b.topk.cpu().numpy()
+    assert ((tk >= 1) & (tk < N)).all()
+    assert all(len(set(row)) == tk.shape[1] for row in tk)
+    cm = b.conf_mask.cpu().numpy().astype(np.uint64)
+    diag = (cm >> np.arange(N, dtype=np.uint64)[None, :]) & np.uint64(1)
+    assert not diag.any()                                  # no self-conflicts
+    # StateBased conflicts are symmetric in exact arithmetic; fp rounding may break a
+    # near-threshold pair, so only require near-symmetry
+    bm = bits(cm, N)
+    assert (bm != bm.transpose(0, 2, 1)).sum() <= max(4, bm.sum() // 1000)
