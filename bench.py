@@ -1,0 +1,212 @@
+"""bench.py -- env steps/s of the MI355X-native BlueSky-Gym step path.
+
+Contract (driver): `python bench.py --gpus N --steps K --warmup W`; N>1 is launched with
+torch.distributed.run, one rank per GPU.  Rank 0 prints ONE JSON line.
+
+Workload (BASELINE.json metric): MergeEnv-v0, 32 aircraft per env, 4096 envs per GPU
+(weak scaling: env shards are independent), ACTION_FREQUENCY=10 substeps of DT=5 s,
+StateBased all-pairs CPA on every step, Gymnasium NEXT_STEP autoreset inside the timed
+region.  Spawns are drawn on the device (Philox); actions come from a bank of U(-1,1)
+batches resident in HBM before timing starts.  With N>1 every step also all-gathers the
+[E, obs+3] fp32 learner rows over RCCL (the north-star's learner hand-off).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [REPO, os.path.join(REPO, "bluesky-gym-hallucination_amd")]
+
+METRIC = "env steps/sec (whole node), MergeEnv-v0 4096 envs × 32 aircraft, 1/2/4/8 GPUs"
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md, chip table)
+
+
+def survey_bytes_per_env_step(N, A=2, O=40, K=5):
+    """SURVEY.md §8(d) algorithmic bytes per Merge env-step:
+    2*N*10*8 (6 kinematic + 4 autopilot fp64 fields, read+write) + 4A + 4O + 6
+    + ceil(N^2/8) (conflict bitmask) + ceil(N/8) (LoS bitmask) + 4K (top-K int32)."""
+    return 2 * N * 10 * 8 + 4 * A + 4 * O + 6 + -(-N * N // 8) + -(-N // 8) + 4 * K
+
+
+def layout_bytes_per_env_step(N, A=2, O=40, K=5, cd=True):
+    """Bytes this build's layout actually moves per env-step:
+    12 fp64 + 1 int32 per aircraft read+write, 56 B of env scalars read+write, fp64
+    actions, fp32 obs, reward/term/trunc, int32 top-K, u64 intrusion mask, and with CD
+    u64 conflict + LoS rows, fp32 tcpamax per aircraft and fp32 min separation."""
+    b = 2 * N * (12 * 8 + 4) + 2 * 56 + 8 * A + 4 * O + 6 + 4 * K + 8
+    if cd:
+        b += N * (8 + 8 + 4) + 4
+    return b
+
+
+def cpu_baseline(seconds: float):
+    """Time the CPU oracle (batched NumPy restatement, 1 core) on a bounded sample of
+    the same workload: 128 Merge envs x 32 aircraft, CD on, NEXT_STEP autoreset."""
+    import numpy as np
+    from oracle import batched as ob
+    E = 128
+    o = ob.MergeOracle(E, num_ac=32, seed=11, compute_cd=True)
+    o.reset()
+    rng = np.random.default_rng(0)
+    o.step(rng.uniform(-1, 1, (E, 2)))
+    n = 0
+    t0 = time.perf_counter()
+    while True:
+        o.step(rng.uniform(-1, 1, (E, 2)))
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= seconds and n >= 3:
+            break
+    model = platform.processor() or "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"value": E * n / el, "unit": "env_steps/s", "cores": 1, "kind": "port",
+            "sample": f"oracle/batched.py MergeOracle {E} envs x 32 aircraft, CD on, "
+                      f"{n} steps in {el:.1f} s, NumPy fp64 single thread on '{model}' "
+                      f"(host has {os.cpu_count()} logical CPUs)"}
+
+
+def load_traffic(E):
+    """Per-launch HBM bytes from the committed rocprofv3 PMC pass (tools/profile.sh)."""
+    p = os.path.join(REPO, "profiles", "traffic.json")
+    try:
+        with open(p) as f:
+            t = json.load(f)
+        if int(t.get("envs", -1)) == E:
+            return float(t["hbm_bytes_per_launch"])
+    except (OSError, ValueError, KeyError):
+        pass
+    return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--envs", type=int, default=4096, help="envs per GPU (weak scaling)")
+    ap.add_argument("--total-envs", type=int, default=0, help="strong scaling: total envs")
+    ap.add_argument("--num-ac", type=int, default=32)
+    ap.add_argument("--no-cd", action="store_true")
+    ap.add_argument("--no-gather", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--skip-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    from bluesky_gym import config, core
+    from bluesky_gym import _native as nat
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    E = args.envs if not args.total_envs else args.total_envs // world
+    gather = world > 1 and not args.no_gather
+    batch = core.DeviceBatch(config.merge_config(num_ac=args.num_ac), E,
+                             autoreset=nat.AUTORESET_NEXT_STEP, compute_cd=not args.no_cd,
+                             seed=1234 + 7919 * rank, learner=gather)
+    batch.reset()
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(17 + rank)
+    bank = torch.rand((16, E, 2), dtype=torch.float64, device=dev, generator=gen) * 2 - 1
+    if gather:
+        gathered = torch.empty((world * E, batch.obs_dim + 3), dtype=torch.float32, device=dev)
+
+    def one(k):
+        batch.step(bank[k % 16])
+        if gather:
+            dist.all_gather_into_tensor(gathered, batch.learner)
+
+    for k in range(args.warmup):
+        one(k)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    batch.step_timing()                       # discard
+    batch.set_timing(True)
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        one(k)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    batch.set_timing(False)
+    kern_ms, launches = batch.step_timing()
+    if world > 1:
+        t = torch.tensor([el, kern_ms / max(launches, 1)], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el, kern_avg_ms = float(t[0]), float(t[1])
+    else:
+        kern_avg_ms = kern_ms / max(launches, 1)
+
+    if rank == 0:
+        total = world * E * args.steps
+        value = total / el
+        N = args.num_ac
+        B = survey_bytes_per_env_step(N)
+        achieved = B * E / (kern_avg_ms * 1e-3) / 1e9
+        out = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "env_steps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": el * 1e3 / args.steps,
+            "higher_is_better": True,
+            "scaling": "strong" if args.total_envs else "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic: device Philox spawns (merge_env.py distributions), U(-1,1) actions",
+            "config": {
+                "workload": f"MergeEnv-v0 {E} envs x {N} aircraft per GPU, 10 substeps x DT 5 s, "
+                            f"StateBased CD {'off' if args.no_cd else 'on'}, NEXT_STEP autoreset"
+                            + (", RCCL all_gather of [E, obs+3] fp32 per step" if gather else ""),
+                "envs_per_gpu": E,
+                "num_ac": N,
+                "parallelism": f"env-shard x{world}" + (" + all_gather" if gather else ""),
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS,
+                "traffic": load_traffic(E),
+                "kernel": "bsg::step_kernel<MERGE,32>",
+                "kernel_avg_ms": kern_avg_ms,
+                "bytes_per_env_step": B,
+                "layout_bytes_per_env_step": layout_bytes_per_env_step(N, cd=not args.no_cd),
+            },
+        }
+        if world == 1 and not args.skip_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

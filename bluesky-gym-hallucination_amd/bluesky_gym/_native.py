@@ -63,6 +63,7 @@ BUFFER_FIELDS = [
     ("obs", _fp), ("final_obs", _fp), ("reward", _fp), ("terminated", _u8p),
     ("truncated", _u8p), ("topk", _i32p), ("intr_mask", _u64p), ("conf_mask", _u64p),
     ("los_mask", _u64p), ("tcpamax", _fp), ("min_sep", _fp), ("ep_info", _dp),
+    ("learner", _fp),
 ]
 
 

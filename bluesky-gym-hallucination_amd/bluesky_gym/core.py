@@ -19,7 +19,7 @@ F64_ENV = ("total_reward", "drift_sum", "target_alt", "final_altitude")
 
 class DeviceBatch:
     def __init__(self, cfg: EnvKindConfig, num_envs: int, *, autoreset=nat.AUTORESET_NEXT_STEP,
-                 compute_cd=True, seed=0, device=None):
+                 compute_cd=True, seed=0, device=None, learner=False):
         if not torch.cuda.is_available():
             raise nat.BsgError("bluesky_gym needs a HIP device (MI355X); none is visible")
         self.lib = nat.load_library()
@@ -30,6 +30,7 @@ class DeviceBatch:
         self.device = torch.device("cuda", torch.cuda.current_device() if device is None
                                    else torch.device(device).index or 0)
         self.autoreset = autoreset
+        self.want_learner = bool(learner)
         self.compute_cd = bool(compute_cd) and cfg.kind != nat.ENV_DESCENT
         self.obs_dim = self.lib.bsg_obs_dim(cfg.kind, cfg.num_ac, cfg.num_ac_state)
         if self.obs_dim < 0:
@@ -61,6 +62,8 @@ class DeviceBatch:
         self.topk = z((E, max(self.K, 1)), torch.int32) if self.cfg.kind == nat.ENV_MERGE else None
         self.intr_mask = z((E,), torch.int64)
         self.ep_info = z((E, 4), torch.float64)
+        # learner hand-off rows [obs, reward, terminated, truncated] (RCCL all-gather payload)
+        self.learner = z((E, self.obs_dim + 3), torch.float32) if self.want_learner else None
         if self.compute_cd:
             self.conf_mask = z((E, N), torch.int64)
             self.los_mask = z((E, N), torch.int64)
@@ -76,7 +79,8 @@ class DeviceBatch:
         src.update(obs=self.obs, final_obs=self.final_obs, reward=self.reward,
                    terminated=self.terminated, truncated=self.truncated, topk=self.topk,
                    intr_mask=self.intr_mask, conf_mask=self.conf_mask, los_mask=self.los_mask,
-                   tcpamax=self.tcpamax, min_sep=self.min_sep, ep_info=self.ep_info)
+                   tcpamax=self.tcpamax, min_sep=self.min_sep, ep_info=self.ep_info,
+                   learner=self.learner)
         for name, ptype in nat.BUFFER_FIELDS:
             t = src.get(name)
             setattr(b, name, C.cast(C.c_void_p(t.data_ptr()), ptype) if t is not None

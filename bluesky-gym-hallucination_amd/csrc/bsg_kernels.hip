@@ -537,9 +537,11 @@ __global__ __launch_bounds__(64) void step_kernel(KParams p) {
   if (active && ok) {
     float* obs = b.obs + (size_t)e * O;
     float* fobs = same_step_reset ? b.final_obs + (size_t)e * O : nullptr;
+    float* lrn = (b.learner && !same_step_reset) ? b.learner + (size_t)e * (O + 3) : nullptr;
     auto put = [&](int off, double v) {
       obs[off] = (float)v;
       if (fobs) fobs[off] = (float)v;
+      if (lrn) lrn[off] = (float)v;
     };
     if constexpr (KIND == BSG_ENV_MERGE) {
       const int K = p.K;
@@ -583,6 +585,12 @@ __global__ __launch_bounds__(64) void step_kernel(KParams p) {
       b.reward[e] = reward;
       b.terminated[e] = term ? 1 : 0;
       b.truncated[e] = trunc ? 1 : 0;
+      if (b.learner) {
+        float* row = b.learner + (size_t)e * (O + 3);
+        row[O] = reward;
+        row[O + 1] = term ? 1.0f : 0.0f;
+        row[O + 2] = trunc ? 1.0f : 0.0f;
+      }
       if (b.intr_mask) b.intr_mask[e] = ib;
       if (done && b.ep_info) {
         double* info = b.ep_info + (size_t)e * 4;
@@ -651,14 +659,19 @@ __global__ __launch_bounds__(64) void step_kernel(KParams p) {
     __syncthreads();
     if (same_step_reset && ok) {
       float* obs = b.obs + (size_t)e * O;
+      float* lrn = b.learner ? b.learner + (size_t)e * (O + 3) : nullptr;
+      auto put = [&](int off, double v) {
+        obs[off] = (float)v;
+        if (lrn) lrn[off] = (float)v;
+      };
       if constexpr (KIND == BSG_ENV_MERGE) {
         const int K = p.K;
         if (j == 0) {
           double wqdr, wdist;
           kwikqdrdist(s.lat, s.lon, p.cfg.wpt_lat[0], p.cfg.wpt_lon[0], &wqdr, &wdist);
           const double drift = bound180(s.hdg - wqdr);
-          obs[0] = (float)s.tas; obs[1] = (float)cos(drift * kD2R); obs[2 + 2 * K] = 0.0f;
-          obs[3 + 2 * K] = (float)sin(drift * kD2R); obs[4 + 5 * K] = (float)(wdist / 250);
+          put(0, s.tas); put(1, cos(drift * kD2R)); put(2 + 2 * K, 0.0);
+          put(3 + 2 * K, sin(drift * kD2R)); put(4 + 5 * K, wdist / 250);
         } else {
           const double dj = L.d[lane];
           int r = 0;
@@ -667,28 +680,28 @@ __global__ __launch_bounds__(64) void step_kernel(KParams p) {
             r += (dk < dj) || (dk == dj && k < j);
           }
           if (r < K) {
-            obs[2 + r] = (float)o4; obs[2 + K + r] = (float)(o6 / 250); obs[4 + 2 * K + r] = (float)o5;
-            obs[4 + 3 * K + r] = (float)(o2 / 150); obs[4 + 4 * K + r] = (float)(o3 / 150);
-            obs[5 + 5 * K + r] = (float)(o0 / 1000000); obs[5 + 6 * K + r] = (float)(o1 / 1000000);
+            put(2 + r, o4); put(2 + K + r, o6 / 250); put(4 + 2 * K + r, o5);
+            put(4 + 3 * K + r, o2 / 150); put(4 + 4 * K + r, o3 / 150);
+            put(5 + 5 * K + r, o0 / 1000000); put(5 + 6 * K + r, o1 / 1000000);
           }
         }
       } else if constexpr (KIND == BSG_ENV_VERTICAL_CR) {
         const int NI = N - 1;
         if (j == 0) {
           const double rd = 200 - kwikdist(52.0, 4.0, s.lat, s.lon) * 1.852;
-          obs[0] = (float)((s.alt - 1500) / 3000); obs[1 + 3 * NI] = (float)((rd - 100) / 200);
-          obs[2 + 4 * NI] = (float)((ev.target_alt - 1500) / 3000); obs[3 + 4 * NI] = (float)((s.vs - 0) / 5);
+          put(0, (s.alt - 1500) / 3000); put(1 + 3 * NI, (rd - 100) / 200);
+          put(2 + 4 * NI, (ev.target_alt - 1500) / 3000); put(3 + 4 * NI, (s.vs - 0) / 5);
         } else {
           const int i = j - 1;
-          obs[1 + i] = (float)(o3 / 3000); obs[1 + NI + i] = (float)o1; obs[1 + 2 * NI + i] = (float)(o0 / 200);
-          obs[2 + 3 * NI + i] = (float)o2; obs[4 + 4 * NI + i] = (float)(o4 / 150);
-          obs[4 + 5 * NI + i] = (float)(o5 / 150); obs[4 + 6 * NI + i] = (float)o6;
+          put(1 + i, o3 / 3000); put(1 + NI + i, o1); put(1 + 2 * NI + i, o0 / 200);
+          put(2 + 3 * NI + i, o2); put(4 + 4 * NI + i, o4 / 150);
+          put(4 + 5 * NI + i, o5 / 150); put(4 + 6 * NI + i, o6);
         }
       } else {
         if (j == 0) {
           const double rd = 200 - kwikdist(52.0, 4.0, s.lat, s.lon) * 1.852;
-          obs[0] = (float)((s.alt - 1500) / 3000); obs[1] = (float)((rd - 100) / 200);
-          obs[2] = (float)((ev.target_alt - 1500) / 3000); obs[3] = (float)((s.vs - 0) / 5);
+          put(0, (s.alt - 1500) / 3000); put(1, (rd - 100) / 200);
+          put(2, (ev.target_alt - 1500) / 3000); put(3, (s.vs - 0) / 5);
         }
       }
     }

@@ -103,6 +103,9 @@ typedef struct bsg_buffers {
                                 total_intrusions, faf_reach | final_altitude,
                                 average_drift (Merge) -- the info dict at done
                                 (merge_env.py:238-244, vertical_cr_env.py:203-211) */
+  float *learner;            /* optional [E, obs_dim + 3]: obs, reward, terminated,
+                                truncated as fp32 -- the per-step learner hand-off row that
+                                the multi-GPU path all-gathers over RCCL (NULL = off) */
 } bsg_buffers;
 
 typedef struct bsg_ctx bsg_ctx;

@@ -1,0 +1,35 @@
+"""Time DeviceBatch.step under configuration ablations (kernel time via HIP events)."""
+import sys, os, json
+sys.path[:0] = [os.getcwd(), os.path.join(os.getcwd(), "bluesky-gym-hallucination_amd")]
+import torch
+from bluesky_gym import core, config
+
+def run(cfg, E, cd, steps=60, warm=10):
+    b = core.DeviceBatch(cfg, E, compute_cd=cd, seed=1)
+    b.reset()
+    act = torch.rand((8, E, b.act_dim), dtype=torch.float64, device="cuda") * 2 - 1
+    for k in range(warm):
+        b.step(act[k % 8])
+    torch.cuda.synchronize(); b.step_timing(); b.set_timing(True)
+    for k in range(steps):
+        b.step(act[k % 8])
+    torch.cuda.synchronize()
+    ms, n = b.step_timing()
+    return ms / n
+
+res = {}
+for name, cfg, E, cd in [
+    ("merge32_full", config.merge_config(num_ac=32), 4096, True),
+    ("merge32_nocd", config.merge_config(num_ac=32), 4096, False),
+    ("merge32_S1", config.merge_config(num_ac=32, action_frequency=1), 4096, True),
+    ("merge32_S1_nocd", config.merge_config(num_ac=32, action_frequency=1), 4096, False),
+    ("merge32_S0_nocd", config.merge_config(num_ac=32, action_frequency=0), 4096, False),
+    ("merge16_full_1024", config.merge_config(num_ac=16), 1024, True),
+    ("vert32_full_2048", config.vertical_config(num_intruders=31), 2048, True),
+    ("descent_4096", config.descent_config(), 4096, False),
+    ("merge32_full_8192", config.merge_config(num_ac=32), 8192, True),
+    ("merge32_full_16384", config.merge_config(num_ac=32), 16384, True),
+]:
+    res[name] = run(cfg, E, cd)
+    print(name, f"{res[name]*1e3:.1f} us", flush=True)
+json.dump(res, open("gpurun_out/ablate.json", "w"), indent=1)
