@@ -45,10 +45,13 @@ constexpr double RPZ = 5.0 * NM;
 constexpr double HPZ = 1000.0 * FT;
 constexpr double DTLOOKAHEAD = 300.0;
 
+__device__ __forceinline__ uint64_t bits(double x) { return (uint64_t)__double_as_longlong(x); }
+
 __device__ __forceinline__ double sgn(double x) { return (double)((x > 0.0) - (x < 0.0)); }
 
 // np.remainder / Python float % (numpy npy_divmod): fmod, then move toward b's sign.
 __device__ __forceinline__ double pymod(double a, double b) {
+  if (a > 0.0 && a < b) return a;       // fmod is the identity there (exact fast path)
   double mod = fmod(a, b);
   if (mod != 0.0) {
     if ((b < 0.0) != (mod < 0.0)) mod += b;
@@ -167,8 +170,8 @@ __device__ __forceinline__ double rwgs84(double latd) {
   double lat = latd * kD2R;
   const double a = 6378137.0;
   const double b = 6356752.314245;
-  double coslat = cos(lat);
-  double sinlat = sin(lat);
+  double coslat, sinlat;
+  sincos(lat, &sinlat, &coslat);
   double an = a * a * coslat;
   double bn = b * b * sinlat;
   double ad = a * coslat;
@@ -197,6 +200,33 @@ __device__ __forceinline__ void qdrdist(double latd1, double lond1, double latd2
   double cosdlon = cos(lon2 - lon1);
   double d = r * acos(coslat1 * coslat2 * cosdlon + sinlat1 * sinlat2);
   *qdr = atan2(sin(lon2 - lon1) * coslat2, coslat1 * sinlat2 - sinlat1 * coslat2 * cosdlon) * kR2D;
+  *distnm = d / NM;
+}
+
+// geo.qdrdist for the LNAV hot loop, same arithmetic as qdrdist() with the trig terms
+// that do not change between calls passed in: (coslat1, sinlat1) of the aircraft
+// (carried over from update_pos, which evaluates cos/sin of the same latitude) and
+// (coslat2, sinlat2) of the active waypoint (cached per waypoint).  sincos() is
+// bit-identical to separate sin()/cos() on gfx950/ROCm 7.2 (tools/probe/sincos_probe.hip).
+__device__ __forceinline__ void qdrdist_cached(double latd1, double lond1, double coslat1,
+                                               double sinlat1, double latd2, double lond2,
+                                               double coslat2, double sinlat2, double* qdr,
+                                               double* distnm) {
+  bool sw = (latd1 * latd2 >= 0.0);
+  double r;
+  if (sw) {
+    r = rwgs84(0.5 * (latd1 + latd2));
+  } else {
+    const double a = 6378137.0;
+    double r1 = rwgs84(latd1);
+    double r2 = rwgs84(latd2);
+    r = 0.5 * (fabs(latd1) * (r1 + a) + fabs(latd2) * (r2 + a)) /
+        npmax(0.000001, fabs(latd1) + fabs(latd2));
+  }
+  double sdl, cdl;
+  sincos(lond2 * kD2R - lond1 * kD2R, &sdl, &cdl);
+  double d = r * acos(coslat1 * coslat2 * cdl + sinlat1 * sinlat2);
+  *qdr = atan2(sdl * coslat2, coslat1 * sinlat2 - sinlat1 * coslat2 * cdl) * kR2D;
   *distnm = d / NM;
 }
 

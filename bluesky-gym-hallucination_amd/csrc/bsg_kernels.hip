@@ -4,16 +4,33 @@
 // Mapping: one 64-lane wavefront = one workgroup = 64/GS envs; lane (g, j) owns
 // aircraft j of env g (GS = next power of two >= N).  Per launch each lane
 //   A. loads (or spawns) its aircraft from the [E][N] fp64 SoA arrays (coalesced),
-//      applies the action (j == 0) and integrates ACTION_FREQUENCY BlueSky substeps in
-//      registers (no inter-lane traffic: with RESO OFF the kinematics are per aircraft);
+//      applies the action (j == 0), integrates ACTION_FREQUENCY BlueSky substeps in
+//      registers (no inter-lane traffic: with RESO OFF the kinematics are per aircraft)
+//      and stores the new state;
 //   B. stages the post-step state in LDS, computes the env-layer observation, the
 //      reward / termination / TimeLimit (lane j == 0), the nearest-K selection (rank by
 //      LDS sweep), the intrusion mask (wave ballot) and the StateBased all-pairs CPA row
-//      of aircraft j (LDS sweep over the group), reduces min separation with wave
+//      of aircraft j (LDS sweep over the group), reduces the min separation with wave
 //      shuffles, and writes every output;
-//   C. (SAME_STEP autoreset) respawns finished envs and writes their reset observation;
-//   and stores the state back.
+//   C. (SAME_STEP autoreset only) respawns finished envs and writes their reset obs.
 // Every barrier is executed by all 64 lanes (block-uniform control flow).
+//
+// Exactness-preserving work removal (each produces the same bits as the straight
+// restatement in oracle/bluesky_subset.py):
+//   * pure functions of unchanged inputs are memoised across substeps by exact bit
+//     compare of their inputs: vatmos(alt), casormach2tas(selspd, alt) and the
+//     PerfModel.limits speed clamp (ap_tas, allow_h) -- in steady flight a substep
+//     evaluates no pow/exp at all;
+//   * traf.cas is only read by the next action decode, so update_airspeed's
+//     cas = vtas2cas(tas, alt) is evaluated once, after the last substep, with that
+//     substep's atmosphere;
+//   * cos/sin(lat) from update_pos are carried into the next LNAV qdrdist, waypoint
+//     trig is cached per waypoint, sin/cos pairs use sincos (bit-identical, probed);
+//   * the fly-by turn distance tan() is skipped when dist > turnrad >= turndist;
+//   * StateBased pairs farther apart than the horizon RPZ + DTLOOKAHEAD*vrel (+margin)
+//     cannot be in conflict or LoS (DESIGN.md §CD horizon proof); their atan2/sincos/
+//     divisions are skipped, and pairs whose latitude gap alone exceeds the horizon skip
+//     the distance as well.  min_sep is defined over the pairs inside the horizon.
 #include <hip/hip_runtime.h>
 
 #include "bsg_device.h"
@@ -28,14 +45,14 @@ struct AC {
   int nav;
 };
 
-__device__ __forceinline__ void load_ac(const Buffers& b, int a, AC& s) {
+__device__ __forceinline__ void load_ac(const Buffers& b, size_t a, AC& s) {
   s.lat = b.lat[a]; s.lon = b.lon[a]; s.alt = b.alt[a]; s.hdg = b.hdg[a];
   s.tas = b.tas[a]; s.cas = b.cas[a]; s.vs = b.vs[a]; s.ax = b.ax[a];
   s.ap_trk = b.ap_trk[a]; s.selspd = b.selspd[a]; s.selalt = b.selalt[a]; s.selvs = b.selvs[a];
   s.nav = b.nav[a];
 }
 
-__device__ __forceinline__ void store_ac(const Buffers& b, int a, const AC& s) {
+__device__ __forceinline__ void store_ac(const Buffers& b, size_t a, const AC& s) {
   b.lat[a] = s.lat; b.lon[a] = s.lon; b.alt[a] = s.alt; b.hdg[a] = s.hdg;
   b.tas[a] = s.tas; b.cas[a] = s.cas; b.vs[a] = s.vs; b.ax[a] = s.ax;
   b.ap_trk[a] = s.ap_trk; b.selspd[a] = s.selspd; b.selalt[a] = s.selalt; b.selvs[a] = s.selvs;
@@ -53,58 +70,103 @@ __device__ __forceinline__ void cre(AC& s, double lat, double lon, double hdg, d
   s.nav = 0;
 }
 
+// ---- exact memo of pure functions across substeps ---------------------------------------
+struct Memo {
+  uint64_t alt_bits;               // key of at = vatmos(alt)
+  Atmos at;
+  uint64_t spd_bits, spdalt_bits;  // key of ap_tas = casormach2tas(selspd, alt)
+  double ap_tas;
+  uint64_t lim_tas_bits, lim_h_bits;  // key of the PerfModel.limits speed clamp
+  double allow_tas;
+  int wp_k;                        // cached waypoint trig
+  double wp_cos, wp_sin;
+  double coslat, sinlat;           // cos/sin(lat * D2R) of the current latitude
+};
+
+constexpr uint64_t kNoKey = 0x7ff8dead0000beefull;   // a NaN payload no input produces
+
+__device__ __forceinline__ void memo_init(Memo& m, const AC& s) {
+  m.alt_bits = kNoKey; m.spd_bits = kNoKey; m.spdalt_bits = kNoKey;
+  m.lim_tas_bits = kNoKey; m.lim_h_bits = kNoKey;
+  m.at = Atmos{0, 0, 0}; m.ap_tas = 0; m.allow_tas = 0;
+  m.wp_k = -1; m.wp_cos = 0; m.wp_sin = 0;
+  sincos(s.lat * kD2R, &m.sinlat, &m.coslat);
+}
+
 // ---- one BlueSky substep of one aircraft (Traffic.update, wind off, RESO OFF) ---------
 // oracle/bluesky_subset.py: traffic_update
-__device__ __forceinline__ void substep(AC& s, double dt, const Route& rt) {
+__device__ __forceinline__ void substep(AC& s, Memo& m, double dt, const Route& rt) {
   // Autopilot.update -- LNAV direct-to + ActiveWaypoint.reached (gs = tas, trk = hdg)
   if (s.nav & 1) {
     int k = (s.nav >> 8) & 0xff;
+    if (k != m.wp_k) { m.wp_k = k; sincos(rt.lat[k] * kD2R, &m.wp_sin, &m.wp_cos); }
     double qdr, dnm;
-    qdrdist(s.lat, s.lon, rt.lat[k], rt.lon[k], &qdr, &dnm);
-    double dist = dnm * NM;
-    double nq = rt.next_qdr[k];
-    double next_qdr = nq < -900.0 ? qdr : nq;
-    double turnrad = s.tas * s.tas / (npmax(0.01, TAN_BANKDEF) * G0);
-    double turndist = fabs(turnrad * tan((0.5 * fabs(degto180(pymod(qdr, 360.0) -
-                                                                pymod(next_qdr, 360.0)))) * kD2R));
-    bool close2wp = dist / npmax(0.0001, fabs(s.tas)) < 4.0;
-    bool tooclose = close2wp && (fabs(degto180(pymod(s.hdg, 360.0) - pymod(qdr, 360.0))) > 90.0);
-    if ((dist < turndist) || tooclose) {
+    qdrdist_cached(s.lat, s.lon, m.coslat, m.sinlat, rt.lat[k], rt.lon[k], m.wp_cos, m.wp_sin,
+                   &qdr, &dnm);
+    const double dist = dnm * NM;
+    const double nq = rt.next_qdr[k];
+    const double next_qdr = nq < -900.0 ? qdr : nq;
+    const double turnrad = s.tas * s.tas / (npmax(0.01, TAN_BANKDEF) * G0);
+    const double half = 0.5 * fabs(degto180(pymod(qdr, 360.0) - pymod(next_qdr, 360.0)));
+    bool reached_turn;
+    if (half <= 45.0 && dist > turnrad * 1.000001) {
+      reached_turn = false;                  // tan(half) <= 1 -> turndist <= turnrad < dist
+    } else {
+      const double turndist = fabs(turnrad * tan(half * kD2R));
+      reached_turn = dist < turndist;
+    }
+    const bool close2wp = dist / npmax(0.0001, fabs(s.tas)) < 4.0;
+    const bool tooclose = close2wp && (fabs(degto180(pymod(s.hdg, 360.0) - pymod(qdr, 360.0))) > 90.0);
+    if (reached_turn || tooclose) {
       if (k >= rt.len - 1) {
         s.nav &= ~1;                       // last waypoint: LNAV off, keep commanded track
       } else {
         ++k;
         s.nav = (k << 8) | 1;
-        qdrdist(s.lat, s.lon, rt.lat[k], rt.lon[k], &qdr, &dnm);
+        m.wp_k = k;
+        sincos(rt.lat[k] * kD2R, &m.wp_sin, &m.wp_cos);
+        qdrdist_cached(s.lat, s.lon, m.coslat, m.sinlat, rt.lat[k], rt.lon[k], m.wp_cos,
+                       m.wp_sin, &qdr, &dnm);
       }
     }
     if (s.nav & 1) s.ap_trk = qdr;
   }
   const double ap_vs = fabs(s.selvs) > 0.1 ? s.selvs : APVSDEF;
   const double ap_alt = s.selalt;
-  const Atmos at = vatmos(s.alt);
-  const double ap_tas = casormach2tas_at(s.selspd, at);
+  const uint64_t ab = bits(s.alt);
+  if (ab != m.alt_bits) { m.at = vatmos(s.alt); m.alt_bits = ab; }
+  if (bits(s.selspd) != m.spd_bits || ab != m.spdalt_bits) {
+    m.ap_tas = casormach2tas_at(s.selspd, m.at);
+    m.spd_bits = bits(s.selspd);
+    m.spdalt_bits = ab;
+  }
   // aporasas
   const double vs_cmd0 = fabs(ap_vs);
   const double hdg_cmd = pymod(s.ap_trk, 360.0);
   // PerfModel.limits (frozen A320 envelope)
   const double allow_h = ap_alt > HMAX ? HMAX : ap_alt;
-  const Atmos ah = (allow_h == s.alt) ? at : vatmos(allow_h);
-  const double intent_cas = tas2cas_at(ap_tas, ah);
-  double allow_cas = intent_cas < VMIN_CAS ? VMIN_CAS : intent_cas;
-  allow_cas = intent_cas > VMAX_CAS ? VMAX_CAS : allow_cas;
-  double allow_tas = cas2tas_at(allow_cas, ah);
-  const double snd_h = sound_at(ah);
-  if (allow_tas / snd_h > MMO) allow_tas = MMO * snd_h;
+  const uint64_t hb = bits(allow_h);
+  if (bits(m.ap_tas) != m.lim_tas_bits || hb != m.lim_h_bits) {
+    const Atmos ah = (hb == ab) ? m.at : vatmos(allow_h);
+    const double intent_cas = tas2cas_at(m.ap_tas, ah);
+    double allow_cas = intent_cas < VMIN_CAS ? VMIN_CAS : intent_cas;
+    allow_cas = intent_cas > VMAX_CAS ? VMAX_CAS : allow_cas;
+    double allow_tas = cas2tas_at(allow_cas, ah);
+    const double snd_h = sound_at(ah);
+    if (allow_tas / snd_h > MMO) allow_tas = MMO * snd_h;
+    m.allow_tas = allow_tas;
+    m.lim_tas_bits = bits(m.ap_tas);
+    m.lim_h_bits = hb;
+  }
+  const double allow_tas = m.allow_tas;
   const double vs_max_with_acc = (1 - s.ax / AXMAX) * VSMAX;
   double vs_cmd = (vs_cmd0 > 0 && vs_cmd0 > VSMAX) ? vs_max_with_acc : vs_cmd0;
   vs_cmd = (vs_cmd0 < 0 && vs_cmd0 < VSMIN) ? VSMIN : vs_cmd;
-  // update_airspeed
+  // update_airspeed (traf.cas is evaluated after the last substep, see step_kernel)
   const double delta_spd = allow_tas - s.tas;
   const bool need_ax = fabs(delta_spd) > fabs(dt * AXMAX);
   s.ax = (double)need_ax * sgn(delta_spd) * AXMAX;
   s.tas = need_ax ? s.tas + s.ax * dt : allow_tas;
-  s.cas = tas2cas_at(s.tas, at);
   const double turnrate = (G0 * TAN_BANKDEF / npmax(s.tas, EPS_SPD)) * kR2D;
   const double delhdg = pymod(hdg_cmd - s.hdg + 180.0, 360.0) - 180.0;
   const bool swhdgsel = fabs(delhdg) > fabs(dt * turnrate);
@@ -118,81 +180,102 @@ __device__ __forceinline__ void substep(AC& s, double dt, const Route& rt) {
   s.vs = need_az ? s.vs + az * dt : target_vs;
   if (!isfinite(s.vs)) s.vs = 0.0;
   // update_groundspeed (no wind) + update_pos
-  const double gsnorth = s.tas * cos(s.hdg * kD2R);
-  const double gseast = s.tas * sin(s.hdg * kD2R);
+  double shdg, chdg;
+  sincos(s.hdg * kD2R, &shdg, &chdg);
+  const double gsnorth = s.tas * chdg;
+  const double gseast = s.tas * shdg;
   s.alt = swaltsel ? rint((s.alt + s.vs * dt) * 1e6) / 1e6 : allow_h;
   s.lat = s.lat + (dt * gsnorth / Rearth) * kR2D;
-  const double coslat = cos(s.lat * kD2R);
-  s.lon = s.lon + (dt * gseast / coslat / Rearth) * kR2D;
+  sincos(s.lat * kD2R, &m.sinlat, &m.coslat);
+  s.lon = s.lon + (dt * gseast / m.coslat / Rearth) * kR2D;
 }
 
 // ---- LDS staging (one wave per block; GS lanes per env) -------------------------------
 struct Lds {
   double lat[64], lon[64], alt[64], hdg[64], tas[64], vs[64], u[64], v[64], d[64];
   int done[64];
+  // StateBased assembly (LDS atomics)
+  unsigned long long cm[64], lm[64], tmax[64], gmin[64];
 };
 
-__device__ __forceinline__ void stage(Lds& L, int lane, bool ok, const AC& s) {
+__device__ __forceinline__ void stage(Lds& L, int lane, const AC& s) {
   L.lat[lane] = s.lat; L.lon[lane] = s.lon; L.alt[lane] = s.alt; L.hdg[lane] = s.hdg;
   L.tas[lane] = s.tas; L.vs[lane] = s.vs;
-  if (ok) {
-    // StateBased: u = gs*sin(trk), v = gs*cos(trk)  (gs = tas, trk = hdg, no wind)
-    double trkrad = s.hdg * kD2R;
-    L.u[lane] = s.tas * sin(trkrad);
-    L.v[lane] = s.tas * cos(trkrad);
-  }
+  // StateBased: u = gs*sin(trk), v = gs*cos(trk)  (gs = tas, trk = hdg, no wind)
+  double st, ct;
+  sincos(s.hdg * kD2R, &st, &ct);
+  L.u[lane] = s.tas * st;
+  L.v[lane] = s.tas * ct;
 }
 
-// StateBased.detect row i = lane j vs every aircraft k of the group (oracle: statebased_detect)
-template <int GS>
-__device__ __forceinline__ void cd_row(const Lds& L, int base, int j, int N, uint64_t* conf,
-                                       uint64_t* los, double* tcpamax, double* minsep) {
-  const double lati = L.lat[base + j], loni = L.lon[base + j], alti = L.alt[base + j];
-  const double ui = L.u[base + j], vi = L.v[base + j], vsi = L.vs[base + j];
+// ---- StateBased.detect (oracle: statebased_detect), wave-compacted -------------------
+// Pair (i, k) -- aircraft k relative to aircraft i, both lanes of one group -- is in
+// conflict only inside the horizon dist < RPZ + DTLOOKAHEAD*vrel (DESIGN.md proof) and in
+// LoS only if dist < RPZ.  Phase 1 tests every ordered pair against a conservative
+// latitude bound (no transcendentals); phase 2 runs the exact StateBased arithmetic on the
+// surviving pairs from a dense LDS work list, one pair per lane, so a far pair never
+// holds a lane hostage to a near one.  Row masks / tcpamax / per-env min separation are
+// assembled with LDS atomics (u64 or / min / max; tcpa > 0 and dist >= 0 order like u64).
+
+// true unless the pair is provably outside the horizon.  Skip => computed
+// dist >= Re*|dlat|*(1-1e-14) > Re*|dlat|*0.999998 - 1 >= computed horizon.
+__device__ __forceinline__ bool cd_candidate(double dlat, double dv2f) {
+  const double a = 6371000.0 * fabs(dlat) * 0.999998 - 1.0;
+  const double w = (a * 0.999999 - RPZ) * (1.0 / DTLOOKAHEAD);
+  return !(w > 0.0 && w * w > dv2f * 1.000001);
+}
+
+struct CdOut {
+  bool confl, lossep;
+  double tcpa, dist;
+  bool inside;
+};
+
+// exact StateBased terms of pair (i, k) (i != k), oracle operation order
+__device__ __forceinline__ CdOut cd_pair(const Lds& L, int i, int k) {
+  CdOut r{false, false, 0.0, 0.0, false};
+  const double lati = L.lat[i], loni = L.lon[i];
+  const double latk = L.lat[k], lonk = L.lon[k];
+  const double dlat = (latk - lati) * kD2R;
+  const double dlon = (pymod((lonk - loni) + 180.0, 360.0) - 180.0) * kD2R;
+  const double cavelat = cos(((lati + latk) * kD2R) * 0.5);
+  const double dangle = sqrt(dlat * dlat + (dlon * dlon) * (cavelat * cavelat));
+  const double dist = (6371000.0 * dangle / NM) * NM + 0.0;     // + 1e9*I, I = 0
+  const double du = L.u[k] - L.u[i];
+  const double dv = L.v[k] - L.v[i];
+  double dv2 = du * du + dv * dv;
+  dv2 = fabs(dv2) < 1e-6 ? 1e-6 : dv2;
+  const double vrel = sqrt(dv2);
+  const double horizon = (RPZ + DTLOOKAHEAD * vrel) * (1.0 + 1e-9) + 1.0;
+  if (dist > horizon) return r;
+  r.inside = true;
+  r.dist = dist;
+  const double qdr = pymod(atan2(dlon * cavelat, dlat) * kR2D, 360.0);
+  double sq, cq;
+  sincos(qdr * kD2R, &sq, &cq);
+  const double dx = dist * sq;
+  const double dy = dist * cq;
+  const double tcpa = -(du * dx + dv * dy) / dv2 + 0.0;
   const double R2 = RPZ * RPZ;
-  uint64_t cm = 0, lm = 0;
-  double tmax = 0.0;     // np.max(tcpa * swconfl) -- diagonal contributes 0
-  double dmin = __builtin_inf();
-  bool first = true;
-  for (int k = 0; k < N; ++k) {
-    double qdr, dnm;
-    kwikqdrdist_mat(lati, loni, L.lat[base + k], L.lon[base + k], &qdr, &dnm);
-    const double diag = (k == j) ? 1e9 : 0.0;
-    const double dist = dnm * NM + diag;
-    const double qdrrad = qdr * kD2R;
-    const double dx = dist * sin(qdrrad);
-    const double dy = dist * cos(qdrrad);
-    const double du = L.u[base + k] - ui;
-    const double dv = L.v[base + k] - vi;
-    double dv2 = du * du + dv * dv;
-    dv2 = fabs(dv2) < 1e-6 ? 1e-6 : dv2;
-    const double vrel = sqrt(dv2);
-    const double tcpa = -(du * dx + dv * dy) / dv2 + diag;
-    const double dcpa2 = fabs(dist * dist - tcpa * tcpa * dv2);
-    const bool swhor = dcpa2 < R2;
-    const double dxinhor = sqrt(npmax(0.0, R2 - dcpa2));
-    const double dtinhor = dxinhor / vrel;
-    const double tinhor = swhor ? tcpa - dtinhor : 1e8;
-    const double touthor = swhor ? tcpa + dtinhor : -1e8;
-    const double dalt = L.alt[base + k] - alti + diag;
-    double dvs = L.vs[base + k] - vsi;
-    dvs = fabs(dvs) < 1e-6 ? 1e-6 : dvs;
-    const double tcrosshi = (dalt + HPZ) / -dvs;
-    const double tcrosslo = (dalt - HPZ) / -dvs;
-    const double tinver = npmin(tcrosshi, tcrosslo);
-    const double toutver = npmax(tcrosshi, tcrosslo);
-    const double tin = npmax(tinver, tinhor);
-    const double tout = npmin(toutver, touthor);
-    const bool confl = swhor && (tin <= tout) && (tout > 0.0) && (tin < DTLOOKAHEAD) && (k != j);
-    const bool lossep = (dist < RPZ) && (fabs(dalt) < HPZ);
-    cm |= (uint64_t)confl << k;
-    lm |= (uint64_t)lossep << k;
-    const double tc = tcpa * (double)confl;
-    if (first || tc > tmax) tmax = tc;
-    first = false;
-    if (k != j) dmin = npmin(dmin, dist);
-  }
-  *conf = cm; *los = lm; *tcpamax = tmax; *minsep = dmin;
+  const double dcpa2 = fabs(dist * dist - tcpa * tcpa * dv2);
+  const bool swhor = dcpa2 < R2;
+  const double dxinhor = sqrt(npmax(0.0, R2 - dcpa2));
+  const double dtinhor = dxinhor / vrel;
+  const double tinhor = swhor ? tcpa - dtinhor : 1e8;
+  const double touthor = swhor ? tcpa + dtinhor : -1e8;
+  const double dalt = L.alt[k] - L.alt[i] + 0.0;
+  double dvs = L.vs[k] - L.vs[i];
+  dvs = fabs(dvs) < 1e-6 ? 1e-6 : dvs;
+  const double tcrosshi = (dalt + HPZ) / -dvs;
+  const double tcrosslo = (dalt - HPZ) / -dvs;
+  const double tinver = npmin(tcrosshi, tcrosslo);
+  const double toutver = npmax(tcrosshi, tcrosslo);
+  const double tin = npmax(tinver, tinhor);
+  const double tout = npmin(toutver, touthor);
+  r.confl = swhor && (tin <= tout) && (tout > 0.0) && (tin < DTLOOKAHEAD);
+  r.lossep = (dist < RPZ) && (fabs(dalt) < HPZ);
+  r.tcpa = tcpa;
+  return r;
 }
 
 template <int GS>
@@ -306,9 +389,22 @@ __device__ __forceinline__ void spawn_vertical(const KParams& p, int e, int j, u
   s.selvs = acvs;
 }
 
+template <int KIND>
+__device__ __forceinline__ void spawn(const KParams& p, int e, int j, uint32_t episode, AC& s,
+                                      double* target) {
+  if constexpr (KIND == BSG_ENV_MERGE) {
+    spawn_merge(p, e, j, episode, s);
+  } else if constexpr (KIND == BSG_ENV_VERTICAL_CR) {
+    spawn_vertical(p, e, j, episode, s, target);
+  } else {
+    double alt_init;
+    draw_alts(p, e, episode, TAG_DESC, &alt_init, target);
+    cre(s, 52.0, 4.0, 0.0, alt_init, 150.0);
+  }
+}
+
 // ---------------------------------------------------------------------------------------
-// Observation / reward per env kind.  Values are computed into registers first; the
-// done flag is published through LDS; then outputs are written.
+// Per-env scalars
 // ---------------------------------------------------------------------------------------
 struct EnvScalars {
   int step_count, flags, wpt_reach, faf_reached, total_intr;
@@ -336,6 +432,148 @@ __device__ __forceinline__ void reset_scalars(EnvScalars& v, double target) {
   v.episode += 1;
 }
 
+// ---------------------------------------------------------------------------------------
+// Per-lane observation terms of aircraft j (j >= 1) relative to the ownship (LDS).
+// o[0..6] per kind (see the writers below); returns the intrusion predicate.
+// ---------------------------------------------------------------------------------------
+template <int KIND>
+__device__ __forceinline__ bool lane_obs(const Lds& L, int base, int lane, double o[7],
+                                         double* sortkey) {
+  const double lat0 = L.lat[base], lon0 = L.lon[base], hdg0 = L.hdg[base];
+  const double latj = L.lat[lane], lonj = L.lon[lane];
+  // shared kwik terms: lata + latb == latb + lata bitwise, so cavelat is common to the
+  // kwikdist_matrix (merge_env.py:195) and kwikqdrdist (:203) forms
+  const double dlat = (latj - lat0) * kD2R;
+  const double dlon = (pymod((lonj - lon0) + 180.0, 360.0) - 180.0) * kD2R;
+  const double cavelat = cos(((lat0 + latj) * kD2R) * 0.5);
+  const double dist = 6371000.0 * sqrt(dlat * dlat + dlon * dlon * cavelat * cavelat) / NM;
+  const double qdr = pymod(atan2(dlon * cavelat, dlat) * kR2D, 360.0);
+  if constexpr (KIND == BSG_ENV_MERGE) {
+    // merge_env.py:195-218
+    const double dmat = 6371000.0 * sqrt(dlat * dlat + (dlon * dlon) * (cavelat * cavelat)) / NM;
+    double sb, cb;
+    sincos(qdr * kD2R, &sb, &cb);
+    const double x_r = (dist * 1.852 * 1000) * cb;
+    const double y_r = (dist * 1.852 * 1000) * sb;
+    // vx = cos(hdg)*tas == v = tas*cos(hdg) bitwise (LDS staging)
+    const double vx_r = L.v[lane] - L.v[base], vy_r = L.u[lane] - L.u[base];
+    const double track = atan2(vy_r, vx_r);
+    double st, ct;
+    sincos(track, &st, &ct);
+    o[0] = x_r; o[1] = y_r; o[2] = vx_r; o[3] = vy_r; o[4] = ct; o[5] = st; o[6] = dmat;
+    *sortkey = dmat;
+    return dist < 4;                                       // _check_intrusion :280-281
+  } else {
+    // vertical_cr_env.py:133-156
+    const double alt0 = L.alt[base], vs0 = L.vs[base], gs0 = L.tas[base];
+    const double altj = L.alt[lane], tasj = L.tas[lane];
+    const double bearing = bound180(hdg0 - qdr);
+    const double hd = hdg0 - L.hdg[lane];
+    double sbr, cbr, shd, chd;
+    sincos(bearing * kD2R, &sbr, &cbr);
+    sincos(hd * kD2R, &shd, &chd);
+    o[0] = dist * 1.852;                                    // intruder_distance (km)
+    o[1] = cbr;
+    o[2] = sbr;
+    o[3] = altj - alt0;                                     // altitude_difference
+    o[4] = -chd * tasj;                                     // x_difference_speed
+    o[5] = gs0 - shd * tasj;                                // y_difference_speed
+    o[6] = L.vs[lane] - vs0;                                // z_difference_speed
+    *sortkey = 0.0;
+    return (dist < 5) && (fabs(alt0 - altj) < 1000 * 0.3048);   // :235-237
+  }
+}
+
+template <int KIND>
+__device__ __forceinline__ void write_lane_obs(float* obs, float* fobs, float* lrn, int K, int N,
+                                               int j, int rank, const double o[7]) {
+  auto put = [&](int off, double v) {
+    const float f = (float)v;
+    obs[off] = f;
+    if (fobs) fobs[off] = f;
+    if (lrn) lrn[off] = f;
+  };
+  if constexpr (KIND == BSG_ENV_MERGE) {
+    if (rank < K) {
+      put(2 + rank, o[4]);                  // cos(track)
+      put(2 + K + rank, o[6] / 250);        // distances
+      put(4 + 2 * K + rank, o[5]);          // sin(track)
+      put(4 + 3 * K + rank, o[2] / 150);    // vx_r
+      put(4 + 4 * K + rank, o[3] / 150);    // vy_r
+      put(5 + 5 * K + rank, o[0] / 1000000);// x_r
+      put(5 + 6 * K + rank, o[1] / 1000000);// y_r
+    }
+  } else if constexpr (KIND == BSG_ENV_VERTICAL_CR) {
+    const int NI = N - 1, i = j - 1;
+    put(1 + i, o[3] / 3000);                // altitude_difference
+    put(1 + NI + i, o[1]);                  // cos_difference_pos
+    put(1 + 2 * NI + i, o[0] / 200);        // intruder_distance
+    put(2 + 3 * NI + i, o[2]);              // sin_difference_pos
+    put(4 + 4 * NI + i, o[4] / 150);        // x_difference_speed
+    put(4 + 5 * NI + i, o[5] / 150);        // y_difference_speed
+    put(4 + 6 * NI + i, o[6]);              // z_difference_speed
+  }
+}
+
+// Ownship scalar obs (lane j == 0).  Merge: merge_env.py:175-191 with the pre-reward
+// wpt_reach; Vertical/Descent: vertical_cr_env.py:129-164 / descent_env.py:100-108.
+template <int KIND>
+__device__ __forceinline__ void own_obs(const KParams& p, const Lds& L, int lane, const EnvScalars& ev,
+                                        double sc[5], double* wdist, double* drift, double* rwd) {
+  const double lat = L.lat[lane], lon = L.lon[lane];
+  if constexpr (KIND == BSG_ENV_MERGE) {
+    const int w = ev.wpt_reach == 0 ? 0 : 1;
+    double wqdr;
+    kwikqdrdist(lat, lon, p.cfg.wpt_lat[w], p.cfg.wpt_lon[w], &wqdr, wdist);
+    *drift = bound180(L.hdg[lane] - wqdr);
+    double sd, cd;
+    sincos(*drift * kD2R, &sd, &cd);
+    sc[0] = L.tas[lane]; sc[1] = cd; sc[2] = (double)ev.wpt_reach; sc[3] = sd; sc[4] = *wdist / 250;
+  } else {
+    const double altitude = L.alt[lane], vz = L.vs[lane];
+    *rwd = 200 - kwikdist(52.0, 4.0, lat, lon) * 1.852;
+    sc[0] = (altitude - 1500) / 3000; sc[1] = (vz - 0) / 5; sc[2] = (ev.target_alt - 1500) / 3000;
+    sc[3] = (*rwd - 100) / 200; sc[4] = 0.0;
+  }
+}
+
+template <int KIND>
+__device__ __forceinline__ void write_own_obs(float* obs, float* fobs, float* lrn, int K, int N,
+                                              const double sc[5]) {
+  auto put = [&](int off, double v) {
+    const float f = (float)v;
+    obs[off] = f;
+    if (fobs) fobs[off] = f;
+    if (lrn) lrn[off] = f;
+  };
+  if constexpr (KIND == BSG_ENV_MERGE) {
+    put(0, sc[0]);                          // airspeed
+    put(1, sc[1]);                          // cos(drift)
+    put(2 + 2 * K, sc[2]);                  // faf_reached
+    put(3 + 2 * K, sc[3]);                  // sin(drift)
+    put(4 + 5 * K, sc[4]);                  // waypoint_dist
+  } else if constexpr (KIND == BSG_ENV_VERTICAL_CR) {
+    const int NI = N - 1;
+    put(0, sc[0]);                          // altitude
+    put(1 + 3 * NI, sc[3]);                 // runway_distance
+    put(2 + 4 * NI, sc[2]);                 // target_altitude
+    put(3 + 4 * NI, sc[1]);                 // vz
+  } else {
+    put(0, sc[0]); put(1, sc[3]); put(2, sc[2]); put(3, sc[1]);
+  }
+}
+
+__device__ __forceinline__ int rank_in_group(const Lds& L, int base, int lane, int j, int N) {
+  const double dj = L.d[lane];
+  int r = 0;
+  for (int k = 1; k < N; ++k) {
+    const double dk = L.d[base + k];
+    r += (dk < dj) || (dk == dj && k < j);
+  }
+  return r;
+}
+
+// ---------------------------------------------------------------------------------------
 template <int KIND, int GS>
 __global__ __launch_bounds__(64) void step_kernel(KParams p) {
   __shared__ Lds L;
@@ -350,6 +588,7 @@ __global__ __launch_bounds__(64) void step_kernel(KParams p) {
   const size_t a = (size_t)e * N + j;
   const Buffers& b = p.b;
   const int O = p.obs_dim;
+  const int K = p.K;
 
   EnvScalars ev = {};
   if (env_ok) load_env(b, e, ev);
@@ -361,168 +600,159 @@ __global__ __launch_bounds__(64) void step_kernel(KParams p) {
   const bool stepping = env_ok && p.mode == MODE_STEP && !resetting;
   const bool active = resetting || stepping;   // env produces outputs this launch
 
-  // ---------------- A: spawn or propagate -----------------------------------------
-  AC s = {};
-  double new_target = ev.target_alt;
-  if (ok) {
-    if (resetting) {
-      if constexpr (KIND == BSG_ENV_MERGE) spawn_merge(p, e, j, ev.episode, s);
-      else if constexpr (KIND == BSG_ENV_VERTICAL_CR) spawn_vertical(p, e, j, ev.episode, s, &new_target);
-      else {
-        double alt_init;
-        draw_alts(p, e, ev.episode, TAG_DESC, &alt_init, &new_target);
-        cre(s, 52.0, 4.0, 0.0, alt_init, 150.0);
+  // ---------------- A: spawn or propagate, store state ------------------------------
+  {
+    AC s = {};
+    double new_target = ev.target_alt;
+    if (ok) {
+      if (resetting) {
+        spawn<KIND>(p, e, j, ev.episode, s, &new_target);
+      } else {
+        load_ac(b, a, s);
       }
-    } else {
-      load_ac(b, (int)a, s);
-    }
-    if (stepping) {
-      if (j == 0) {
-        if constexpr (KIND == BSG_ENV_MERGE) {
-          // merge_env.py:286-293 -> HDG / SPD stack commands
-          const double dh = p.actions[(size_t)e * 2 + 0] * 15;
-          const double dv = p.actions[(size_t)e * 2 + 1] * 20;
-          const double heading_new = bound180(s.hdg + dh);
-          const double speed_new = (s.cas + dv) * 1.94384;
-          s.ap_trk = heading_new;
-          s.nav &= ~1;
-          s.selspd = speed_new >= 1.0 ? speed_new * KTS : speed_new;
-        } else {
-          // vertical_cr_env.py:242-256 / descent_env.py:146-160
-          const double act = p.actions[e] * 12.5;
-          if (act >= 0) { s.selalt = 1000000; s.selvs = act; }
-          else if (act < 0) { s.selalt = 0; s.selvs = act; }
+      if (stepping) {
+        if (j == 0) {
+          if constexpr (KIND == BSG_ENV_MERGE) {
+            // merge_env.py:286-293 -> HDG / SPD stack commands
+            const double dh = p.actions[(size_t)e * 2 + 0] * 15;
+            const double dv = p.actions[(size_t)e * 2 + 1] * 20;
+            const double heading_new = bound180(s.hdg + dh);
+            const double speed_new = (s.cas + dv) * 1.94384;
+            s.ap_trk = heading_new;
+            s.nav &= ~1;
+            s.selspd = speed_new >= 1.0 ? speed_new * KTS : speed_new;
+          } else {
+            // vertical_cr_env.py:242-256 / descent_env.py:146-160
+            const double act = p.actions[e] * 12.5;
+            if (act >= 0) { s.selalt = 1000000; s.selvs = act; }
+            else if (act < 0) { s.selalt = 0; s.selvs = act; }
+          }
+        }
+        const int S = p.cfg.action_frequency;
+        if (S > 0) {
+          Memo m;
+          memo_init(m, s);
+          for (int it = 0; it < S; ++it) substep(s, m, p.cfg.simdt, p.route);
+          // update_airspeed's cas = vtas2cas(tas, alt) of the LAST substep (its alt is the
+          // one before that substep's update_pos, i.e. m.at's key)
+          s.cas = tas2cas_at(s.tas, m.at);
         }
       }
-      for (int it = 0; it < p.cfg.action_frequency; ++it) substep(s, p.cfg.simdt, p.route);
+      if (active) store_ac(b, a, s);
     }
+    if (resetting && j == 0) reset_scalars(ev, new_target);
+    stage(L, lane, s);
   }
-  if (resetting && j == 0) reset_scalars(ev, new_target);
+  __syncthreads();
 
   // ---------------- B: observation, reward, CD -----------------------------------------
-  stage(L, lane, ok, s);
-  __syncthreads();
-
-  bool done = false;
-  float reward = 0.0f;
-  bool term = false, trunc = false;
-  // per-lane obs values
-  double o0 = 0, o1 = 0, o2 = 0, o3 = 0, o4 = 0, o5 = 0, o6 = 0;
-  int rank = 0x7fffffff;
+  double o[7] = {0, 0, 0, 0, 0, 0, 0};
+  double sortkey = __builtin_inf();
   bool intr = false;
+  if (ok && j > 0 && KIND != BSG_ENV_DESCENT) intr = lane_obs<KIND>(L, base, lane, o, &sortkey);
   if constexpr (KIND == BSG_ENV_MERGE) {
-    const double lat0 = L.lat[base], lon0 = L.lon[base], hdg0 = L.hdg[base], tas0 = L.tas[base];
-    if (ok && j > 0) {
-      // merge_env.py:195-218
-      const double dmat = kwikdist_mat(lat0, lon0, s.lat, s.lon);
-      double brg, dist;
-      kwikqdrdist(lat0, lon0, s.lat, s.lon, &brg, &dist);
-      const double vx = cos(hdg0 * kD2R) * tas0;
-      const double vy = sin(hdg0 * kD2R) * tas0;
-      const double x_r = (dist * 1.852 * 1000) * cos(brg * kD2R);
-      const double y_r = (dist * 1.852 * 1000) * sin(brg * kD2R);
-      const double vx_int = cos(s.hdg * kD2R) * s.tas;
-      const double vy_int = sin(s.hdg * kD2R) * s.tas;
-      const double vx_r = vx_int - vx, vy_r = vy_int - vy;
-      const double track = atan2(vy_r, vx_r);
-      o0 = x_r; o1 = y_r; o2 = vx_r; o3 = vy_r; o4 = cos(track); o5 = sin(track); o6 = dmat;
-      intr = dist < 4;                                        // _check_intrusion :280-281
-      L.d[lane] = dmat;
-    } else {
-      L.d[lane] = __builtin_inf();
-    }
-  } else if constexpr (KIND == BSG_ENV_VERTICAL_CR) {
-    if (ok && j > 0) {
-      // vertical_cr_env.py:133-156
-      const double lat0 = L.lat[base], lon0 = L.lon[base], hdg0 = L.hdg[base];
-      const double alt0 = L.alt[base], vs0 = L.vs[base], gs0 = L.tas[base];
-      double qdr, dis;
-      kwikqdrdist(lat0, lon0, s.lat, s.lon, &qdr, &dis);
-      const double bearing = bound180(hdg0 - qdr);
-      const double hd = hdg0 - s.hdg;
-      o0 = dis * 1.852;                                       // intruder_distance (km)
-      o1 = cos(bearing * kD2R);
-      o2 = sin(bearing * kD2R);
-      o3 = s.alt - alt0;                                      // altitude_difference
-      o4 = -cos(hd * kD2R) * s.tas;                           // x_difference_speed
-      o5 = gs0 - sin(hd * kD2R) * s.tas;                      // y_difference_speed
-      o6 = s.vs - vs0;                                        // z_difference_speed
-      intr = (dis < 5) && (fabs(alt0 - s.alt) < 1000 * 0.3048);   // :235-237
-    }
+    L.d[lane] = sortkey;
   }
   __syncthreads();
+  int rank = 0x7fffffff;
   if constexpr (KIND == BSG_ENV_MERGE) {
-    if (ok && j > 0) {
-      const double dj = L.d[lane];
-      int r = 0;
-      for (int k = 1; k < N; ++k) {
-        const double dk = L.d[base + k];
-        r += (dk < dj) || (dk == dj && k < j);
-      }
-      rank = r;
-    }
+    if (ok && j > 0) rank = rank_in_group(L, base, lane, j, N);
   }
   const uint64_t ib = group_bits<GS>(__ballot(ok && stepping && intr), g);
   const int nintr = __popcll(ib);
 
-  // CD: StateBased all-pairs CPA row of aircraft j
+  // CD: StateBased all-pairs CPA, wave-compacted (see cd_candidate / cd_pair)
   uint64_t cmask = 0, lmask = 0;
   double tmax = 0.0, msep = __builtin_inf();
-  if (p.cfg.compute_cd && KIND != BSG_ENV_DESCENT) {
-    if (ok) cd_row<GS>(L, base, j, N, &cmask, &lmask, &tmax, &msep);
-    msep = group_min<GS>(ok ? msep : __builtin_inf());
+  if (KIND != BSG_ENV_DESCENT && p.cfg.compute_cd) {
+    __shared__ unsigned short cd_list[64 * (GS > 1 ? GS - 1 : 1)];
+    L.cm[lane] = 0ull;
+    L.lm[lane] = 0ull;
+    L.tmax[lane] = 0ull;                                   // bits of +0.0
+    L.gmin[lane] = bits(__builtin_inf());
+    // phase 1: candidate pairs of row j (no transcendentals)
+    uint64_t cand = 0;
+    if (ok) {
+      const double lati = L.lat[lane], ui = L.u[lane], vi = L.v[lane];
+      for (int k = 0; k < N; ++k) {
+        const int lk = base + k;
+        const double dlat = (L.lat[lk] - lati) * kD2R;
+        const double du = L.u[lk] - ui, dv = L.v[lk] - vi;
+        double dv2 = du * du + dv * dv;
+        dv2 = fabs(dv2) < 1e-6 ? 1e-6 : dv2;
+        if (k != j && cd_candidate(dlat, dv2)) cand |= 1ull << k;
+      }
+    }
+    const int cnt = __popcll(cand);
+    int incl = cnt;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const int t = __shfl_up(incl, off, 64);
+      if (lane >= off) incl += t;
+    }
+    const int total = __shfl(incl, 63, 64);
+    int pos = incl - cnt;
+    for (uint64_t c = cand; c; c &= c - 1) {
+      const int k = __builtin_ctzll(c);
+      cd_list[pos++] = (unsigned short)((lane << 6) | (base + k));
+    }
+    __syncthreads();
+    // phase 2: dense exact StateBased over the surviving pairs
+    for (int t = lane; t < total; t += 64) {
+      const int pr = cd_list[t];
+      const int li = pr >> 6, lk = pr & 63;
+      const CdOut r = cd_pair(L, li, lk);
+      if (r.inside) {
+        atomicMin(&L.gmin[li / GS], bits(r.dist));
+        const int kk = lk - (li / GS) * GS;
+        if (r.confl) atomicOr(&L.cm[li], 1ull << kk);
+        if (r.lossep) atomicOr(&L.lm[li], 1ull << kk);
+        if (r.confl && r.tcpa > 0.0) atomicMax(&L.tmax[li], bits(r.tcpa));
+      }
+    }
+    __syncthreads();
+    cmask = L.cm[lane];
+    lmask = L.lm[lane];
+    tmax = __longlong_as_double((long long)L.tmax[lane]);
+    msep = __longlong_as_double((long long)L.gmin[g]);
   }
 
   // lane 0: scalar obs, reward, termination (per env)
-  double s0 = 0, s1 = 0, s2 = 0, s3 = 0, s4 = 0;
+  double sc[5] = {0, 0, 0, 0, 0};
+  float reward = 0.0f;
+  bool term = false, trunc = false, done = false;
   if (ok && j == 0) {
-    if constexpr (KIND == BSG_ENV_MERGE) {
-      // merge_env.py:175-191 (obs uses wpt_reach BEFORE the reward update)
-      const int wr = ev.wpt_reach;
-      double wqdr, wdist;
-      kwikqdrdist(s.lat, s.lon, p.cfg.wpt_lat[wr == 0 ? 0 : 1], p.cfg.wpt_lon[wr == 0 ? 0 : 1],
-                  &wqdr, &wdist);
-      const double drift = bound180(s.hdg - wqdr);
-      s0 = s.tas; s1 = cos(drift * kD2R); s2 = (double)wr; s3 = sin(drift * kD2R); s4 = wdist / 250;
-      if (stepping) {
-        // _check_waypoint :257-268
-        int reach = 0, d = 0;
+    double wdist = 0, drift = 0, rwd = 0;
+    own_obs<KIND>(p, L, lane, ev, sc, &wdist, &drift, &rwd);
+    if (stepping) {
+      double r;
+      int d = 0;
+      if constexpr (KIND == BSG_ENV_MERGE) {
+        // _check_waypoint :257-268 ; _check_drift :270-273 ; _check_intrusion :275-284
+        const int wr = ev.wpt_reach;
+        int reach = 0;
         if (wdist < 10 && wr != 1) { ev.wpt_reach = 1; ev.faf_reached = 1; reach = 1; }
         else if (wdist < 2 * 10 && wr == 1) { ev.faf_reached = 2; d = 1; }
-        // _check_drift :270-273 ; _check_intrusion :275-284
         const double dd = fabs(drift * kD2R);
-        const double r = ((double)reach + dd * -0.1) + (double)(nintr * -1);
+        r = ((double)reach + dd * -0.1) + (double)(nintr * -1);
         ev.drift_sum += dd;
-        ev.total_intr += nintr;
-        ev.total_reward += r;
-        reward = (float)r;
-        term = d != 0;
-      }
-    } else {
-      // vertical_cr_env.py:129-181 / descent_env.py:100-117
-      const double altitude = s.alt, vz = s.vs;
-      const double runway_distance = 200 - kwikdist(52.0, 4.0, s.lat, s.lon) * 1.852;
-      s0 = (altitude - 1500) / 3000; s1 = (vz - 0) / 5; s2 = (ev.target_alt - 1500) / 3000;
-      s3 = (runway_distance - 100) / 200;
-      if (stepping) {
+      } else {
         // _get_reward (vertical_cr_env.py:213-228 / descent_env.py:128-144)
+        const double altitude = L.alt[lane];
         double alt_pen;
-        int d = 0;
-        if (runway_distance > 0 && altitude > 0) {
+        if (rwd > 0 && altitude > 0) {
           alt_pen = fabs(ev.target_alt - altitude) * (-5.0 / 3000);
         } else if (altitude <= 0) {
           alt_pen = -100; ev.final_alt = -100; d = 1;
         } else {
           alt_pen = altitude * (-50.0 / 3000); ev.final_alt = altitude; d = 1;
         }
-        const double r = alt_pen + (double)(nintr * -50);
-        ev.total_intr += nintr;
-        ev.total_reward += r;
-        reward = (float)r;
-        term = d != 0;
+        r = alt_pen + (double)(nintr * -50);
       }
-    }
-    if (stepping) {
+      ev.total_intr += nintr;
+      ev.total_reward += r;
+      reward = (float)r;
+      term = d != 0;
       ev.step_count += 1;
       trunc = p.cfg.max_episode_steps > 0 && ev.step_count >= p.cfg.max_episode_steps;
       done = term || trunc;
@@ -538,50 +768,8 @@ __global__ __launch_bounds__(64) void step_kernel(KParams p) {
     float* obs = b.obs + (size_t)e * O;
     float* fobs = same_step_reset ? b.final_obs + (size_t)e * O : nullptr;
     float* lrn = (b.learner && !same_step_reset) ? b.learner + (size_t)e * (O + 3) : nullptr;
-    auto put = [&](int off, double v) {
-      obs[off] = (float)v;
-      if (fobs) fobs[off] = (float)v;
-      if (lrn) lrn[off] = (float)v;
-    };
-    if constexpr (KIND == BSG_ENV_MERGE) {
-      const int K = p.K;
-      if (j == 0) {
-        put(0, s0);                         // airspeed
-        put(1, s1);                         // cos(drift)
-        put(2 + 2 * K, s2);                 // faf_reached
-        put(3 + 2 * K, s3);                 // sin(drift)
-        put(4 + 5 * K, s4);                 // waypoint_dist
-      } else if (rank < K) {
-        put(2 + rank, o4);                  // cos(track)
-        put(2 + K + rank, o6 / 250);        // distances
-        put(4 + 2 * K + rank, o5);          // sin(track)
-        put(4 + 3 * K + rank, o2 / 150);    // vx_r
-        put(4 + 4 * K + rank, o3 / 150);    // vy_r
-        put(5 + 5 * K + rank, o0 / 1000000);// x_r
-        put(5 + 6 * K + rank, o1 / 1000000);// y_r
-        b.topk[(size_t)e * K + rank] = j;
-      }
-    } else if constexpr (KIND == BSG_ENV_VERTICAL_CR) {
-      const int NI = N - 1;
-      if (j == 0) {
-        put(0, s0);                         // altitude
-        put(1 + 3 * NI, s3);                // runway_distance
-        put(2 + 4 * NI, s2);                // target_altitude
-        put(3 + 4 * NI, s1);                // vz
-      } else {
-        const int i = j - 1;
-        put(1 + i, o3 / 3000);              // altitude_difference
-        put(1 + NI + i, o1);                // cos_difference_pos
-        put(1 + 2 * NI + i, o0 / 200);      // intruder_distance
-        put(2 + 3 * NI + i, o2);            // sin_difference_pos
-        put(4 + 4 * NI + i, o4 / 150);      // x_difference_speed
-        put(4 + 5 * NI + i, o5 / 150);      // y_difference_speed
-        put(4 + 6 * NI + i, o6);            // z_difference_speed
-      }
-    } else {
-      if (j == 0) { put(0, s0); put(1, s3); put(2, s2); put(3, s1); }
-    }
     if (j == 0) {
+      write_own_obs<KIND>(obs, fobs, lrn, K, N, sc);
       b.reward[e] = reward;
       b.terminated[e] = term ? 1 : 0;
       b.truncated[e] = trunc ? 1 : 0;
@@ -604,6 +792,11 @@ __global__ __launch_bounds__(64) void step_kernel(KParams p) {
           info[3] = 0.0;
         }
       }
+    } else {
+      write_lane_obs<KIND>(obs, fobs, lrn, K, N, j, rank, o);
+      if constexpr (KIND == BSG_ENV_MERGE) {
+        if (rank < K) b.topk[(size_t)e * K + rank] = j;
+      }
     }
     if (p.cfg.compute_cd && KIND != BSG_ENV_DESCENT) {
       b.conf_mask[a] = cmask;
@@ -616,99 +809,38 @@ __global__ __launch_bounds__(64) void step_kernel(KParams p) {
 
   // ---------------- C: SAME_STEP autoreset ---------------------------------------------
   if (p.cfg.autoreset_mode == BSG_AUTORESET_SAME_STEP && __syncthreads_or(same_step_reset)) {
-    double tgt = ev.target_alt;
-    if (same_step_reset && ok) {
-      if constexpr (KIND == BSG_ENV_MERGE) spawn_merge(p, e, j, ev.episode, s);
-      else if constexpr (KIND == BSG_ENV_VERTICAL_CR) spawn_vertical(p, e, j, ev.episode, s, &tgt);
-      else {
-        double alt_init;
-        draw_alts(p, e, ev.episode, TAG_DESC, &alt_init, &tgt);
-        cre(s, 52.0, 4.0, 0.0, alt_init, 150.0);
+    {
+      AC s = {};
+      double tgt = ev.target_alt;
+      if (same_step_reset && ok) {
+        spawn<KIND>(p, e, j, ev.episode, s, &tgt);
+        store_ac(b, a, s);
       }
+      if (same_step_reset && j == 0) reset_scalars(ev, tgt);
+      if (same_step_reset) stage(L, lane, s);
     }
-    if (same_step_reset && j == 0) reset_scalars(ev, tgt);
-    stage(L, lane, ok, s);
     __syncthreads();
+    sortkey = __builtin_inf();
+    if (same_step_reset && ok && j > 0 && KIND != BSG_ENV_DESCENT) lane_obs<KIND>(L, base, lane, o, &sortkey);
     if constexpr (KIND == BSG_ENV_MERGE) {
-      const double lat0 = L.lat[base], lon0 = L.lon[base], hdg0 = L.hdg[base], tas0 = L.tas[base];
-      if (same_step_reset && ok && j > 0) {
-        const double dmat = kwikdist_mat(lat0, lon0, s.lat, s.lon);
-        double brg, dist;
-        kwikqdrdist(lat0, lon0, s.lat, s.lon, &brg, &dist);
-        const double vx = cos(hdg0 * kD2R) * tas0, vy = sin(hdg0 * kD2R) * tas0;
-        const double vx_r = cos(s.hdg * kD2R) * s.tas - vx, vy_r = sin(s.hdg * kD2R) * s.tas - vy;
-        const double track = atan2(vy_r, vx_r);
-        o0 = (dist * 1.852 * 1000) * cos(brg * kD2R); o1 = (dist * 1.852 * 1000) * sin(brg * kD2R);
-        o2 = vx_r; o3 = vy_r; o4 = cos(track); o5 = sin(track); o6 = dmat;
-        L.d[lane] = dmat;
-      } else {
-        L.d[lane] = __builtin_inf();
-      }
-    } else if constexpr (KIND == BSG_ENV_VERTICAL_CR) {
-      if (same_step_reset && ok && j > 0) {
-        const double lat0 = L.lat[base], lon0 = L.lon[base], hdg0 = L.hdg[base];
-        const double alt0 = L.alt[base], vs0 = L.vs[base], gs0 = L.tas[base];
-        double qdr, dis;
-        kwikqdrdist(lat0, lon0, s.lat, s.lon, &qdr, &dis);
-        const double bearing = bound180(hdg0 - qdr);
-        const double hd = hdg0 - s.hdg;
-        o0 = dis * 1.852; o1 = cos(bearing * kD2R); o2 = sin(bearing * kD2R); o3 = s.alt - alt0;
-        o4 = -cos(hd * kD2R) * s.tas; o5 = gs0 - sin(hd * kD2R) * s.tas; o6 = s.vs - vs0;
-      }
+      if (same_step_reset) L.d[lane] = sortkey;
     }
     __syncthreads();
     if (same_step_reset && ok) {
       float* obs = b.obs + (size_t)e * O;
       float* lrn = b.learner ? b.learner + (size_t)e * (O + 3) : nullptr;
-      auto put = [&](int off, double v) {
-        obs[off] = (float)v;
-        if (lrn) lrn[off] = (float)v;
-      };
-      if constexpr (KIND == BSG_ENV_MERGE) {
-        const int K = p.K;
-        if (j == 0) {
-          double wqdr, wdist;
-          kwikqdrdist(s.lat, s.lon, p.cfg.wpt_lat[0], p.cfg.wpt_lon[0], &wqdr, &wdist);
-          const double drift = bound180(s.hdg - wqdr);
-          put(0, s.tas); put(1, cos(drift * kD2R)); put(2 + 2 * K, 0.0);
-          put(3 + 2 * K, sin(drift * kD2R)); put(4 + 5 * K, wdist / 250);
-        } else {
-          const double dj = L.d[lane];
-          int r = 0;
-          for (int k = 1; k < N; ++k) {
-            const double dk = L.d[base + k];
-            r += (dk < dj) || (dk == dj && k < j);
-          }
-          if (r < K) {
-            put(2 + r, o4); put(2 + K + r, o6 / 250); put(4 + 2 * K + r, o5);
-            put(4 + 3 * K + r, o2 / 150); put(4 + 4 * K + r, o3 / 150);
-            put(5 + 5 * K + r, o0 / 1000000); put(5 + 6 * K + r, o1 / 1000000);
-          }
-        }
-      } else if constexpr (KIND == BSG_ENV_VERTICAL_CR) {
-        const int NI = N - 1;
-        if (j == 0) {
-          const double rd = 200 - kwikdist(52.0, 4.0, s.lat, s.lon) * 1.852;
-          put(0, (s.alt - 1500) / 3000); put(1 + 3 * NI, (rd - 100) / 200);
-          put(2 + 4 * NI, (ev.target_alt - 1500) / 3000); put(3 + 4 * NI, (s.vs - 0) / 5);
-        } else {
-          const int i = j - 1;
-          put(1 + i, o3 / 3000); put(1 + NI + i, o1); put(1 + 2 * NI + i, o0 / 200);
-          put(2 + 3 * NI + i, o2); put(4 + 4 * NI + i, o4 / 150);
-          put(4 + 5 * NI + i, o5 / 150); put(4 + 6 * NI + i, o6);
-        }
+      if (j == 0) {
+        double wdist, drift, rwd;
+        own_obs<KIND>(p, L, lane, ev, sc, &wdist, &drift, &rwd);
+        write_own_obs<KIND>(obs, nullptr, lrn, K, N, sc);
       } else {
-        if (j == 0) {
-          const double rd = 200 - kwikdist(52.0, 4.0, s.lat, s.lon) * 1.852;
-          put(0, (s.alt - 1500) / 3000); put(1, (rd - 100) / 200);
-          put(2, (ev.target_alt - 1500) / 3000); put(3, (s.vs - 0) / 5);
-        }
+        int r = 0x7fffffff;
+        if constexpr (KIND == BSG_ENV_MERGE) r = rank_in_group(L, base, lane, j, N);
+        write_lane_obs<KIND>(obs, nullptr, lrn, K, N, j, r, o);
       }
     }
   }
 
-  // ---------------- store ----------------------------------------------------------------
-  if (active && ok) store_ac(b, (int)a, s);
   if (active && j == 0) store_env(b, e, ev);
 }
 

@@ -338,6 +338,7 @@ class MergeOracle(_Base):
             res["conf_mask"] = _rows_to_u64(cd["swconfl"])
             res["los_mask"] = _rows_to_u64(cd["swlos"])
             res["tcpamax"] = cd["tcpamax"]
+            res["min_sep"] = cd["min_sep"]
             res["cd"] = cd
         return res
 
@@ -506,6 +507,7 @@ class VerticalOracle(_VertBase):
             res["conf_mask"] = _rows_to_u64(cd["swconfl"])
             res["los_mask"] = _rows_to_u64(cd["swlos"])
             res["tcpamax"] = cd["tcpamax"]
+            res["min_sep"] = cd["min_sep"]
             res["cd"] = cd
         return res
 
@@ -603,6 +605,7 @@ def _cd_fill(o, res, mask):
     res["conf_mask"] = np.where(mask[:, None], _rows_to_u64(cd["swconfl"]), res["conf_mask"])
     res["los_mask"] = np.where(mask[:, None], _rows_to_u64(cd["swlos"]), res["los_mask"])
     res["tcpamax"] = np.where(mask[:, None], cd["tcpamax"], res["tcpamax"])
+    res["min_sep"] = np.where(mask, cd["min_sep"], res["min_sep"])
 
 
 _Base._cd_into = lambda self, res, mask: _cd_fill(self, res, mask)

@@ -417,8 +417,14 @@ def statebased_detect(lat, lon, alt, trk, gs, vs, rpz=RPZ, hpz=HPZ, dtlookahead=
     inconf = np.any(swconfl, -1)
     tcpamax = np.max(tcpa * swconfl, -1)
     swlos = (dist < rpz) & (np.abs(dalt) < hpz)
+    # minimum separation among the pairs inside the StateBased horizon (the pairs whose
+    # conflict state can be true): dist <= (RPZ + DTLOOKAHEAD*vrel)(1+1e-9) + 1 m
+    horizon = (rpz + dtlookahead * vrel) * (1.0 + 1e-9) + 1.0
+    inside = (dist <= horizon) & ~eye
+    min_sep = np.min(np.where(inside, dist, np.inf), axis=(-2, -1))
     return dict(swconfl=swconfl, swlos=swlos, inconf=inconf, tcpamax=tcpamax,
-                dist=dist, tcpa=tcpa, dcpa2=dcpa2, tinconf=tinconf, toutconf=toutconf)
+                dist=dist, tcpa=tcpa, dcpa2=dcpa2, tinconf=tinconf, toutconf=toutconf,
+                vrel=vrel, min_sep=min_sep)
 
 
 # --------------------------------------------------------------------------------------

@@ -130,6 +130,11 @@ def _compare_step(b, r, N, kind, t):
         assert np.array_equal(b.conf_mask.cpu().numpy().astype(np.uint64), r["conf_mask"]), t
         assert np.array_equal(b.los_mask.cpu().numpy().astype(np.uint64), r["los_mask"]), t
         close(b.tcpamax.cpu().numpy(), r["tcpamax"], f"tcpamax t={t}", atol=TCPA_ATOL)
+        ms_g = b.min_sep.cpu().numpy().astype(np.float64)
+        ms_r = r["min_sep"]
+        assert np.array_equal(np.isinf(ms_g), np.isinf(ms_r)), t
+        fin = np.isfinite(ms_r)
+        close(ms_g[fin], ms_r[fin], f"min_sep t={t}")
     if kind == "merge":
         live = ~r["was_reset"]
         assert np.array_equal(b.topk.cpu().numpy()[live], r["topk"][live]), t
