@@ -106,34 +106,44 @@ def main():
 
     import torch
     import torch.distributed as dist
-    from bluesky_gym import config, core
-    from bluesky_gym import _native as nat
+    from bluesky_gym.parallel import ShardedVectorEnv
+    from bluesky_gym.vector import MergeVectorEnv
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # BENCH_BACKEND=gloo rehearses the multi-rank path on fewer GPUs than ranks (test only)
+    backend = os.environ.get("BENCH_BACKEND", "nccl")
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        torch.cuda.set_device(local % torch.cuda.device_count())
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", torch.cuda.current_device()))
+        else:
+            dist.init_process_group(backend)
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
     E = args.envs if not args.total_envs else args.total_envs // world
     gather = world > 1 and not args.no_gather
-    batch = core.DeviceBatch(config.merge_config(num_ac=args.num_ac), E,
-                             autoreset=nat.AUTORESET_NEXT_STEP, compute_cd=not args.no_cd,
-                             seed=1234 + 7919 * rank, learner=gather)
-    batch.reset()
+    make_local = lambda **kw: MergeVectorEnv(num_ac=args.num_ac, seed=1234,  # noqa: E731
+                                             compute_cd=not args.no_cd, **kw)
+    if gather:
+        env = ShardedVectorEnv(make_local, world * E, overlap=(backend == "nccl"))
+        batch = env.local.batch
+        env.reset()
+    else:
+        venv = make_local(num_envs=E, env_offset=rank * E)
+        batch = venv.batch
+        venv.reset()
     gen = torch.Generator(device=dev)
     gen.manual_seed(17 + rank)
     bank = torch.rand((16, E, 2), dtype=torch.float64, device=dev, generator=gen) * 2 - 1
-    if gather:
-        gathered = torch.empty((world * E, batch.obs_dim + 3), dtype=torch.float32, device=dev)
 
     def one(k):
-        batch.step(bank[k % 16])
         if gather:
-            dist.all_gather_into_tensor(gathered, batch.learner)
+            env.step(bank[k % 16])
+        else:
+            batch.step(bank[k % 16])
 
     for k in range(args.warmup):
         one(k)
@@ -185,7 +195,8 @@ def main():
                             + (", RCCL all_gather of [E, obs+3] fp32 per step" if gather else ""),
                 "envs_per_gpu": E,
                 "num_ac": N,
-                "parallelism": f"env-shard x{world}" + (" + all_gather" if gather else ""),
+                "parallelism": f"env-shard x{world}" + (" + RCCL all_gather (overlapped)" if gather else ""),
+                "backend": backend if world > 1 else None,
             },
             "roofline": {
                 "bound": "hbm",

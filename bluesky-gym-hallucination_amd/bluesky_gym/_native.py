@@ -43,7 +43,7 @@ class BsgConfig(C.Structure):
         ("device", C.c_int32),
         ("seed", C.c_uint64),
         ("route_len", C.c_int32),
-        ("_pad0", C.c_int32),
+        ("env_offset", C.c_int32),
         ("route_lat", C.c_double * MAX_ROUTE),
         ("route_lon", C.c_double * MAX_ROUTE),
         ("route_next_qdr", C.c_double * MAX_ROUTE),

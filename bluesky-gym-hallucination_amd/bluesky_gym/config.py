@@ -60,7 +60,7 @@ class EnvKindConfig:
     simdt: float
     max_episode_steps: int
 
-    def to_c(self, num_envs, autoreset, compute_cd, seed, device) -> nat.BsgConfig:
+    def to_c(self, num_envs, autoreset, compute_cd, seed, device, env_offset=0) -> nat.BsgConfig:
         c = nat.BsgConfig()
         c.abi_version = nat.ABI_VERSION
         c.env_kind = self.kind
@@ -74,6 +74,7 @@ class EnvKindConfig:
         c.compute_cd = int(bool(compute_cd))
         c.device = int(device)
         c.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+        c.env_offset = int(env_offset)
         if self.kind == nat.ENV_MERGE:
             # ADDWPT FIX ; DEST RWY (merge_env.py:155-156)
             c.route_len = 2

@@ -19,7 +19,7 @@ F64_ENV = ("total_reward", "drift_sum", "target_alt", "final_altitude")
 
 class DeviceBatch:
     def __init__(self, cfg: EnvKindConfig, num_envs: int, *, autoreset=nat.AUTORESET_NEXT_STEP,
-                 compute_cd=True, seed=0, device=None, learner=False):
+                 compute_cd=True, seed=0, device=None, learner=False, env_offset=0):
         if not torch.cuda.is_available():
             raise nat.BsgError("bluesky_gym needs a HIP device (MI355X); none is visible")
         self.lib = nat.load_library()
@@ -37,7 +37,9 @@ class DeviceBatch:
             raise nat.BsgError(f"invalid env config {cfg}")
         self.act_dim = self.lib.bsg_action_dim(cfg.kind)
         self.spawn_width = self.lib.bsg_spawn_width(cfg.kind, cfg.num_ac)
-        ccfg = cfg.to_c(self.E, autoreset, self.compute_cd, seed, self.device.index)
+        self.env_offset = int(env_offset)
+        self.seed = int(seed)
+        ccfg = cfg.to_c(self.E, autoreset, self.compute_cd, seed, self.device.index, env_offset)
         ctx = C.c_void_p()
         nat.check(self.lib.bsg_create(C.byref(ccfg), C.byref(ctx)), "bsg_create")
         self._ctx = ctx

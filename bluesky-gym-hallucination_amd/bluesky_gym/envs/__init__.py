@@ -1,0 +1,6 @@
+"""Env classes (bluesky_gym/envs/__init__.py:1-7 of the reference re-exports all)."""
+from .descent_env import DescentEnv  # noqa: F401
+from .merge_env import MergeEnv  # noqa: F401
+from .vertical_cr_env import VerticalCREnv  # noqa: F401
+from ._out_of_scope import (HorizontalCREnv, PlanWaypointEnv, SectorCREnv,  # noqa: F401
+                            StaticObstacleEnv)

@@ -1,0 +1,2 @@
+"""Out of scope (see envs/_out_of_scope.py)."""
+from ._out_of_scope import HorizontalCREnv  # noqa: F401

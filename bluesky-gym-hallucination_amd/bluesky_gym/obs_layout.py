@@ -1,0 +1,61 @@
+"""Observation layouts: the reference observation_space keys, their sizes and the
+flat (sorted-key) offsets the HIP kernel writes.
+
+merge_env.py:59-74, vertical_cr_env.py:67-83, descent_env.py:53-60.  Gymnasium's
+spaces.Dict sorts its keys, and SB3's MultiInputPolicy flattens in that order, so the
+flat fp32 row of libbsg is laid out in sorted-key order.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import _native as nat
+
+
+def merge_sizes(k):
+    return {"airspeed": 1, "cos(drift)": 1, "cos(track)": k, "distances": k,
+            "faf_reached": 1, "sin(drift)": 1, "sin(track)": k, "vx_r": k, "vy_r": k,
+            "waypoint_dist": 1, "x_r": k, "y_r": k}
+
+
+def vertical_sizes(ni):
+    return {"altitude": 1, "altitude_difference": ni, "cos_difference_pos": ni,
+            "intruder_distance": ni, "runway_distance": 1, "sin_difference_pos": ni,
+            "target_altitude": 1, "vz": 1, "x_difference_speed": ni,
+            "y_difference_speed": ni, "z_difference_speed": ni}
+
+
+def descent_sizes():
+    return {"altitude": 1, "runway_distance": 1, "target_altitude": 1, "vz": 1}
+
+
+# reference Box bounds (low, high) per key
+_BOUNDS = {"cos(drift)": (-1, 1), "sin(drift)": (-1, 1), "faf_reached": (0, 1)}
+
+
+class ObsLayout:
+    def __init__(self, kind, num_ac, num_ac_state):
+        if kind == nat.ENV_MERGE:
+            sizes = merge_sizes(num_ac_state)
+        elif kind == nat.ENV_VERTICAL_CR:
+            sizes = vertical_sizes(num_ac - 1)
+        else:
+            sizes = descent_sizes()
+        self.keys = tuple(sorted(sizes))
+        self.sizes = {k: sizes[k] for k in self.keys}
+        off = 0
+        self.slices = {}
+        for k in self.keys:
+            self.slices[k] = slice(off, off + self.sizes[k])
+            off += self.sizes[k]
+        self.dim = off
+
+    def split(self, flat) -> dict:
+        """[..., dim] -> {key: [..., size]} (float64 numpy, like the reference obs)."""
+        flat = np.asarray(flat, np.float64)
+        return {k: flat[..., s] for k, s in self.slices.items()}
+
+    def observation_space(self, spaces):
+        return spaces.Dict({k: spaces.Box(*_BOUNDS.get(k, (-np.inf, np.inf)), shape=(n,),
+                                          dtype=np.float64)
+                            for k, n in self.sizes.items()})

@@ -1,0 +1,159 @@
+"""Gymnasium VectorEnv front-ends of the device batch (the ``vector_entry_point`` of
+MergeEnv-v0 / VerticalCREnv-v0 / DescentEnv-v0, registered by ``register_envs``).
+
+``gym.make_vec("MergeEnv-v0", num_envs=4096, vectorization_mode="vector_entry_point",
+num_ac=32)`` returns a :class:`MergeVectorEnv` whose E envs live on one HIP device and
+advance with one kernel launch per ``step``.
+
+Autoreset follows Gymnasium >= 1.0's default NEXT_STEP mode: the step after a
+terminated/truncated step resets that env (its action is ignored, reward 0).
+Observations come back as the reference's Dict of float64 arrays, batched [E, k];
+``step_tensors`` returns the device-resident fp32 views for zero-copy learners.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import _gym, _native as nat, config as cfgmod, spawn as spawnmod
+from .core import DeviceBatch
+from .obs_layout import ObsLayout
+
+_INFO_KEYS = {
+    nat.ENV_MERGE: ("total_reward", "faf_reach", "average_drift", "total_intrusions"),
+    nat.ENV_VERTICAL_CR: ("total_reward", "total_intrusions", "final_altitude"),
+    nat.ENV_DESCENT: ("total_reward", "final_altitude"),
+}
+
+
+class BlueSkyVectorEnv(_gym.VectorEnv):
+    """E independent envs of one kind on one device."""
+
+    metadata = {"autoreset_mode": "NextStep", "render_modes": []}
+
+    def __init__(self, kind_cfg: cfgmod.EnvKindConfig, num_envs: int, *, device=None, seed=0,
+                 compute_cd=True, spawn="device", autoreset=nat.AUTORESET_NEXT_STEP,
+                 env_offset=0, learner=False):
+        self.kind_cfg = kind_cfg
+        self.num_envs = int(num_envs)
+        self.device = device
+        self.compute_cd = compute_cd
+        self.spawn_mode = spawn
+        self.autoreset = autoreset
+        self.env_offset = env_offset
+        self.learner = learner
+        self.layout = ObsLayout(kind_cfg.kind, kind_cfg.num_ac, kind_cfg.num_ac_state)
+        self.single_observation_space = self.layout.observation_space(_gym.spaces)
+        act = 2 if kind_cfg.kind == nat.ENV_MERGE else 1
+        self.single_action_space = _gym.spaces.Box(-1, 1, shape=(act,), dtype=np.float64)
+        self.observation_space = _gym.spaces.Dict(
+            {k: _gym.spaces.Box(-np.inf, np.inf, shape=(self.num_envs, n), dtype=np.float64)
+             for k, n in self.layout.sizes.items()})
+        self.action_space = _gym.spaces.Box(-1, 1, shape=(self.num_envs, act), dtype=np.float64)
+        self._seed = seed
+        self._host_rngs = None
+        self.batch = DeviceBatch(kind_cfg, self.num_envs, autoreset=autoreset, compute_cd=compute_cd,
+                                 seed=seed, device=device, learner=learner, env_offset=env_offset)
+
+    # ---------------------------------------------------------------- spawns
+    def _host_spawn(self, mask=None):
+        """Per-env host RNG streams consuming draws like the reference (spawn='host')."""
+        if self._host_rngs is None:
+            ss = np.random.SeedSequence(self._seed)
+            self._host_rngs = [np.random.RandomState(s.generate_state(1)[0])
+                               for s in ss.spawn(self.num_envs)]
+        k = self.kind_cfg
+        rows = []
+        for e in range(self.num_envs):
+            if mask is not None and not mask[e]:
+                rows.append(np.zeros(self.batch.spawn_width))
+                continue
+            rs = self._host_rngs[e]
+            if k.kind == nat.ENV_MERGE:
+                rows.append(spawnmod.merge_spawn(k.num_ac, rs))
+            elif k.kind == nat.ENV_VERTICAL_CR:
+                rows.append(spawnmod.vertical_spawn(k.num_ac - 1, rs))
+            else:
+                rows.append(spawnmod.descent_spawn(rs))
+        return torch.from_numpy(np.stack(rows))
+
+    # ---------------------------------------------------------------- API
+    def reset(self, *, seed=None, options=None):
+        if seed is not None and seed != self._seed:
+            self._seed = seed
+            self._host_rngs = None
+            self.batch.close()
+            self.batch = DeviceBatch(self.kind_cfg, self.num_envs, autoreset=self.autoreset,
+                                     compute_cd=self.compute_cd, seed=seed, device=self.device,
+                                     learner=self.learner, env_offset=self.env_offset)
+        sp = self._host_spawn() if self.spawn_mode == "host" else None
+        self.batch.reset(spawn=sp)
+        return self.layout.split(self.batch.obs.cpu().numpy()), self._infos(done=None)
+
+    def step_tensors(self, actions):
+        """Device path: actions [E, A] (torch, any device) -> device views
+        (obs fp32 [E, O], reward fp32 [E], terminated u8 [E], truncated u8 [E])."""
+        sp = None
+        if self.spawn_mode == "host":
+            pend = self.batch.envs["flags"].cpu().numpy() & 1
+            sp = self._host_spawn(pend.astype(bool)) if pend.any() else None
+        return self.batch.step(actions, spawn=sp)
+
+    def step(self, actions):
+        a = actions if isinstance(actions, torch.Tensor) else torch.as_tensor(np.asarray(actions, np.float64))
+        obs, rew, term, trunc = self.step_tensors(a)
+        term_np = term.cpu().numpy().astype(bool)
+        trunc_np = trunc.cpu().numpy().astype(bool)
+        return (self.layout.split(obs.cpu().numpy()), rew.cpu().numpy().astype(np.float64),
+                term_np, trunc_np, self._infos(done=term_np | trunc_np))
+
+    def _infos(self, done):
+        """Gymnasium dict-of-arrays infos: the reference's per-env info dict
+        (merge_env.py:238-244; vertical_cr_env.py:203-211; descent_env.py:119-126)."""
+        b = self.batch
+        tr = b.envs["total_reward"].cpu().numpy()
+        out = {}
+        kind = self.kind_cfg.kind
+        if kind == nat.ENV_MERGE:
+            cnt = b.envs["step_count"].cpu().numpy()
+            with np.errstate(invalid="ignore", divide="ignore"):
+                avg = b.envs["drift_sum"].cpu().numpy() / cnt
+            out = {"total_reward": tr, "faf_reach": b.envs["faf_reached"].cpu().numpy(),
+                   "average_drift": np.where(cnt > 0, avg, np.nan),
+                   "total_intrusions": b.envs["total_intrusions"].cpu().numpy()}
+        elif kind == nat.ENV_VERTICAL_CR:
+            out = {"total_reward": tr, "total_intrusions": b.envs["total_intrusions"].cpu().numpy(),
+                   "final_altitude": b.envs["final_altitude"].cpu().numpy()}
+        else:
+            out = {"total_reward": tr, "final_altitude": b.envs["final_altitude"].cpu().numpy()}
+        if b.compute_cd:
+            out["conflicts"] = (b.conf_mask.cpu().numpy() != 0).sum(axis=1)
+        if done is not None:
+            out["_final"] = done
+        return out
+
+    def close(self):
+        self.batch.close()
+
+
+class MergeVectorEnv(BlueSkyVectorEnv):
+    def __init__(self, num_envs=1, num_ac=20, num_ac_state=5, action_frequency=10, simdt=5.0,
+                 max_episode_steps=50, **kw):
+        super().__init__(cfgmod.merge_config(num_ac, num_ac_state, action_frequency, simdt,
+                                             max_episode_steps or 0), num_envs, **kw)
+
+
+class VerticalCRVectorEnv(BlueSkyVectorEnv):
+    def __init__(self, num_envs=1, num_intruders=5, action_frequency=30, simdt=1.0,
+                 max_episode_steps=300, num_ac=None, **kw):
+        if num_ac is not None:
+            num_intruders = num_ac - 1
+        super().__init__(cfgmod.vertical_config(num_intruders, action_frequency, simdt,
+                                                max_episode_steps or 0), num_envs, **kw)
+
+
+class DescentVectorEnv(BlueSkyVectorEnv):
+    def __init__(self, num_envs=1, action_frequency=30, simdt=1.0, max_episode_steps=300, **kw):
+        kw.pop("compute_cd", None)
+        super().__init__(cfgmod.descent_config(action_frequency, simdt, max_episode_steps or 0),
+                         num_envs, compute_cd=False, **kw)

@@ -141,6 +141,7 @@ int32_t bsg_create(const bsg_config* cfg, bsg_ctx** out) {
     return fail(BSG_E_INVALID_ARG, "bsg_create: invalid autoreset_mode%s%lld");
   if (cfg->route_len < 0 || cfg->route_len > BSG_MAX_ROUTE)
     return fail(BSG_E_INVALID_ARG, "bsg_create: route_len out of range%s%lld");
+  if (cfg->env_offset < 0) return fail(BSG_E_INVALID_ARG, "bsg_create: env_offset < 0%s%lld");
   if (cfg->env_kind == BSG_ENV_MERGE && cfg->route_len < 1)
     return fail(BSG_E_INVALID_ARG, "bsg_create: Merge needs the FIX/RWY route%s%lld");
   int ndev = 0;

@@ -302,7 +302,7 @@ __device__ __forceinline__ void spawn_merge(const KParams& p, int e, int j, uint
     brg = p.spawn[(size_t)e * W + 2 * j];
     dist = p.spawn[(size_t)e * W + 2 * j + 1];
   } else {
-    U4 r = philox4x32_10((uint32_t)e, episode, (uint32_t)j, TAG_MERGE, p.seed);
+    U4 r = philox4x32_10((uint32_t)(e + p.cfg.env_offset), episode, (uint32_t)j, TAG_MERGE, p.seed);
     double ua = u01_53(r.x, r.y), ub = u01_53(r.z, r.w);
     const double a = -15.0, b = 15.0;                       // +-D_HEADING (merge_env.py:27)
     brg = a + (b - a) * ua;
@@ -323,7 +323,7 @@ __device__ __forceinline__ void draw_alts(const KParams& p, int e, uint32_t epis
     *alt_init = p.spawn[(size_t)e * W + 0];
     *target = p.spawn[(size_t)e * W + 1];
   } else {
-    U4 r = philox4x32_10((uint32_t)e, episode, 0u, tag, p.seed);
+    U4 r = philox4x32_10((uint32_t)(e + p.cfg.env_offset), episode, 0u, tag, p.seed);
     int64_t ai = randint_u32(r.x, 2000, 4000);
     int64_t dt = randint_u32(r.y, -500, 500);
     *alt_init = (double)ai;
@@ -346,7 +346,7 @@ __device__ __forceinline__ void spawn_vertical(const KParams& p, int e, int j, u
     dpsi = q[0]; cpa = q[1]; tlosh = q[2]; dH = q[3];
   } else {
     // distributions of vertical_cr_env.py:187-195, Philox multiply-shift randint
-    U4 r = philox4x32_10((uint32_t)e, episode, (uint32_t)j, TAG_VERT, p.seed);
+    U4 r = philox4x32_10((uint32_t)(e + p.cfg.env_offset), episode, (uint32_t)j, TAG_VERT, p.seed);
     const double altitude = alt_init;
     dpsi = (double)randint_u32(r.x, 45, 315);
     cpa = (double)randint_u32(r.y, 0, 5);

@@ -63,7 +63,8 @@ typedef struct bsg_config {
   int32_t device;            /* HIP device ordinal */
   uint64_t seed;             /* Philox key for device-side spawns */
   int32_t route_len;         /* Merge intruder route (ADDWPT FIX; DEST RWY, merge_env.py:155-156) */
-  int32_t _pad0;
+  int32_t env_offset;        /* global id of env 0 of this batch (Philox counter); a shard of a
+                                multi-GPU job passes its first global env id */
   double route_lat[BSG_MAX_ROUTE];
   double route_lon[BSG_MAX_ROUTE];
   double route_next_qdr[BSG_MAX_ROUTE]; /* qdrdist bearing wp k -> k+1; -999 for the last */

@@ -1,0 +1,84 @@
+"""C-ABI checks that need no GPU: libbsg.so loads, exports every entry point declared in
+include/bsg.h, the ctypes mirror has the C struct layout (checked against gcc), and the
+shape helpers agree with the reference observation/action spaces."""
+import ctypes as C
+import os
+import re
+import subprocess
+
+import pytest
+
+from bluesky_gym import _native as nat
+from bluesky_gym.obs_layout import ObsLayout
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HDR = os.path.join(REPO, "include", "bsg.h")
+
+
+def declared_functions():
+    src = open(HDR).read()
+    return sorted(set(re.findall(r"^\s*(?:int32_t|const char\*)\s+(bsg_\w+)\s*\(", src, re.M)))
+
+
+def test_header_declares_the_ctypes_symbol_set():
+    assert declared_functions() == sorted(nat.EXPORTED_SYMBOLS)
+
+
+def test_library_exports_every_declared_symbol():
+    lib = nat.load_library()
+    out = subprocess.run(["nm", "-D", "--defined-only", nat.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    exported = set(re.findall(r"\bT (bsg_\w+)", out))
+    for sym in declared_functions():
+        assert sym in exported, sym
+        getattr(lib, sym)
+    assert lib.bsg_abi_version() == nat.ABI_VERSION
+
+
+def test_shape_helpers_match_reference_spaces():
+    lib = nat.load_library()
+    # merge_env.py:59-74 (K=5 -> 40), vertical_cr_env.py:67-83 (5 intruders -> 39), descent 4
+    assert lib.bsg_obs_dim(nat.ENV_MERGE, 20, 5) == 40
+    assert lib.bsg_obs_dim(nat.ENV_VERTICAL_CR, 6, 0) == 39
+    assert lib.bsg_obs_dim(nat.ENV_VERTICAL_CR, 32, 0) == 221
+    assert lib.bsg_obs_dim(nat.ENV_DESCENT, 1, 0) == 4
+    assert lib.bsg_obs_dim(nat.ENV_MERGE, 4, 5) < 0            # fewer intruders than K
+    assert lib.bsg_action_dim(nat.ENV_MERGE) == 2
+    assert lib.bsg_action_dim(nat.ENV_DESCENT) == 1
+    assert lib.bsg_spawn_width(nat.ENV_MERGE, 32) == 64
+    assert lib.bsg_spawn_width(nat.ENV_VERTICAL_CR, 6) == 22
+    for kind, n, k in ((nat.ENV_MERGE, 32, 5), (nat.ENV_VERTICAL_CR, 32, 0), (nat.ENV_DESCENT, 1, 0)):
+        assert ObsLayout(kind, n, k).dim == lib.bsg_obs_dim(kind, n, k)
+
+
+def test_ctypes_struct_layout_matches_c(tmp_path):
+    prog = tmp_path / "layout.c"
+    fields_c = [f[0] for f in nat.BsgConfig._fields_]
+    fields_b = [f[0] for f in nat.BsgBuffers._fields_]
+    lines = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{HDR}"', "int main(void){",
+             'printf("%zu %zu\\n", sizeof(bsg_config), sizeof(bsg_buffers));']
+    lines += [f'printf("%zu\\n", offsetof(bsg_config, {f}));' for f in fields_c]
+    lines += [f'printf("%zu\\n", offsetof(bsg_buffers, {f}));' for f in fields_b]
+    lines += ["return 0;}"]
+    prog.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-std=c99", "-o", str(exe), str(prog)], check=True)
+    vals = subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()
+    assert int(vals[0]) == C.sizeof(nat.BsgConfig)
+    assert int(vals[1]) == C.sizeof(nat.BsgBuffers)
+    offs = [int(v) for v in vals[2:]]
+    assert offs[:len(fields_c)] == [getattr(nat.BsgConfig, f).offset for f in fields_c]
+    assert offs[len(fields_c):] == [getattr(nat.BsgBuffers, f).offset for f in fields_b]
+
+
+def test_create_fails_cleanly_without_device_or_bad_config():
+    lib = nat.load_library()
+    from bluesky_gym import config
+    ctx = C.c_void_p()
+    bad = config.merge_config(num_ac=70).to_c(16, 1, 1, 0, 0)      # > 64 aircraft
+    rc = lib.bsg_create(C.byref(bad), C.byref(ctx))
+    assert rc == -1 and b"num_ac" in lib.bsg_last_error()
+    cfg = config.merge_config(num_ac=32).to_c(16, 1, 1, 0, 0)
+    cfg.abi_version = 99
+    assert lib.bsg_create(C.byref(cfg), C.byref(ctx)) == -1
+    assert lib.bsg_step(None, None, None, None) == -1               # null ctx -> error, no crash

@@ -1,0 +1,65 @@
+"""Host-side API checks (no GPU): env registry, observation layouts, and that the host
+spawn draws consume Python `random` / legacy `np.random` exactly as the reference env
+code does (checked against the golden fixtures recorded from the reference)."""
+import os
+import random
+
+import numpy as np
+import pytest
+
+import bluesky_gym
+from bluesky_gym import _gym, spawn
+from bluesky_gym import _native as nat
+from bluesky_gym.obs_layout import ObsLayout
+from oracle import batched as ob
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def test_register_envs_matches_reference_ids_and_limits():
+    bluesky_gym.register_envs()
+    expect = {"DescentEnv-v0": 300, "PlanWaypointEnv-v0": 300, "HorizontalCREnv-v0": 300,
+              "VerticalCREnv-v0": 300, "SectorCREnv-v0": 200, "StaticObstacleEnv-v0": 100,
+              "MergeEnv-v0": 50}
+    reg = _gym.registry
+    for k, v in expect.items():
+        assert reg[k].max_episode_steps == v
+        assert reg[k].entry_point.startswith("bluesky_gym.envs.")
+    for k in ("MergeEnv-v0", "VerticalCREnv-v0", "DescentEnv-v0"):
+        assert reg[k].vector_entry_point.startswith("bluesky_gym.vector:")
+    with pytest.raises(NotImplementedError):
+        _gym.make("SectorCREnv-v0")
+
+
+def test_obs_layout_keys_sorted_like_gymnasium():
+    m = ObsLayout(nat.ENV_MERGE, 20, 5)
+    assert list(m.keys) == list(ob.MERGE_OBS_KEYS) and m.dim == 40
+    v = ObsLayout(nat.ENV_VERTICAL_CR, 6, 0)
+    assert list(v.keys) == list(ob.VERTICAL_OBS_KEYS) and v.dim == 39
+    d = ObsLayout(nat.ENV_DESCENT, 1, 0)
+    assert list(d.keys) == list(ob.DESCENT_OBS_KEYS) and d.dim == 4
+    space = m.observation_space(_gym.spaces)
+    assert list(space.spaces) == sorted(space.spaces)
+
+
+@pytest.mark.parametrize("name,seed", [("merge_N8", 0), ("merge_N16", 1), ("merge_N32", 3)])
+def test_merge_host_spawn_consumes_random_like_reference(name, seed):
+    g = dict(np.load(f"{GOLD}/{name}.npz"))
+    random.seed(seed)
+    for ep in range(len(g["length"])):
+        assert np.array_equal(spawn.merge_spawn(int(g["num_ac"])), g["spawn"][ep])
+
+
+@pytest.mark.parametrize("name,seed", [("vertical_N6", 4), ("vertical_N32", 5)])
+def test_vertical_host_spawn_consumes_np_random_like_reference(name, seed):
+    g = dict(np.load(f"{GOLD}/{name}.npz"))
+    np.random.seed(seed)
+    for ep in range(len(g["length"])):
+        assert np.array_equal(spawn.vertical_spawn(int(g["num_ac"]) - 1), g["spawn"][ep])
+
+
+def test_descent_host_spawn_consumes_np_random_like_reference():
+    g = dict(np.load(f"{GOLD}/descent.npz"))
+    np.random.seed(6)
+    for ep in range(len(g["length"])):
+        assert np.array_equal(spawn.descent_spawn(), g["spawn"][ep])
