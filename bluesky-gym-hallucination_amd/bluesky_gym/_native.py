@@ -74,7 +74,7 @@ class BsgBuffers(C.Structure):
 EXPORTED_SYMBOLS = (
     "bsg_abi_version", "bsg_last_error", "bsg_obs_dim", "bsg_action_dim", "bsg_spawn_width",
     "bsg_create", "bsg_destroy", "bsg_bind", "bsg_reset", "bsg_step", "bsg_set_timing",
-    "bsg_step_timing",
+    "bsg_step_timing", "bsg_set_stamps",
 )
 
 _lib = None
@@ -120,6 +120,8 @@ def load_library(path: str | None = None):
     lib.bsg_set_timing.argtypes = [C.c_void_p, C.c_int32]
     lib.bsg_step_timing.restype = C.c_int32
     lib.bsg_step_timing.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_int32)]
+    lib.bsg_set_stamps.restype = C.c_int32
+    lib.bsg_set_stamps.argtypes = [C.c_void_p, C.c_void_p]
     if lib.bsg_abi_version() != ABI_VERSION:
         raise BsgError(f"libbsg ABI {lib.bsg_abi_version()} != expected {ABI_VERSION}")
     if path is None:

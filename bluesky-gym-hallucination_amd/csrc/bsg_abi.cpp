@@ -22,6 +22,7 @@ struct bsg_ctx {
   bsg::Route route{};
   // optional per-launch timing (bsg_set_timing)
   bool timing = false;
+  unsigned long long* stamps = nullptr;
   std::vector<hipEvent_t> ev_pool;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> pending;
 };
@@ -66,6 +67,7 @@ bsg::KParams make_params(const bsg_ctx* c, int mode) {
   p.obs_dim = c->obs_dim;
   p.spawn_width = c->spawn_width;
   p.seed = c->cfg.seed;
+  p.stamps = c->stamps;
   return p;
 }
 
@@ -213,6 +215,17 @@ int32_t bsg_step(bsg_ctx* c, const double* actions, const double* spawn, void* s
   p.actions = actions;
   p.spawn = spawn;
   return launch(c, p, stream);
+}
+
+int32_t bsg_set_stamps(bsg_ctx* c, void* buf) {
+  if (!c) return fail(BSG_E_INVALID_ARG, "bsg_set_stamps: null ctx%s%lld");
+#if defined(BSG_STAMPS) && BSG_STAMPS
+  c->stamps = static_cast<unsigned long long*>(buf);
+  return BSG_OK;
+#else
+  (void)buf;
+  return fail(BSG_E_UNSUPPORTED, "bsg_set_stamps: library built without -DBSG_STAMPS=1%s%lld");
+#endif
 }
 
 int32_t bsg_set_timing(bsg_ctx* c, int32_t enable) {

@@ -51,7 +51,8 @@ __device__ __forceinline__ double sgn(double x) { return (double)((x > 0.0) - (x
 
 // np.remainder / Python float % (numpy npy_divmod): fmod, then move toward b's sign.
 __device__ __forceinline__ double pymod(double a, double b) {
-  if (a > 0.0 && a < b) return a;       // fmod is the identity there (exact fast path)
+  // exact fast path for b > 0, |a| < b: fmod(a, b) == a, then the floor-mod sign fix
+  if (b > 0.0 && fabs(a) < b) return a > 0.0 ? a : (a < 0.0 ? a + b : 0.0);
   double mod = fmod(a, b);
   if (mod != 0.0) {
     if ((b < 0.0) != (mod < 0.0)) mod += b;
@@ -208,10 +209,15 @@ __device__ __forceinline__ void qdrdist(double latd1, double lond1, double latd2
 // (carried over from update_pos, which evaluates cos/sin of the same latitude) and
 // (coslat2, sinlat2) of the active waypoint (cached per waypoint).  sincos() is
 // bit-identical to separate sin()/cos() on gfx950/ROCm 7.2 (tools/probe/sincos_probe.hip).
+__device__ __forceinline__ bool b_times_dphi_far(double latd1, double latd2, double far_m) {
+  const double bmin = 6356752.314245;                       // WGS84 minor semi-axis
+  return bmin * (fabs(latd2 - latd1) * kD2R) * 0.999999 > far_m;
+}
+
 __device__ __forceinline__ void qdrdist_cached(double latd1, double lond1, double coslat1,
                                                double sinlat1, double latd2, double lond2,
-                                               double coslat2, double sinlat2, double* qdr,
-                                               double* distnm) {
+                                               double coslat2, double sinlat2, double far_m,
+                                               double* qdr, double* distnm) {
   bool sw = (latd1 * latd2 >= 0.0);
   double r;
   if (sw) {
@@ -225,8 +231,15 @@ __device__ __forceinline__ void qdrdist_cached(double latd1, double lond1, doubl
   }
   double sdl, cdl;
   sincos(lond2 * kD2R - lond1 * kD2R, &sdl, &cdl);
-  double d = r * acos(coslat1 * coslat2 * cdl + sinlat1 * sinlat2);
   *qdr = atan2(sdl * coslat2, coslat1 * sinlat2 - sinlat1 * coslat2 * cdl) * kR2D;
+  // d = r*acos(.) is only compared against thresholds by the caller; when the meridian
+  // gap alone puts it beyond `far_m` (great-circle >= r*|dphi|, r >= b, with a 1e-6
+  // relative margin) the acos is skipped and +inf returned.
+  if (b_times_dphi_far(latd1, latd2, far_m)) {
+    *distnm = __builtin_inf();
+    return;
+  }
+  double d = r * acos(coslat1 * coslat2 * cdl + sinlat1 * sinlat2);
   *distnm = d / NM;
 }
 

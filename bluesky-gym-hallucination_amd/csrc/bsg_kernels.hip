@@ -71,6 +71,27 @@ __device__ __forceinline__ void cre(AC& s, double lat, double lon, double hdg, d
 }
 
 // ---- exact memo of pure functions across substeps ---------------------------------------
+// Route waypoints held in registers for the substep loop (a per-lane indexed read of
+// the kernarg segment would be a vector memory round trip every substep).
+// The first two waypoints (the whole Merge route FIX -> RWY) live in registers; further
+// waypoints (unused by the in-scope envs) are read from the kernarg segment.
+struct RouteRegs {
+  int len;
+  double lat0, lon0, nq0, lat1, lon1, nq1;
+  const Route* r;
+  __device__ __forceinline__ void load(const Route& rr) {
+    r = &rr;
+    len = rr.len;
+    lat0 = rr.lat[0]; lon0 = rr.lon[0]; nq0 = rr.next_qdr[0];
+    lat1 = rr.lat[1]; lon1 = rr.lon[1]; nq1 = rr.next_qdr[1];
+  }
+  __device__ __forceinline__ void get(int k, double* la, double* lo, double* q) const {
+    if (k == 0) { *la = lat0; *lo = lon0; *q = nq0; }
+    else if (k == 1) { *la = lat1; *lo = lon1; *q = nq1; }
+    else { *la = r->lat[k]; *lo = r->lon[k]; *q = r->next_qdr[k]; }
+  }
+};
+
 struct Memo {
   uint64_t alt_bits;               // key of at = vatmos(alt)
   Atmos at;
@@ -78,9 +99,11 @@ struct Memo {
   double ap_tas;
   uint64_t lim_tas_bits, lim_h_bits;  // key of the PerfModel.limits speed clamp
   double allow_tas;
-  int wp_k;                        // cached waypoint trig
-  double wp_cos, wp_sin;
+  int wp_k;                        // cached waypoint (coords, next-leg bearing, trig)
+  double wp_lat, wp_lon, wp_nq, wp_cos, wp_sin;
   double coslat, sinlat;           // cos/sin(lat * D2R) of the current latitude
+  uint64_t tr_bits;                // key of turnrate = deg(g0*tan(bank)/max(tas, eps))
+  double turnrate;
 };
 
 constexpr uint64_t kNoKey = 0x7ff8dead0000beefull;   // a NaN payload no input produces
@@ -89,44 +112,62 @@ __device__ __forceinline__ void memo_init(Memo& m, const AC& s) {
   m.alt_bits = kNoKey; m.spd_bits = kNoKey; m.spdalt_bits = kNoKey;
   m.lim_tas_bits = kNoKey; m.lim_h_bits = kNoKey;
   m.at = Atmos{0, 0, 0}; m.ap_tas = 0; m.allow_tas = 0;
-  m.wp_k = -1; m.wp_cos = 0; m.wp_sin = 0;
+  m.wp_k = -1; m.wp_lat = 0; m.wp_lon = 0; m.wp_nq = 0; m.wp_cos = 0; m.wp_sin = 0;
+  m.tr_bits = kNoKey; m.turnrate = 0;
   sincos(s.lat * kD2R, &m.sinlat, &m.coslat);
+}
+
+__device__ __forceinline__ void memo_wp(Memo& m, const RouteRegs& rt, int k) {
+  m.wp_k = k;
+  rt.get(k, &m.wp_lat, &m.wp_lon, &m.wp_nq);
+  sincos(m.wp_lat * kD2R, &m.wp_sin, &m.wp_cos);
 }
 
 // ---- one BlueSky substep of one aircraft (Traffic.update, wind off, RESO OFF) ---------
 // oracle/bluesky_subset.py: traffic_update
-__device__ __forceinline__ void substep(AC& s, Memo& m, double dt, const Route& rt) {
+__device__ __forceinline__ void substep(AC& s, Memo& m, double dt, const RouteRegs& rt) {
   // Autopilot.update -- LNAV direct-to + ActiveWaypoint.reached (gs = tas, trk = hdg)
   if (s.nav & 1) {
     int k = (s.nav >> 8) & 0xff;
-    if (k != m.wp_k) { m.wp_k = k; sincos(rt.lat[k] * kD2R, &m.wp_sin, &m.wp_cos); }
-    double qdr, dnm;
-    qdrdist_cached(s.lat, s.lon, m.coslat, m.sinlat, rt.lat[k], rt.lon[k], m.wp_cos, m.wp_sin,
-                   &qdr, &dnm);
-    const double dist = dnm * NM;
-    const double nq = rt.next_qdr[k];
-    const double next_qdr = nq < -900.0 ? qdr : nq;
+    if (k != m.wp_k) memo_wp(m, rt, k);
+    // the waypoint distance only feeds `dist < turndist` (turndist <= turnrad while the
+    // leg change is <= 90 deg) and `dist/|gs| < 4 s`; beyond both it need not be exact
     const double turnrad = s.tas * s.tas / (npmax(0.01, TAN_BANKDEF) * G0);
+    const double far_m = npmax(turnrad, 4.0 * fabs(s.tas)) * 1.000001 + 1.0;
+    double qdr, dnm;
+    qdrdist_cached(s.lat, s.lon, m.coslat, m.sinlat, m.wp_lat, m.wp_lon, m.wp_cos, m.wp_sin,
+                   far_m, &qdr, &dnm);
+    const double next_qdr = m.wp_nq < -900.0 ? qdr : m.wp_nq;
     const double half = 0.5 * fabs(degto180(pymod(qdr, 360.0) - pymod(next_qdr, 360.0)));
-    bool reached_turn;
-    if (half <= 45.0 && dist > turnrad * 1.000001) {
-      reached_turn = false;                  // tan(half) <= 1 -> turndist <= turnrad < dist
-    } else {
-      const double turndist = fabs(turnrad * tan(half * kD2R));
-      reached_turn = dist < turndist;
+    if (half > 45.0 && dnm == __builtin_inf())   // turndist may exceed turnrad: exact d
+      qdrdist_cached(s.lat, s.lon, m.coslat, m.sinlat, m.wp_lat, m.wp_lon, m.wp_cos, m.wp_sin,
+                     __builtin_inf(), &qdr, &dnm);
+    bool reached = false;
+    if (dnm != __builtin_inf()) {
+      const double dist = dnm * NM;
+      bool reached_turn;
+      if (half <= 45.0 && dist > turnrad * 1.000001) {
+        reached_turn = false;                // tan(half) <= 1 -> turndist <= turnrad < dist
+      } else {
+        const double turndist = fabs(turnrad * tan(half * kD2R));
+        reached_turn = dist < turndist;
+      }
+      const double g = npmax(0.0001, fabs(s.tas));
+      // dist/g < 4, decided without the division outside a 1e-6 band around 4*g
+      const bool close2wp = dist < 4.0 * g * 0.999999 ? true
+                          : (dist > 4.0 * g * 1.000001 ? false : dist / g < 4.0);
+      const bool tooclose = close2wp && (fabs(degto180(pymod(s.hdg, 360.0) - pymod(qdr, 360.0))) > 90.0);
+      reached = reached_turn || tooclose;
     }
-    const bool close2wp = dist / npmax(0.0001, fabs(s.tas)) < 4.0;
-    const bool tooclose = close2wp && (fabs(degto180(pymod(s.hdg, 360.0) - pymod(qdr, 360.0))) > 90.0);
-    if (reached_turn || tooclose) {
+    if (reached) {
       if (k >= rt.len - 1) {
         s.nav &= ~1;                       // last waypoint: LNAV off, keep commanded track
       } else {
         ++k;
         s.nav = (k << 8) | 1;
-        m.wp_k = k;
-        sincos(rt.lat[k] * kD2R, &m.wp_sin, &m.wp_cos);
-        qdrdist_cached(s.lat, s.lon, m.coslat, m.sinlat, rt.lat[k], rt.lon[k], m.wp_cos,
-                       m.wp_sin, &qdr, &dnm);
+        memo_wp(m, rt, k);
+        qdrdist_cached(s.lat, s.lon, m.coslat, m.sinlat, m.wp_lat, m.wp_lon, m.wp_cos,
+                       m.wp_sin, __builtin_inf(), &qdr, &dnm);
       }
     }
     if (s.nav & 1) s.ap_trk = qdr;
@@ -167,7 +208,11 @@ __device__ __forceinline__ void substep(AC& s, Memo& m, double dt, const Route& 
   const bool need_ax = fabs(delta_spd) > fabs(dt * AXMAX);
   s.ax = (double)need_ax * sgn(delta_spd) * AXMAX;
   s.tas = need_ax ? s.tas + s.ax * dt : allow_tas;
-  const double turnrate = (G0 * TAN_BANKDEF / npmax(s.tas, EPS_SPD)) * kR2D;
+  if (bits(s.tas) != m.tr_bits) {
+    m.turnrate = (G0 * TAN_BANKDEF / npmax(s.tas, EPS_SPD)) * kR2D;
+    m.tr_bits = bits(s.tas);
+  }
+  const double turnrate = m.turnrate;
   const double delhdg = pymod(hdg_cmd - s.hdg + 180.0, 360.0) - 180.0;
   const bool swhdgsel = fabs(delhdg) > fabs(dt * turnrate);
   s.hdg = pymod(swhdgsel ? s.hdg + dt * turnrate * sgn(delhdg) : hdg_cmd, 360.0);
@@ -574,8 +619,26 @@ __device__ __forceinline__ int rank_in_group(const Lds& L, int base, int lane, i
 }
 
 // ---------------------------------------------------------------------------------------
+// Diagnostic stamps (BSG_STAMPS builds): one record of 8 u64 per workgroup (= wave).
+#if defined(BSG_STAMPS) && BSG_STAMPS
+#define BSG_STAMP(slot, val) \
+  do { if (p.stamps && threadIdx.x == 0) p.stamps[(size_t)blockIdx.x * 8 + (slot)] = (val); } while (0)
+__device__ __forceinline__ unsigned long long stamp_clock() {
+  __builtin_amdgcn_sched_barrier(0);
+  unsigned long long t = __builtin_amdgcn_s_memtime();
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+#else
+#define BSG_STAMP(slot, val) do { } while (0)
+#endif
+
 template <int KIND, int GS>
 __global__ __launch_bounds__(64) void step_kernel(KParams p) {
+#if defined(BSG_STAMPS) && BSG_STAMPS
+  BSG_STAMP(0, __builtin_amdgcn_s_memrealtime());
+  BSG_STAMP(1, stamp_clock());
+#endif
   __shared__ Lds L;
   const int lane = threadIdx.x;
   const int g = lane / GS;
@@ -632,7 +695,10 @@ __global__ __launch_bounds__(64) void step_kernel(KParams p) {
         if (S > 0) {
           Memo m;
           memo_init(m, s);
-          for (int it = 0; it < S; ++it) substep(s, m, p.cfg.simdt, p.route);
+          RouteRegs rt;
+          rt.load(p.route);
+          const double dt = p.cfg.simdt;
+          for (int it = 0; it < S; ++it) substep(s, m, dt, rt);
           // update_airspeed's cas = vtas2cas(tas, alt) of the LAST substep (its alt is the
           // one before that substep's update_pos, i.e. m.at's key)
           s.cas = tas2cas_at(s.tas, m.at);
@@ -644,6 +710,9 @@ __global__ __launch_bounds__(64) void step_kernel(KParams p) {
     stage(L, lane, s);
   }
   __syncthreads();
+#if defined(BSG_STAMPS) && BSG_STAMPS
+  BSG_STAMP(2, stamp_clock());
+#endif
 
   // ---------------- B: observation, reward, CD -----------------------------------------
   double o[7] = {0, 0, 0, 0, 0, 0, 0};
@@ -660,6 +729,9 @@ __global__ __launch_bounds__(64) void step_kernel(KParams p) {
   }
   const uint64_t ib = group_bits<GS>(__ballot(ok && stepping && intr), g);
   const int nintr = __popcll(ib);
+#if defined(BSG_STAMPS) && BSG_STAMPS
+  BSG_STAMP(3, stamp_clock());
+#endif
 
   // CD: StateBased all-pairs CPA, wave-compacted (see cd_candidate / cd_pair)
   uint64_t cmask = 0, lmask = 0;
@@ -697,6 +769,9 @@ __global__ __launch_bounds__(64) void step_kernel(KParams p) {
       cd_list[pos++] = (unsigned short)((lane << 6) | (base + k));
     }
     __syncthreads();
+#if defined(BSG_STAMPS) && BSG_STAMPS
+    BSG_STAMP(4, stamp_clock() | ((unsigned long long)total << 48));
+#endif
     // phase 2: dense exact StateBased over the surviving pairs
     for (int t = lane; t < total; t += 64) {
       const int pr = cd_list[t];
@@ -842,6 +917,11 @@ __global__ __launch_bounds__(64) void step_kernel(KParams p) {
   }
 
   if (active && j == 0) store_env(b, e, ev);
+#if defined(BSG_STAMPS) && BSG_STAMPS
+  BSG_STAMP(5, stamp_clock());
+  BSG_STAMP(6, __builtin_amdgcn_s_memrealtime());
+  BSG_STAMP(7, (unsigned long long)__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11)));
+#endif
 }
 
 // ---------------------------------------------------------------------------------------

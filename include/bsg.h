@@ -158,6 +158,12 @@ int32_t bsg_step(bsg_ctx* ctx, const double* actions, const double* spawn, void*
 int32_t bsg_set_timing(bsg_ctx* ctx, int32_t enable);
 int32_t bsg_step_timing(bsg_ctx* ctx, double* total_ms, int32_t* launches);
 
+/* Diagnostics: per-wave phase stamps (8 x u64 per workgroup: realtime start/end at 100 MHz,
+ * shader-clock stamps after each phase, hardware XCC/CU ids) into a caller-owned device
+ * buffer of grid_size*8 u64.  Only a library built with -DBSG_STAMPS=1 (make stamps)
+ * writes them; otherwise returns BSG_E_UNSUPPORTED.  Never used on the measured path. */
+int32_t bsg_set_stamps(bsg_ctx* ctx, void* device_buf);
+
 #ifdef __cplusplus
 }
 #endif
