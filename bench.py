@@ -77,14 +77,15 @@ def cpu_baseline(seconds: float):
                       f"(host has {os.cpu_count()} logical CPUs)"}
 
 
-def load_traffic(E):
-    """Per-launch HBM bytes from the committed rocprofv3 PMC pass (tools/profile.sh)."""
+def load_profile(E):
+    """Per-launch HBM bytes and VALU counts from the committed rocprofv3 PMC passes
+    (tools/profile.sh -> profiles/traffic.json); None when absent or for another size."""
     p = os.path.join(REPO, "profiles", "traffic.json")
     try:
         with open(p) as f:
             t = json.load(f)
         if int(t.get("envs", -1)) == E:
-            return float(t["hbm_bytes_per_launch"])
+            return t
     except (OSError, ValueError, KeyError):
         pass
     return None
@@ -176,6 +177,16 @@ def main():
         N = args.num_ac
         B = survey_bytes_per_env_step(N)
         achieved = B * E / (kern_avg_ms * 1e-3) / 1e9
+        prof = load_profile(E) if args.num_ac == 32 and not args.no_cd else None
+        valu = None
+        if prof and "valu_issue_cycles_per_simd" in prof:
+            # VALU issue utilisation of the same kernel: PMC instruction counts priced at
+            # 4 cycles per f64 and 2 per other wave64 VALU instruction, over 1024 SIMDs
+            # at the 2.4 GHz peak clock, divided by this run's kernel time
+            cyc = prof["valu_issue_cycles_per_simd"]
+            valu = {"valu_insts_per_launch": prof["valu_insts_per_launch"],
+                    "f64_insts_per_launch": prof["valu_f64_insts_per_launch"],
+                    "issue_frac": cyc / (kern_avg_ms * 1e-3 * 2.4e9)}
         out = {
             "metric": METRIC,
             "value": value,
@@ -204,11 +215,12 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
-                "traffic": load_traffic(E),
+                "traffic": prof["hbm_bytes_per_launch"] if prof else None,
                 "kernel": "bsg::step_kernel<MERGE,32>",
                 "kernel_avg_ms": kern_avg_ms,
                 "bytes_per_env_step": B,
                 "layout_bytes_per_env_step": layout_bytes_per_env_step(N, cd=not args.no_cd),
+                "valu": valu,
             },
         }
         if world == 1 and not args.skip_cpu_baseline:

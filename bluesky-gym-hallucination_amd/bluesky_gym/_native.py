@@ -15,7 +15,7 @@ LIB_PATH = os.environ.get("BSG_LIBRARY", os.path.join(_HERE, "_lib", "libbsg.so"
 ABI_VERSION = 1
 MAX_ROUTE = 4
 
-ENV_MERGE, ENV_VERTICAL_CR, ENV_DESCENT = 0, 1, 2
+ENV_MERGE, ENV_VERTICAL_CR, ENV_DESCENT, ENV_HORIZONTAL_CR = 0, 1, 2, 3
 AUTORESET_NONE, AUTORESET_NEXT_STEP, AUTORESET_SAME_STEP = 0, 1, 2
 
 E_CODES = {-1: "BSG_E_INVALID_ARG", -2: "BSG_E_HIP", -3: "BSG_E_STATE", -4: "BSG_E_UNSUPPORTED"}
@@ -60,6 +60,7 @@ BUFFER_FIELDS = [
     ("step_count", _i32p), ("flags", _i32p), ("episode", _u32p), ("wpt_reach", _i32p),
     ("faf_reached", _i32p), ("total_intrusions", _i32p), ("total_reward", _dp),
     ("drift_sum", _dp), ("target_alt", _dp), ("final_altitude", _dp),
+    ("env_wpt_lat", _dp), ("env_wpt_lon", _dp),
     ("obs", _fp), ("final_obs", _fp), ("reward", _fp), ("terminated", _u8p),
     ("truncated", _u8p), ("topk", _i32p), ("intr_mask", _u64p), ("conf_mask", _u64p),
     ("los_mask", _u64p), ("tcpamax", _fp), ("min_sep", _fp), ("ep_info", _dp),

@@ -6,6 +6,8 @@ Vertical: bluesky_gym/envs/vertical_cr_env.py:12-45 (NUM_INTRUDERS=5 -- redefine
           ACTION_FREQUENCY=30, 'DT 1' at :95, TimeLimit 300 at __init__.py:27)
 Descent:  bluesky_gym/envs/descent_env.py:10-30 (ACTION_FREQUENCY=30, 'DT 1' at :72,
           TimeLimit 300 at __init__.py:9)
+HorizontalCR: bluesky_gym/envs/horizontal_cr_env.py:11-30 (NUM_INTRUDERS=5,
+          ACTION_FREQUENCY=10, 'DT 5' at :71, TimeLimit 300 at __init__.py:19-22)
 """
 from __future__ import annotations
 
@@ -95,6 +97,11 @@ def merge_config(num_ac=20, num_ac_state=5, action_frequency=10, simdt=5.0,
 
 def vertical_config(num_intruders=5, action_frequency=30, simdt=1.0, max_episode_steps=300):
     return EnvKindConfig(nat.ENV_VERTICAL_CR, num_intruders + 1, 0, action_frequency, simdt,
+                         max_episode_steps)
+
+
+def horizontal_config(num_intruders=5, action_frequency=10, simdt=5.0, max_episode_steps=300):
+    return EnvKindConfig(nat.ENV_HORIZONTAL_CR, num_intruders + 1, 0, action_frequency, simdt,
                          max_episode_steps)
 
 

@@ -64,6 +64,9 @@ class DeviceBatch:
         self.topk = z((E, max(self.K, 1)), torch.int32) if self.cfg.kind == nat.ENV_MERGE else None
         self.intr_mask = z((E,), torch.int64)
         self.ep_info = z((E, 4), torch.float64)
+        if self.cfg.kind == nat.ENV_HORIZONTAL_CR:
+            self.envs["env_wpt_lat"] = z((E,), torch.float64)
+            self.envs["env_wpt_lon"] = z((E,), torch.float64)
         # learner hand-off rows [obs, reward, terminated, truncated] (RCCL all-gather payload)
         self.learner = z((E, self.obs_dim + 3), torch.float32) if self.want_learner else None
         if self.compute_cd:

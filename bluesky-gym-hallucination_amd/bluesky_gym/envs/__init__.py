@@ -2,5 +2,5 @@
 from .descent_env import DescentEnv  # noqa: F401
 from .merge_env import MergeEnv  # noqa: F401
 from .vertical_cr_env import VerticalCREnv  # noqa: F401
-from ._out_of_scope import (HorizontalCREnv, PlanWaypointEnv, SectorCREnv,  # noqa: F401
-                            StaticObstacleEnv)
+from .horizontal_cr_env import HorizontalCREnv  # noqa: F401
+from ._out_of_scope import PlanWaypointEnv, SectorCREnv, StaticObstacleEnv  # noqa: F401

@@ -1,7 +1,8 @@
 """Observation layouts: the reference observation_space keys, their sizes and the
 flat (sorted-key) offsets the HIP kernel writes.
 
-merge_env.py:59-74, vertical_cr_env.py:67-83, descent_env.py:53-60.  Gymnasium's
+merge_env.py:59-74, vertical_cr_env.py:67-83, descent_env.py:53-60,
+horizontal_cr_env.py:49-60.  Gymnasium's
 spaces.Dict sorts its keys, and SB3's MultiInputPolicy flattens in that order, so the
 flat fp32 row of libbsg is laid out in sorted-key order.
 """
@@ -25,6 +26,12 @@ def vertical_sizes(ni):
             "y_difference_speed": ni, "z_difference_speed": ni}
 
 
+def horizontal_sizes(ni):
+    return {"cos_difference_pos": ni, "cos_drift": 1, "intruder_distance": ni,
+            "sin_difference_pos": ni, "sin_drift": 1, "waypoint_distance": 1,
+            "x_difference_speed": ni, "y_difference_speed": ni}
+
+
 def descent_sizes():
     return {"altitude": 1, "runway_distance": 1, "target_altitude": 1, "vz": 1}
 
@@ -39,6 +46,8 @@ class ObsLayout:
             sizes = merge_sizes(num_ac_state)
         elif kind == nat.ENV_VERTICAL_CR:
             sizes = vertical_sizes(num_ac - 1)
+        elif kind == nat.ENV_HORIZONTAL_CR:
+            sizes = horizontal_sizes(num_ac - 1)
         else:
             sizes = descent_sizes()
         self.keys = tuple(sorted(sizes))

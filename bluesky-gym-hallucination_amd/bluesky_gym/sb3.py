@@ -84,6 +84,9 @@ class SB3VecEnv(_SB3Base):
                 elif self._kind == nat.ENV_VERTICAL_CR:
                     d["total_intrusions"] = int(ep[i, 1])
                     d["final_altitude"] = float(ep[i, 2])
+                elif self._kind == nat.ENV_HORIZONTAL_CR:
+                    d["total_intrusions"] = int(ep[i, 1])
+                    d["average_drift"] = float(ep[i, 2])
                 else:
                     d["final_altitude"] = float(ep[i, 2])
                 d["TimeLimit.truncated"] = bool(trunc[i] and not term[i])

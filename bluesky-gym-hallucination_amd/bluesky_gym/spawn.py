@@ -6,6 +6,7 @@ vector envs.
 merge_env.py:115-116 + _gen_aircraft :150-151   (random.uniform, 2 + 2*(N-1) draws)
 vertical_cr_env.py:267-268 + :187-195          (np.random.randint, 2 + 4*(N-1) draws)
 descent_env.py:170-171                         (np.random.randint, 2 draws)
+horizontal_cr_env.py:130-132 + :140            (np.random.randint, 3*(N-1) + 1 draws)
 """
 from __future__ import annotations
 
@@ -22,6 +23,7 @@ DEFAULT_RWY_DIS = 200
 ACTION_2_MS = 12.5
 V_AC_SPD = 150
 INTRUSION_DISTANCE_NM = 5
+H_WAYPOINT_DISTANCE_MIN, H_WAYPOINT_DISTANCE_MAX = 100, 150
 
 # bluesky.tools.aero constants (for the reference's randint bound, vertical_cr_env.py:190)
 _P0, _RHO0, _R = 101325.0, 1.225, 287.05287
@@ -65,6 +67,18 @@ def vertical_spawn(num_intruders, rs=None):
         else:
             dH = rs.randint(int((target_alt - altitude) - 500), int((target_alt - altitude) + 500))
         out += [float(dpsi), float(cpa), float(tlosh), float(dH)]
+    return np.array(out, np.float64)
+
+
+def horizontal_spawn(num_intruders, rs=None):
+    rs = np.random if rs is None else rs
+    out = []
+    for _ in range(num_intruders):
+        dpsi = rs.randint(45, 315)
+        cpa = rs.randint(0, INTRUSION_DISTANCE_NM)
+        tlosh = rs.randint(100, 1000)
+        out += [float(dpsi), float(cpa), float(tlosh)]
+    out.append(float(rs.randint(H_WAYPOINT_DISTANCE_MIN, H_WAYPOINT_DISTANCE_MAX)))
     return np.array(out, np.float64)
 
 

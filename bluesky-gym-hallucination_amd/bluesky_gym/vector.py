@@ -1,5 +1,6 @@
 """Gymnasium VectorEnv front-ends of the device batch (the ``vector_entry_point`` of
-MergeEnv-v0 / VerticalCREnv-v0 / DescentEnv-v0, registered by ``register_envs``).
+MergeEnv-v0 / VerticalCREnv-v0 / DescentEnv-v0 / HorizontalCREnv-v0, registered by
+``register_envs``).
 
 ``gym.make_vec("MergeEnv-v0", num_envs=4096, vectorization_mode="vector_entry_point",
 num_ac=32)`` returns a :class:`MergeVectorEnv` whose E envs live on one HIP device and
@@ -23,6 +24,7 @@ _INFO_KEYS = {
     nat.ENV_MERGE: ("total_reward", "faf_reach", "average_drift", "total_intrusions"),
     nat.ENV_VERTICAL_CR: ("total_reward", "total_intrusions", "final_altitude"),
     nat.ENV_DESCENT: ("total_reward", "final_altitude"),
+    nat.ENV_HORIZONTAL_CR: ("total_reward", "total_intrusions", "average_drift"),
 }
 
 
@@ -73,6 +75,8 @@ class BlueSkyVectorEnv(_gym.VectorEnv):
                 rows.append(spawnmod.merge_spawn(k.num_ac, rs))
             elif k.kind == nat.ENV_VERTICAL_CR:
                 rows.append(spawnmod.vertical_spawn(k.num_ac - 1, rs))
+            elif k.kind == nat.ENV_HORIZONTAL_CR:
+                rows.append(spawnmod.horizontal_spawn(k.num_ac - 1, rs))
             else:
                 rows.append(spawnmod.descent_spawn(rs))
         return torch.from_numpy(np.stack(rows))
@@ -109,7 +113,8 @@ class BlueSkyVectorEnv(_gym.VectorEnv):
 
     def _infos(self, done):
         """Gymnasium dict-of-arrays infos: the reference's per-env info dict
-        (merge_env.py:238-244; vertical_cr_env.py:203-211; descent_env.py:119-126)."""
+        (merge_env.py:238-244; vertical_cr_env.py:203-211; descent_env.py:119-126;
+        horizontal_cr_env.py:215-223)."""
         b = self.batch
         tr = b.envs["total_reward"].cpu().numpy()
         out = {}
@@ -124,6 +129,12 @@ class BlueSkyVectorEnv(_gym.VectorEnv):
         elif kind == nat.ENV_VERTICAL_CR:
             out = {"total_reward": tr, "total_intrusions": b.envs["total_intrusions"].cpu().numpy(),
                    "final_altitude": b.envs["final_altitude"].cpu().numpy()}
+        elif kind == nat.ENV_HORIZONTAL_CR:
+            cnt = b.envs["step_count"].cpu().numpy()
+            with np.errstate(invalid="ignore", divide="ignore"):
+                avg = b.envs["drift_sum"].cpu().numpy() / cnt
+            out = {"total_reward": tr, "total_intrusions": b.envs["total_intrusions"].cpu().numpy(),
+                   "average_drift": np.where(cnt > 0, avg, np.nan)}
         else:
             out = {"total_reward": tr, "final_altitude": b.envs["final_altitude"].cpu().numpy()}
         if b.compute_cd:
@@ -150,6 +161,15 @@ class VerticalCRVectorEnv(BlueSkyVectorEnv):
             num_intruders = num_ac - 1
         super().__init__(cfgmod.vertical_config(num_intruders, action_frequency, simdt,
                                                 max_episode_steps or 0), num_envs, **kw)
+
+
+class HorizontalCRVectorEnv(BlueSkyVectorEnv):
+    def __init__(self, num_envs=1, num_intruders=5, action_frequency=10, simdt=5.0,
+                 max_episode_steps=300, num_ac=None, **kw):
+        if num_ac is not None:
+            num_intruders = num_ac - 1
+        super().__init__(cfgmod.horizontal_config(num_intruders, action_frequency, simdt,
+                                                  max_episode_steps or 0), num_envs, **kw)
 
 
 class DescentVectorEnv(BlueSkyVectorEnv):

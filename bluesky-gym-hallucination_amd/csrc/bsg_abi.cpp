@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -23,6 +24,7 @@ struct bsg_ctx {
   // optional per-launch timing (bsg_set_timing)
   bool timing = false;
   unsigned long long* stamps = nullptr;
+  unsigned lds_pad = 0;
   std::vector<hipEvent_t> ev_pool;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> pending;
 };
@@ -68,6 +70,7 @@ bsg::KParams make_params(const bsg_ctx* c, int mode) {
   p.spawn_width = c->spawn_width;
   p.seed = c->cfg.seed;
   p.stamps = c->stamps;
+  p.lds_pad = c->lds_pad;
   return p;
 }
 
@@ -104,6 +107,7 @@ int32_t bsg_obs_dim(int32_t kind, int32_t num_ac, int32_t k) {
     case BSG_ENV_MERGE: return (num_ac >= 2 && k >= 1 && k <= num_ac - 1) ? 5 + 7 * k : BSG_E_INVALID_ARG;
     case BSG_ENV_VERTICAL_CR: return num_ac >= 2 ? 4 + 7 * (num_ac - 1) : BSG_E_INVALID_ARG;
     case BSG_ENV_DESCENT: return num_ac == 1 ? 4 : BSG_E_INVALID_ARG;
+    case BSG_ENV_HORIZONTAL_CR: return num_ac >= 2 ? 3 + 5 * (num_ac - 1) : BSG_E_INVALID_ARG;
     default: return BSG_E_INVALID_ARG;
   }
 }
@@ -112,7 +116,8 @@ int32_t bsg_action_dim(int32_t kind) {
   switch (kind) {
     case BSG_ENV_MERGE: return 2;
     case BSG_ENV_VERTICAL_CR:
-    case BSG_ENV_DESCENT: return 1;
+    case BSG_ENV_DESCENT:
+    case BSG_ENV_HORIZONTAL_CR: return 1;
     default: return BSG_E_INVALID_ARG;
   }
 }
@@ -122,6 +127,7 @@ int32_t bsg_spawn_width(int32_t kind, int32_t num_ac) {
     case BSG_ENV_MERGE: return 2 * num_ac;
     case BSG_ENV_VERTICAL_CR: return 2 + 4 * (num_ac - 1);
     case BSG_ENV_DESCENT: return 2;
+    case BSG_ENV_HORIZONTAL_CR: return 3 * (num_ac - 1) + 1;
     default: return BSG_E_INVALID_ARG;
   }
 }
@@ -162,6 +168,7 @@ int32_t bsg_create(const bsg_config* cfg, bsg_ctx** out) {
     c->route.lon[k] = cfg->route_lon[k];
     c->route.next_qdr[k] = cfg->route_next_qdr[k];
   }
+  if (const char* pad = std::getenv("BSG_LDS_PAD_BYTES")) c->lds_pad = (unsigned)std::atoi(pad);
   *out = c;
   return BSG_OK;
 }
@@ -186,6 +193,8 @@ int32_t bsg_bind(bsg_ctx* c, const bsg_buffers* b) {
                             b->final_altitude, b->obs, b->reward, b->terminated, b->truncated};
   for (size_t i = 0; i < sizeof(required) / sizeof(required[0]); ++i)
     if (!required[i]) return fail(BSG_E_INVALID_ARG, "bsg_bind: required buffer #%s%lld is NULL", "", (long long)i);
+  if (c->cfg.env_kind == BSG_ENV_HORIZONTAL_CR && (!b->env_wpt_lat || !b->env_wpt_lon))
+    return fail(BSG_E_INVALID_ARG, "bsg_bind: HorizontalCR needs env_wpt_lat/env_wpt_lon%s%lld");
   if (c->cfg.env_kind == BSG_ENV_MERGE && !b->topk)
     return fail(BSG_E_INVALID_ARG, "bsg_bind: Merge needs topk%s%lld");
   if (c->cfg.autoreset_mode == BSG_AUTORESET_SAME_STEP && !b->final_obs)

@@ -285,5 +285,6 @@ __device__ __forceinline__ int64_t randint_u32(uint32_t x, int64_t lo, int64_t h
 constexpr uint32_t TAG_MERGE = 0x4D455247u;
 constexpr uint32_t TAG_VERT = 0x56455254u;
 constexpr uint32_t TAG_DESC = 0x44455343u;
+constexpr uint32_t TAG_HORZ = 0x484F525Au;
 
 }  // namespace bsg

@@ -28,6 +28,7 @@ struct KParams {
   const double* spawn;       // [E, spawn_width] or nullptr (Philox)
   const uint8_t* env_mask;   // [E] or nullptr (all)  -- reset mode only
   unsigned long long* stamps; // diagnostics (BSG_STAMPS builds only)
+  unsigned lds_pad;          // extra dynamic LDS per workgroup (occupancy shaping)
 };
 
 hipError_t launch_step(const KParams& p, hipStream_t stream);

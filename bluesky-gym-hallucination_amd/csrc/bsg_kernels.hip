@@ -376,6 +376,30 @@ __device__ __forceinline__ void draw_alts(const KParams& p, int e, uint32_t epis
   }
 }
 
+// Traffic.creconfs (spd=None branch) around an ownship at 52N 4E with track 0 and ground
+// speed gsref; oracle/bluesky_subset.py: creconfs_params.  Places and cre()s aircraft s at
+// altitude acalt.
+__device__ __forceinline__ void creconfs_place(AC& s, double gsref, double dpsi, double cpa,
+                                               double tlosh, double acalt) {
+  const double trkref = 0.0 * kD2R;
+  const double cpam = cpa * NM;
+  const double pzr = RPZ;
+  const double trk = trkref + dpsi * kD2R;
+  const double gsn = gsref * cos(trk), gse = gsref * sin(trk);
+  const double vreln = gsref * cos(trkref) - gsn, vrele = gsref * sin(trkref) - gse;
+  const double vrel = sqrt(vreln * vreln + vrele * vrele);
+  const double drelcpa = tlosh * vrel + (cpam > pzr ? 0.0 : sqrt(pzr * pzr - cpam * cpam));
+  const double dist = sqrt(drelcpa * drelcpa + cpam * cpam);
+  const double rd = drelcpa / dist;
+  const double rx = cpam / dist;
+  const double brn = atan2(-rx * vreln + rd * vrele, rd * vreln + rx * vrele) * kR2D;
+  double aclat, aclon;
+  kwikpos(52.0, 4.0, brn, dist / NM, &aclat, &aclon);
+  const double acspd = tas2cas_at(sqrt(gsn * gsn + gse * gse), vatmos(acalt));
+  const double achdg = atan2(gse, gsn) * kR2D;
+  cre(s, aclat, aclon, achdg, acalt, acspd);
+}
+
 __device__ __forceinline__ void spawn_vertical(const KParams& p, int e, int j, uint32_t episode,
                                                AC& s, double* target_out) {
   double alt_init, target;
@@ -407,33 +431,51 @@ __device__ __forceinline__ void spawn_vertical(const KParams& p, int e, int j, u
     }
     dH = (double)randint_u32(r.w, lo, hi);
   }
-  // Traffic.creconfs (spd=None branch), oracle/bluesky_subset.py: creconfs_params
-  const double trkref = 0.0 * kD2R;
-  const double cpam = cpa * NM;
-  const double pzr = RPZ, pzh = HPZ;
-  const double trk = trkref + dpsi * kD2R;
   const double acalt = alt_init + dH;
   const double tlosv = 100000000000.0;
-  const double acvs = 0.0 - sgn(dH) * (fabs(dH) - pzh) / tlosv;
-  const double gsn = gsref * cos(trk), gse = gsref * sin(trk);
-  const double vreln = gsref * cos(trkref) - gsn, vrele = gsref * sin(trkref) - gse;
-  const double vrel = sqrt(vreln * vreln + vrele * vrele);
-  const double drelcpa = tlosh * vrel + (cpam > pzr ? 0.0 : sqrt(pzr * pzr - cpam * cpam));
-  const double dist = sqrt(drelcpa * drelcpa + cpam * cpam);
-  const double rd = drelcpa / dist;
-  const double rx = cpam / dist;
-  const double brn = atan2(-rx * vreln + rd * vrele, rd * vreln + rx * vrele) * kR2D;
-  double aclat, aclon;
-  kwikpos(52.0, 4.0, brn, dist / NM, &aclat, &aclon);
-  const double acspd = tas2cas_at(sqrt(gsn * gsn + gse * gse), vatmos(acalt));
-  const double achdg = atan2(gse, gsn) * kR2D;
-  cre(s, aclat, aclon, achdg, acalt, acspd);
+  const double acvs = 0.0 - sgn(dH) * (fabs(dH) - HPZ) / tlosv;
+  creconfs_place(s, gsref, dpsi, cpa, tlosh, acalt);
   s.vs = acvs;
   s.alt = alt_init + dH;            // vertical_cr_env.py:199
   s.selalt = alt_init + dH;         // :200 selaltcmd(i+1, alt + dH, 0)
   s.selvs = acvs;
 }
 
+// horizontal_cr_env.py:82-101 (reset), :127-133 (_generate_conflicts: creconfs with dH=None,
+// so intruders fly level at the ownship's altitude 0 with vs 0), :135-148 (_generate_waypoint:
+// one waypoint at bearing 0, 100..150 km from the ownship).  aux[0..1] <- waypoint lat/lon.
+__device__ __forceinline__ void spawn_horizontal(const KParams& p, int e, int j, uint32_t episode,
+                                                 AC& s, double* aux) {
+  cre(s, 52.0, 4.0, 0.0, 0.0, 150.0);
+  const int W = p.spawn_width;
+  if (j == 0) {
+    double wdis;
+    if (p.spawn) {
+      wdis = p.spawn[(size_t)e * W + W - 1];
+    } else {
+      U4 r = philox4x32_10((uint32_t)(e + p.cfg.env_offset), episode, 0u, TAG_HORZ, p.seed);
+      wdis = (double)randint_u32(r.x, 100, 150);
+    }
+    get_point_at_distance(52.0, 4.0, wdis, 0.0, &aux[0], &aux[1]);
+    return;
+  }
+  const double gsref = s.tas;
+  double dpsi, cpa, tlosh;
+  if (p.spawn) {
+    const double* q = p.spawn + (size_t)e * W + 3 * (j - 1);
+    dpsi = q[0]; cpa = q[1]; tlosh = q[2];
+  } else {
+    U4 r = philox4x32_10((uint32_t)(e + p.cfg.env_offset), episode, (uint32_t)j, TAG_HORZ, p.seed);
+    dpsi = (double)randint_u32(r.x, 45, 315);
+    cpa = (double)randint_u32(r.y, 0, 5);
+    tlosh = (double)randint_u32(r.z, 100, 1000);
+  }
+  creconfs_place(s, gsref, dpsi, cpa, tlosh, 0.0);
+  s.vs = 0.0;
+  s.selalt = 0.0;
+}
+
+// aux[0]: target altitude (Vertical/Descent); aux[0..1]: waypoint (HorizontalCR)
 template <int KIND>
 __device__ __forceinline__ void spawn(const KParams& p, int e, int j, uint32_t episode, AC& s,
                                       double* target) {
@@ -441,6 +483,8 @@ __device__ __forceinline__ void spawn(const KParams& p, int e, int j, uint32_t e
     spawn_merge(p, e, j, episode, s);
   } else if constexpr (KIND == BSG_ENV_VERTICAL_CR) {
     spawn_vertical(p, e, j, episode, s, target);
+  } else if constexpr (KIND == BSG_ENV_HORIZONTAL_CR) {
+    spawn_horizontal(p, e, j, episode, s, target);
   } else {
     double alt_init;
     draw_alts(p, e, episode, TAG_DESC, &alt_init, target);
@@ -455,6 +499,7 @@ struct EnvScalars {
   int step_count, flags, wpt_reach, faf_reached, total_intr;
   uint32_t episode;
   double total_reward, drift_sum, target_alt, final_alt;
+  double wpt_lat, wpt_lon;          // HorizontalCR waypoint
 };
 
 __device__ __forceinline__ void load_env(const Buffers& b, int e, EnvScalars& v) {
@@ -462,6 +507,7 @@ __device__ __forceinline__ void load_env(const Buffers& b, int e, EnvScalars& v)
   v.faf_reached = b.faf_reached[e]; v.total_intr = b.total_intrusions[e];
   v.episode = b.episode[e]; v.total_reward = b.total_reward[e]; v.drift_sum = b.drift_sum[e];
   v.target_alt = b.target_alt[e]; v.final_alt = b.final_altitude[e];
+  if (b.env_wpt_lat) { v.wpt_lat = b.env_wpt_lat[e]; v.wpt_lon = b.env_wpt_lon[e]; }
 }
 
 __device__ __forceinline__ void store_env(const Buffers& b, int e, const EnvScalars& v) {
@@ -469,11 +515,15 @@ __device__ __forceinline__ void store_env(const Buffers& b, int e, const EnvScal
   b.faf_reached[e] = v.faf_reached; b.total_intrusions[e] = v.total_intr;
   b.episode[e] = v.episode; b.total_reward[e] = v.total_reward; b.drift_sum[e] = v.drift_sum;
   b.target_alt[e] = v.target_alt; b.final_altitude[e] = v.final_alt;
+  if (b.env_wpt_lat) { b.env_wpt_lat[e] = v.wpt_lat; b.env_wpt_lon[e] = v.wpt_lon; }
 }
 
-__device__ __forceinline__ void reset_scalars(EnvScalars& v, double target) {
+template <int KIND>
+__device__ __forceinline__ void reset_scalars(EnvScalars& v, const double aux[2]) {
   v.step_count = 0; v.flags = 0; v.wpt_reach = 0; v.faf_reached = 0; v.total_intr = 0;
-  v.total_reward = 0.0; v.drift_sum = 0.0; v.target_alt = target; v.final_alt = 0.0;
+  v.total_reward = 0.0; v.drift_sum = 0.0; v.final_alt = 0.0;
+  if constexpr (KIND == BSG_ENV_HORIZONTAL_CR) { v.wpt_lat = aux[0]; v.wpt_lon = aux[1]; }
+  else v.target_alt = aux[0];
   v.episode += 1;
 }
 
@@ -509,7 +559,7 @@ __device__ __forceinline__ bool lane_obs(const Lds& L, int base, int lane, doubl
     *sortkey = dmat;
     return dist < 4;                                       // _check_intrusion :280-281
   } else {
-    // vertical_cr_env.py:133-156
+    // vertical_cr_env.py:133-156 / horizontal_cr_env.py:172-188 (gs == tas: no wind)
     const double alt0 = L.alt[base], vs0 = L.vs[base], gs0 = L.tas[base];
     const double altj = L.alt[lane], tasj = L.tas[lane];
     const double bearing = bound180(hdg0 - qdr);
@@ -525,6 +575,7 @@ __device__ __forceinline__ bool lane_obs(const Lds& L, int base, int lane, doubl
     o[5] = gs0 - shd * tasj;                                // y_difference_speed
     o[6] = L.vs[lane] - vs0;                                // z_difference_speed
     *sortkey = 0.0;
+    if constexpr (KIND == BSG_ENV_HORIZONTAL_CR) return dist < 5;   // horizontal_cr_env.py:262
     return (dist < 5) && (fabs(alt0 - altj) < 1000 * 0.3048);   // :235-237
   }
 }
@@ -557,6 +608,13 @@ __device__ __forceinline__ void write_lane_obs(float* obs, float* fobs, float* l
     put(4 + 4 * NI + i, o[4] / 150);        // x_difference_speed
     put(4 + 5 * NI + i, o[5] / 150);        // y_difference_speed
     put(4 + 6 * NI + i, o[6]);              // z_difference_speed
+  } else if constexpr (KIND == BSG_ENV_HORIZONTAL_CR) {
+    const int NI = N - 1, i = j - 1;
+    put(i, o[1]);                           // cos_difference_pos
+    put(NI + 1 + i, o[0] / 150);            // intruder_distance
+    put(2 * NI + 1 + i, o[2]);              // sin_difference_pos
+    put(3 * NI + 3 + i, o[4] / 150);        // x_difference_speed
+    put(4 * NI + 3 + i, o[5] / 150);        // y_difference_speed
   }
 }
 
@@ -574,6 +632,15 @@ __device__ __forceinline__ void own_obs(const KParams& p, const Lds& L, int lane
     double sd, cd;
     sincos(*drift * kD2R, &sd, &cd);
     sc[0] = L.tas[lane]; sc[1] = cd; sc[2] = (double)ev.wpt_reach; sc[3] = sd; sc[4] = *wdist / 250;
+  } else if constexpr (KIND == BSG_ENV_HORIZONTAL_CR) {
+    // horizontal_cr_env.py:191-203
+    double wqdr, wd;
+    kwikqdrdist(lat, lon, ev.wpt_lat, ev.wpt_lon, &wqdr, &wd);
+    *wdist = wd * 1.852;                                   // km
+    *drift = bound180(L.hdg[lane] - wqdr);
+    double sd, cd;
+    sincos(*drift * kD2R, &sd, &cd);
+    sc[0] = cd; sc[1] = sd; sc[2] = *wdist / 150; sc[3] = 0.0; sc[4] = 0.0;
   } else {
     const double altitude = L.alt[lane], vz = L.vs[lane];
     *rwd = 200 - kwikdist(52.0, 4.0, lat, lon) * 1.852;
@@ -603,6 +670,11 @@ __device__ __forceinline__ void write_own_obs(float* obs, float* fobs, float* lr
     put(1 + 3 * NI, sc[3]);                 // runway_distance
     put(2 + 4 * NI, sc[2]);                 // target_altitude
     put(3 + 4 * NI, sc[1]);                 // vz
+  } else if constexpr (KIND == BSG_ENV_HORIZONTAL_CR) {
+    const int NI = N - 1;
+    put(NI, sc[0]);                         // cos_drift
+    put(3 * NI + 1, sc[1]);                 // sin_drift
+    put(3 * NI + 2, sc[2]);                 // waypoint_distance
   } else {
     put(0, sc[0]); put(1, sc[3]); put(2, sc[2]); put(3, sc[1]);
   }
@@ -666,10 +738,10 @@ __global__ __launch_bounds__(64) void step_kernel(KParams p) {
   // ---------------- A: spawn or propagate, store state ------------------------------
   {
     AC s = {};
-    double new_target = ev.target_alt;
+    double aux[2] = {ev.target_alt, 0.0};
     if (ok) {
       if (resetting) {
-        spawn<KIND>(p, e, j, ev.episode, s, &new_target);
+        spawn<KIND>(p, e, j, ev.episode, s, aux);
       } else {
         load_ac(b, a, s);
       }
@@ -684,6 +756,10 @@ __global__ __launch_bounds__(64) void step_kernel(KParams p) {
             s.ap_trk = heading_new;
             s.nav &= ~1;
             s.selspd = speed_new >= 1.0 ? speed_new * KTS : speed_new;
+          } else if constexpr (KIND == BSG_ENV_HORIZONTAL_CR) {
+            // horizontal_cr_env.py:272-275: HDG KL001 {hdg + a*45} (no wrap)
+            s.ap_trk = s.hdg + p.actions[e] * 45;
+            s.nav &= ~1;
           } else {
             // vertical_cr_env.py:242-256 / descent_env.py:146-160
             const double act = p.actions[e] * 12.5;
@@ -706,7 +782,7 @@ __global__ __launch_bounds__(64) void step_kernel(KParams p) {
       }
       if (active) store_ac(b, a, s);
     }
-    if (resetting && j == 0) reset_scalars(ev, new_target);
+    if (resetting && j == 0) reset_scalars<KIND>(ev, aux);
     stage(L, lane, s);
   }
   __syncthreads();
@@ -811,6 +887,14 @@ __global__ __launch_bounds__(64) void step_kernel(KParams p) {
         const double dd = fabs(drift * kD2R);
         r = ((double)reach + dd * -0.1) + (double)(nintr * -1);
         ev.drift_sum += dd;
+      } else if constexpr (KIND == BSG_ENV_HORIZONTAL_CR) {
+        // _check_waypoint :237-248 ; _check_drift :250-253 ; _check_intrusion :255-265
+        int reach = 0;
+        if (wdist < 5 && ev.wpt_reach != 1) { ev.wpt_reach = 1; reach = 1; }
+        const double dd = fabs(drift * kD2R);
+        r = ((double)reach + dd * -0.1) + (double)(nintr * -1);
+        ev.drift_sum += dd;
+        d = ev.wpt_reach == 1;
       } else {
         // _get_reward (vertical_cr_env.py:213-228 / descent_env.py:128-144)
         const double altitude = L.alt[lane];
@@ -862,6 +946,9 @@ __global__ __launch_bounds__(64) void step_kernel(KParams p) {
         if constexpr (KIND == BSG_ENV_MERGE) {
           info[2] = (double)ev.faf_reached;
           info[3] = ev.drift_sum / (double)ev.step_count;
+        } else if constexpr (KIND == BSG_ENV_HORIZONTAL_CR) {
+          info[2] = ev.drift_sum / (double)ev.step_count;   // average_drift
+          info[3] = 0.0;
         } else {
           info[2] = ev.final_alt;
           info[3] = 0.0;
@@ -886,12 +973,12 @@ __global__ __launch_bounds__(64) void step_kernel(KParams p) {
   if (p.cfg.autoreset_mode == BSG_AUTORESET_SAME_STEP && __syncthreads_or(same_step_reset)) {
     {
       AC s = {};
-      double tgt = ev.target_alt;
+      double aux[2] = {ev.target_alt, 0.0};
       if (same_step_reset && ok) {
-        spawn<KIND>(p, e, j, ev.episode, s, &tgt);
+        spawn<KIND>(p, e, j, ev.episode, s, aux);
         store_ac(b, a, s);
       }
-      if (same_step_reset && j == 0) reset_scalars(ev, tgt);
+      if (same_step_reset && j == 0) reset_scalars<KIND>(ev, aux);
       if (same_step_reset) stage(L, lane, s);
     }
     __syncthreads();
@@ -933,7 +1020,7 @@ static hipError_t launch_kind(const KParams& p, hipStream_t st) {
   const int grid = (p.E + epb - 1) / epb;
   switch (gs) {
 #define BSG_CASE(G) \
-    case G: hipLaunchKernelGGL((step_kernel<KIND, G>), dim3(grid), dim3(64), 0, st, p); break;
+    case G: hipLaunchKernelGGL((step_kernel<KIND, G>), dim3(grid), dim3(64), p.lds_pad, st, p); break;
     BSG_CASE(1) BSG_CASE(2) BSG_CASE(4) BSG_CASE(8) BSG_CASE(16) BSG_CASE(32) BSG_CASE(64)
 #undef BSG_CASE
     default: return hipErrorInvalidValue;
@@ -946,6 +1033,7 @@ hipError_t launch_step(const KParams& p, hipStream_t st) {
     case BSG_ENV_MERGE: return launch_kind<BSG_ENV_MERGE>(p, st);
     case BSG_ENV_VERTICAL_CR: return launch_kind<BSG_ENV_VERTICAL_CR>(p, st);
     case BSG_ENV_DESCENT: return launch_kind<BSG_ENV_DESCENT>(p, st);
+    case BSG_ENV_HORIZONTAL_CR: return launch_kind<BSG_ENV_HORIZONTAL_CR>(p, st);
     default: return hipErrorInvalidValue;
   }
 }

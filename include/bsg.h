@@ -39,7 +39,8 @@ enum {
   BSG_E_UNSUPPORTED = -4
 };
 
-enum { BSG_ENV_MERGE = 0, BSG_ENV_VERTICAL_CR = 1, BSG_ENV_DESCENT = 2 };
+enum { BSG_ENV_MERGE = 0, BSG_ENV_VERTICAL_CR = 1, BSG_ENV_DESCENT = 2,
+       BSG_ENV_HORIZONTAL_CR = 3 };
 
 /* Vector-env autoreset conventions:
  *   NEXT_STEP: Gymnasium >= 1.0 VectorEnv default -- the step AFTER a done step resets
@@ -88,6 +89,8 @@ typedef struct bsg_buffers {
   double *drift_sum;         /* info average_drift numerator (count = step_count) */
   double *target_alt;        /* vertical/descent target altitude (m) */
   double *final_altitude;    /* vertical/descent info */
+  double *env_wpt_lat;       /* HorizontalCR per-env waypoint (horizontal_cr_env.py:135-148) */
+  double *env_wpt_lon;
   /* ---- outputs --------------------------------------------------------------------- */
   float *obs;                /* [E, obs_dim] sorted-key flatten (gymnasium spaces.Dict order) */
   float *final_obs;          /* [E, obs_dim] terminal obs (SAME_STEP only; else may be NULL) */
@@ -119,10 +122,12 @@ const char* bsg_last_error(void);
 
 /* Flat observation length for an env kind (sum of the Box sizes of the reference
  * observation_space: merge_env.py:59-74 -> 5+7K; vertical_cr_env.py:67-83 -> 4+7(N-1);
- * descent_env.py:53-60 -> 4). Negative on invalid input. */
+ * descent_env.py:53-60 -> 4; horizontal_cr_env.py:49-60 -> 3+5(N-1)). Negative on
+ * invalid input. */
 int32_t bsg_obs_dim(int32_t env_kind, int32_t num_ac, int32_t num_ac_state);
 
-/* Action width (merge_env.py:76 -> 2; vertical_cr_env.py:85 / descent_env.py:62 -> 1). */
+/* Action width (merge_env.py:76 -> 2; vertical_cr_env.py:85 / descent_env.py:62 /
+ * horizontal_cr_env.py:62 -> 1). */
 int32_t bsg_action_dim(int32_t env_kind);
 
 /* Doubles per env of host-supplied spawn parameters for bsg_reset / bsg_step:
@@ -130,7 +135,9 @@ int32_t bsg_action_dim(int32_t env_kind);
  *                        random.uniform draws of merge_env.py:115-116,150-151
  *   Vertical [2+4(N-1)]: alt_init, target_alt, then (dpsi, cpa, tlosh, dH) per intruder,
  *                        the np.random draws of vertical_cr_env.py:188-195,267-268
- *   Descent  [2]       : alt_init, target_alt (descent_env.py:170-171) */
+ *   Descent  [2]       : alt_init, target_alt (descent_env.py:170-171)
+ *   Horizontal [3(N-1)+1]: (dpsi, cpa, tlosh) per intruder, then the waypoint distance
+ *                        (km), the np.random draws of horizontal_cr_env.py:130-132,140 */
 int32_t bsg_spawn_width(int32_t env_kind, int32_t num_ac);
 
 /* Replaces: gym.make(id) -> Env.__init__ (merge_env.py:54-101): validates the config

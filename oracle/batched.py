@@ -71,6 +71,19 @@ VERTICAL_OBS_KEYS = ("altitude", "altitude_difference", "cos_difference_pos",
                      "target_altitude", "vz", "x_difference_speed", "y_difference_speed",
                      "z_difference_speed")
 DESCENT_OBS_KEYS = ("altitude", "runway_distance", "target_altitude", "vz")
+HORIZONTAL_OBS_KEYS = ("cos_difference_pos", "cos_drift", "intruder_distance",
+                       "sin_difference_pos", "sin_drift", "waypoint_distance",
+                       "x_difference_speed", "y_difference_speed")
+
+# ---- horizontal_cr_env.py:11-30 ------------------------------------------------------------
+H_DISTANCE_MARGIN = 5
+H_REACH_REWARD = 1
+H_DRIFT_PENALTY = -0.1
+H_INTRUSION_PENALTY = -1
+H_INTRUSION_DISTANCE = 5
+H_WAYPOINT_DISTANCE_MIN, H_WAYPOINT_DISTANCE_MAX = 100, 150
+H_D_HEADING = 45
+H_AC_SPD = 150
 
 
 def merge_obs_sizes(k):
@@ -84,6 +97,12 @@ def vertical_obs_sizes(ni):
             "intruder_distance": ni, "runway_distance": 1, "sin_difference_pos": ni,
             "target_altitude": 1, "vz": 1, "x_difference_speed": ni,
             "y_difference_speed": ni, "z_difference_speed": ni}
+
+
+def horizontal_obs_sizes(ni):
+    return {"cos_difference_pos": ni, "cos_drift": 1, "intruder_distance": ni,
+            "sin_difference_pos": ni, "sin_drift": 1, "waypoint_distance": 1,
+            "x_difference_speed": ni, "y_difference_speed": ni}
 
 
 def descent_obs_sizes():
@@ -466,8 +485,8 @@ class VerticalOracle(_VertBase):
         cosb = np.cos(np.deg2rad(bearing))
         sinb = np.sin(np.deg2rad(bearing))
         hd = hdg0 - st.hdg[:, 1:]
-        x_dif = -np.cos(np.deg2rad(hd)) * st.tas[:, 1:]
-        y_dif = st.tas[:, :1] - np.sin(np.deg2rad(hd)) * st.tas[:, 1:]
+        x_dif = -np.cos(np.deg2rad(hd)) * st.gs[:, 1:]
+        y_dif = st.gs[:, :1] - np.sin(np.deg2rad(hd)) * st.gs[:, 1:]
         runway_distance = DEFAULT_RWY_DIS - bsx.kwikdist(V_RWY_LAT, V_RWY_LON, st.lat[:, 0], st.lon[:, 0]) * NM2KM
         obs = {
             "altitude": ((altitude - ALT_MEAN) / ALT_STD)[:, None],
@@ -609,6 +628,146 @@ def _cd_fill(o, res, mask):
 
 
 _Base._cd_into = lambda self, res, mask: _cd_fill(self, res, mask)
+
+
+class HorizontalOracle(_Base):
+    """HorizontalCREnv-v0 (horizontal_cr_env.py).  N = 1 + NUM_INTRUDERS."""
+    kind = "horizontal"
+
+    def __init__(self, num_envs, num_ac=6, action_frequency=10, simdt=5.0,
+                 max_episode_steps=300, autoreset=AUTORESET_NEXT_STEP, seed=0,
+                 compute_cd=True):
+        super().__init__(num_envs, num_ac, action_frequency, simdt, max_episode_steps,
+                         autoreset, seed)
+        self.NI = self.N - 1
+        self.compute_cd = compute_cd
+        self.obs_sizes = horizontal_obs_sizes(self.NI)
+        self.obs_dim = sum(self.obs_sizes.values())
+        self.wpt_lat = np.zeros(self.E)
+        self.wpt_lon = np.zeros(self.E)
+        self.wpt_reach = np.zeros(self.E, np.int32)
+        self.drift_sum = np.zeros(self.E)
+        self.drift_cnt = np.zeros(self.E, np.int32)
+
+    def spawn_width(self):
+        return 3 * self.NI + 1
+
+    def device_spawn_params(self, env_ids, episodes):
+        ids = np.asarray(env_ids, np.uint32)
+        eps = np.asarray(episodes, np.uint32)
+        out = np.zeros((len(ids), self.spawn_width()))
+        for i in range(self.NI):
+            y0, y1, y2, _ = philox.philox4x32_10(ids, eps, i + 1, philox.TAG_HORZ, self.seed)
+            out[:, 3 * i] = philox.randint_u32(y0, 45, 315)
+            out[:, 3 * i + 1] = philox.randint_u32(y1, 0, H_INTRUSION_DISTANCE)
+            out[:, 3 * i + 2] = philox.randint_u32(y2, 100, 1000)
+        x0, _, _, _ = philox.philox4x32_10(ids, eps, 0, philox.TAG_HORZ, self.seed)
+        out[:, -1] = philox.randint_u32(x0, H_WAYPOINT_DISTANCE_MIN, H_WAYPOINT_DISTANCE_MAX)
+        return out
+
+    def _reset_ids(self, ids, spawn):
+        """horizontal_cr_env.py:82-101 + _generate_conflicts :127-133 + _generate_waypoint
+        :135-148."""
+        st = self.st
+        for j in range(self.N):
+            bsx.cre_state(st, (ids, np.full(len(ids), j)), 0.0, 0.0, 0.0, 0.0, 0.0)
+        # cre('KL001', acspd=150): default 52N 4E, hdg 0, alt 0
+        bsx.cre_state(st, (ids, np.zeros(len(ids), int)), 52.0, 4.0, 0.0, 0.0, H_AC_SPD)
+        for e in ids:
+            gs0 = float(st.tas[e, 0])
+            for i in range(self.NI):
+                dpsi, cpa, tlosh = spawn[e, 3 * i: 3 * i + 3]
+                lat, lon, hdg, acalt, acspd, acvs = bsx.creconfs_params(
+                    52.0, 4.0, 0.0, 0.0, gs0, 0.0, float(dpsi), float(cpa), float(tlosh))
+                bsx.cre_state(st, (e, i + 1), lat, lon, hdg, acalt, acspd)
+                st.vs[e, i + 1] = acvs
+                st.selalt[e, i + 1] = 0.0
+            wlat, wlon = bsx.get_point_at_distance(st.lat[e, 0], st.lon[e, 0], spawn[e, -1], 0)
+            self.wpt_lat[e], self.wpt_lon[e] = float(wlat), float(wlon)
+        self.wpt_reach[ids] = 0
+        self.drift_sum[ids] = 0.0
+        self.drift_cnt[ids] = 0
+
+    def _apply_action(self, actions):
+        """horizontal_cr_env.py:272-275: HDG = hdg + a*45 (no wrap), LNAV off."""
+        st = self.st
+        st.ap_trk[:, 0] = st.hdg[:, 0] + actions[:, 0] * H_D_HEADING
+        st.swlnav[:, 0] = False
+
+    def _obs_core(self):
+        """horizontal_cr_env.py:150-213."""
+        st = self.st
+        lat0, lon0, hdg0 = st.lat[:, :1], st.lon[:, :1], st.hdg[:, :1]
+        int_qdr, int_dis = bsx.kwikqdrdist(lat0, lon0, st.lat[:, 1:], st.lon[:, 1:])
+        bearing = bsx.bound_angle_positive_negative_180(hdg0 - int_qdr)
+        hd = hdg0 - st.hdg[:, 1:]
+        x_dif = -np.cos(np.deg2rad(hd)) * st.gs[:, 1:]
+        y_dif = st.gs[:, :1] - np.sin(np.deg2rad(hd)) * st.gs[:, 1:]
+        wpt_qdr, wpt_dis = bsx.kwikqdrdist(st.lat[:, 0], st.lon[:, 0], self.wpt_lat, self.wpt_lon)
+        drift = bsx.bound_angle_positive_negative_180(st.hdg[:, 0] - wpt_qdr)
+        obs = {
+            "intruder_distance": (int_dis * NM2KM) / H_WAYPOINT_DISTANCE_MAX,
+            "cos_difference_pos": np.cos(np.deg2rad(bearing)),
+            "sin_difference_pos": np.sin(np.deg2rad(bearing)),
+            "x_difference_speed": x_dif / H_AC_SPD,
+            "y_difference_speed": y_dif / H_AC_SPD,
+            "waypoint_distance": ((wpt_dis * NM2KM) / H_WAYPOINT_DISTANCE_MAX)[:, None],
+            "cos_drift": np.cos(np.deg2rad(drift))[:, None],
+            "sin_drift": np.sin(np.deg2rad(drift))[:, None],
+        }
+        return obs, int_dis, wpt_dis * NM2KM, drift
+
+    def observe(self):
+        obs, *_ = self._obs_core()
+        return {"obs": flatten_obs(obs, HORIZONTAL_OBS_KEYS), "obs_dict": obs}
+
+    def _observe_and_reward(self):
+        obs, int_dis, wpt_km, drift = self._obs_core()
+        c = (wpt_km < H_DISTANCE_MARGIN) & (self.wpt_reach != 1)
+        reach = np.where(c, H_REACH_REWARD, 0)
+        new_wr = np.where(c, 1, self.wpt_reach)
+        d = np.abs(np.deg2rad(drift))
+        intr = int_dis < H_INTRUSION_DISTANCE
+        nintr = intr.sum(axis=1)
+        reward = reach + d * H_DRIFT_PENALTY + nintr * H_INTRUSION_PENALTY
+        intr_mask = np.zeros(self.E, np.uint64)
+        for i in range(self.NI):
+            intr_mask |= intr[:, i].astype(np.uint64) << np.uint64(i + 1)
+        res = dict(obs=flatten_obs(obs, HORIZONTAL_OBS_KEYS), obs_dict=obs, reward=reward,
+                   terminated=new_wr == 1, intr_mask=intr_mask, nintr=nintr, _new_wr=new_wr, _d=d)
+        if self.compute_cd:
+            st = self.st
+            cd = bsx.statebased_detect(st.lat, st.lon, st.alt, st.hdg, st.tas, st.vs)
+            res["conf_mask"] = _rows_to_u64(cd["swconfl"])
+            res["los_mask"] = _rows_to_u64(cd["swlos"])
+            res["tcpamax"] = cd["tcpamax"]
+            res["min_sep"] = cd["min_sep"]
+            res["cd"] = cd
+        return res
+
+    def _commit(self, res, live):
+        self.wpt_reach = np.where(live, res["_new_wr"], self.wpt_reach).astype(np.int32)
+        self.drift_sum = np.where(live, self.drift_sum + res["_d"], self.drift_sum)
+        self.drift_cnt = self.drift_cnt + live
+        self.total_intrusions = self.total_intrusions + np.where(live, res["nintr"], 0).astype(np.int32)
+        self.total_reward = np.where(live, self.total_reward + res["reward"], self.total_reward)
+
+    def info(self):
+        with np.errstate(invalid="ignore", divide="ignore"):
+            avg = self.drift_sum / self.drift_cnt
+        return {"total_reward": self.total_reward.copy(),
+                "total_intrusions": self.total_intrusions.copy(),
+                "average_drift": np.where(self.drift_cnt > 0, avg, np.nan)}
+
+
+def horizontal_spawn_from_np_random(rs, num_intruders):
+    """np.random draws of horizontal_cr_env.py:130-132 (per intruder) then :140."""
+    out = []
+    for _ in range(num_intruders):
+        out += [float(rs.randint(45, 315)), float(rs.randint(0, H_INTRUSION_DISTANCE)),
+                float(rs.randint(100, 1000))]
+    out.append(float(rs.randint(H_WAYPOINT_DISTANCE_MIN, H_WAYPOINT_DISTANCE_MAX)))
+    return np.array(out, np.float64)
 
 
 def _rows_to_u64(m):

@@ -21,6 +21,7 @@ MASK32 = np.uint64(0xFFFFFFFF)
 TAG_MERGE = 0x4D455247      # 'MERG'
 TAG_VERT = 0x56455254       # 'VERT'
 TAG_DESC = 0x44455343       # 'DESC'
+TAG_HORZ = 0x484F525A       # 'HORZ'
 
 
 def philox4x32_10(c0, c1, c2, c3, seed):

@@ -312,6 +312,7 @@ def load_reference_envs(reference_root="/root/reference"):
         "merge": importlib.import_module("bluesky_gym.envs.merge_env"),
         "vertical": importlib.import_module("bluesky_gym.envs.vertical_cr_env"),
         "descent": importlib.import_module("bluesky_gym.envs.descent_env"),
+        "horizontal": importlib.import_module("bluesky_gym.envs.horizontal_cr_env"),
         "functions": importlib.import_module("bluesky_gym.envs.common.functions"),
     }
     return bs, out

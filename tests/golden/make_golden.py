@@ -142,6 +142,57 @@ def gen_vertical(bs, mods, num_intruders, episodes, seed, max_steps=300):
     return out
 
 
+def gen_horizontal(bs, mods, num_intruders, episodes, seed, max_steps=300):
+    m = mods["horizontal"]
+    m.NUM_INTRUDERS = num_intruders
+    np.random.seed(seed)
+    rng_act = np.random.default_rng(seed)
+    env = m.HorizontalCREnv()
+    rec = {k: [] for k in ("spawn", "obs0", "actions", "obs", "reward", "terminated",
+                           "truncated", "intr", "state", "info", "length", "wpt")}
+    for ep in range(episodes):
+        rs = np.random.RandomState()
+        rs.set_state(np.random.get_state())
+        spawn = ob.horizontal_spawn_from_np_random(rs, num_intruders)
+        obs0, _ = env.reset()
+        acts = rng_act.uniform(-1, 1, (max_steps, 1))
+        O, R, T, TR, IN, ST, INF = [], [], [], [], [], [], []
+        for t in range(max_steps):
+            obs, rew, term, trunc, info = env.step(acts[t])
+            trunc = (t + 1) >= max_steps
+            O.append(flat(obs, ob.HORIZONTAL_OBS_KEYS)); R.append(rew); T.append(int(term))
+            TR.append(trunc)
+            INF.append([info["total_reward"], info["total_intrusions"], info["average_drift"]])
+            if term:        # the env deleted every aircraft (horizontal_cr_env.py:119-122)
+                ST.append(ST[-1] if ST else np.zeros((len(STATE_FIELDS), num_intruders + 1)))
+                IN.append(np.zeros(num_intruders, bool))
+                break
+            ST.append(snap(bs))
+            lat, lon = bs.traf.lat, bs.traf.lon
+            _, di = bs.tools.geo.kwikqdrdist(lat[0], lon[0], lat[1:], lon[1:])
+            IN.append(di < m.INTRUSION_DISTANCE)
+            if trunc:
+                break
+        L = len(O)
+        pad = lambda a, shape, dt: np.concatenate([np.asarray(a, dt), np.zeros((max_steps - L,) + shape, dt)])
+        rec["spawn"].append(spawn)
+        rec["obs0"].append(flat(obs0, ob.HORIZONTAL_OBS_KEYS))
+        rec["actions"].append(acts)
+        rec["obs"].append(pad(O, (len(O[0]),), np.float64))
+        rec["reward"].append(pad(R, (), np.float64))
+        rec["terminated"].append(pad(T, (), np.int8))
+        rec["truncated"].append(pad(TR, (), np.int8))
+        rec["intr"].append(pad(IN, (num_intruders,), np.int8))
+        rec["state"].append(pad(ST, ST[0].shape, np.float64))
+        rec["info"].append(pad(INF, (3,), np.float64))
+        rec["length"].append(L)
+        rec["wpt"].append([env.wpt_lat[0], env.wpt_lon[0]])
+    out = {k: np.stack(v) if k != "length" else np.array(v) for k, v in rec.items()}
+    out["num_ac"] = np.array(num_intruders + 1)
+    out["seed"] = np.array(seed)
+    return out
+
+
 def gen_descent(bs, mods, episodes, seed, max_steps=300):
     m = mods["descent"]
     np.random.seed(seed)
@@ -202,6 +253,8 @@ def main():
         ("vertical_N6", lambda: gen_vertical(bs, mods, 5, 3, 4)),
         ("vertical_N32", lambda: gen_vertical(bs, mods, 31, 2, 5)),
         ("descent", lambda: gen_descent(bs, mods, 4, 6)),
+        ("horizontal_N6", lambda: gen_horizontal(bs, mods, 5, 3, 7)),
+        ("horizontal_N16", lambda: gen_horizontal(bs, mods, 15, 2, 8)),
     ]
     for name, job in jobs:
         out = job()

@@ -25,7 +25,7 @@ def test_register_envs_matches_reference_ids_and_limits():
     for k, v in expect.items():
         assert reg[k].max_episode_steps == v
         assert reg[k].entry_point.startswith("bluesky_gym.envs.")
-    for k in ("MergeEnv-v0", "VerticalCREnv-v0", "DescentEnv-v0"):
+    for k in ("MergeEnv-v0", "VerticalCREnv-v0", "DescentEnv-v0", "HorizontalCREnv-v0"):
         assert reg[k].vector_entry_point.startswith("bluesky_gym.vector:")
     with pytest.raises(NotImplementedError):
         _gym.make("SectorCREnv-v0")
@@ -38,6 +38,8 @@ def test_obs_layout_keys_sorted_like_gymnasium():
     assert list(v.keys) == list(ob.VERTICAL_OBS_KEYS) and v.dim == 39
     d = ObsLayout(nat.ENV_DESCENT, 1, 0)
     assert list(d.keys) == list(ob.DESCENT_OBS_KEYS) and d.dim == 4
+    h = ObsLayout(nat.ENV_HORIZONTAL_CR, 6, 0)
+    assert list(h.keys) == list(ob.HORIZONTAL_OBS_KEYS) and h.dim == 28
     space = m.observation_space(_gym.spaces)
     assert list(space.spaces) == sorted(space.spaces)
 
@@ -63,3 +65,23 @@ def test_descent_host_spawn_consumes_np_random_like_reference():
     np.random.seed(6)
     for ep in range(len(g["length"])):
         assert np.array_equal(spawn.descent_spawn(), g["spawn"][ep])
+
+
+@pytest.mark.parametrize("name,seed", [("horizontal_N6", 7), ("horizontal_N16", 8)])
+def test_horizontal_host_spawn_consumes_np_random_like_reference(name, seed):
+    g = dict(np.load(f"{GOLD}/{name}.npz"))
+    np.random.seed(seed)
+    for ep in range(len(g["length"])):
+        assert np.array_equal(spawn.horizontal_spawn(int(g["num_ac"]) - 1), g["spawn"][ep])
+
+
+def test_device_spawn_draws_in_reference_ranges():
+    """The Philox spawn distributions stay inside the reference's randint ranges."""
+    o = ob.HorizontalOracle(512, num_ac=6, seed=3)
+    sp = o.device_spawn_params(np.arange(512), np.zeros(512))
+    dpsi, cpa, tlosh = sp[:, 0:15:3], sp[:, 1:15:3], sp[:, 2:15:3]
+    assert dpsi.min() >= 45 and dpsi.max() < 315
+    assert cpa.min() >= 0 and cpa.max() < 5
+    assert tlosh.min() >= 100 and tlosh.max() < 1000
+    assert sp[:, -1].min() >= 100 and sp[:, -1].max() < 150
+    assert np.array_equal(sp, np.floor(sp))

@@ -55,7 +55,8 @@ def test_gym_make_merge_reproduces_reference_episode():
 def test_gym_make_vertical_and_descent_reproduce_reference():
     bluesky_gym.register_envs()
     for name, eid, seed, kw in (("vertical_N6", "VerticalCREnv-v0", 4, {}),
-                                ("descent", "DescentEnv-v0", 6, {})):
+                                ("descent", "DescentEnv-v0", 6, {}),
+                                ("horizontal_N6", "HorizontalCREnv-v0", 7, {})):
         g = dict(np.load(f"{GOLD}/{name}.npz"))
         np.random.seed(seed)
         env = _gym.make(eid, **kw)

@@ -118,6 +118,34 @@ def test_descent_golden_on_gpu(bg):
         assert np.array_equal(term.cpu().numpy()[live], g["terminated"][live, t].astype(np.uint8)), t
 
 
+@pytest.mark.parametrize("name", ["horizontal_N6", "horizontal_N16"])
+def test_horizontal_golden_on_gpu(bg, name):
+    core, config, nat = bg
+    g = load(name)
+    n_ep, T = g["actions"].shape[:2]
+    N = int(g["num_ac"])
+    b = core.DeviceBatch(config.horizontal_config(num_intruders=N - 1), n_ep,
+                         autoreset=nat.AUTORESET_NONE, compute_cd=True)
+    obs0 = b.reset(spawn=torch.from_numpy(g["spawn"])).cpu().numpy()
+    close(obs0, g["obs0"], "reset obs")
+    wpt = np.stack([b.envs["env_wpt_lat"].cpu().numpy(), b.envs["env_wpt_lon"].cpu().numpy()], 1)
+    assert np.array_equal(wpt, g["wpt"])
+    m = rp.step_mask(g)
+    act = torch.from_numpy(g["actions"]).cuda()
+    for t in range(T):
+        obs, rew, term, trunc = b.step(act[:, t])
+        live = m[:, t]
+        if not live.any():
+            break
+        close(obs.cpu().numpy()[live], g["obs"][live, t], f"obs t={t}")
+        close(rew.cpu().numpy()[live], g["reward"][live, t], f"reward t={t}")
+        assert np.array_equal(term.cpu().numpy()[live], g["terminated"][live, t].astype(np.uint8)), t
+        assert np.array_equal(trunc.cpu().numpy()[live], g["truncated"][live, t].astype(np.uint8)), t
+        nt = live & (g["terminated"][:, t] == 0)
+        ib = bits(b.intr_mask.cpu().numpy(), N)[:, 1:]
+        assert np.array_equal(ib[nt], g["intr"][nt, t]), t
+
+
 def _compare_step(b, r, N, kind, t):
     close(b.obs.cpu().numpy(), r["obs"], f"obs t={t}")
     close(b.reward.cpu().numpy(), r["reward"], f"reward t={t}")
@@ -175,6 +203,32 @@ def test_vertical_batch_autoreset_parity(bg, N):
         b.step(torch.from_numpy(a))
         r = o.step(a)
         _compare_step(b, r, N, "vertical", t)
+
+
+@pytest.mark.parametrize("N,autoreset", [(6, ob.AUTORESET_NEXT_STEP), (6, ob.AUTORESET_SAME_STEP),
+                                         (32, ob.AUTORESET_NEXT_STEP)])
+def test_horizontal_batch_autoreset_parity(bg, N, autoreset):
+    """Device Philox spawns, random headings, short TimeLimit (40) so that every env
+    auto-resets at least twice; waypoint reaches terminate some episodes early."""
+    core, config, nat = bg
+    E, T = 128, 90
+    b = core.DeviceBatch(config.horizontal_config(num_intruders=N - 1, max_episode_steps=40), E,
+                         autoreset=autoreset, compute_cd=True, seed=17)
+    o = ob.HorizontalOracle(E, num_ac=N, seed=17, compute_cd=True, max_episode_steps=40,
+                            autoreset=autoreset)
+    close(b.reset().cpu().numpy(), o.reset()["obs"], "reset obs")
+    rng = np.random.default_rng(5)
+    for t in range(T):
+        a = rng.uniform(-1, 1, (E, 1))
+        b.step(torch.from_numpy(a))
+        r = o.step(a)
+        _compare_step(b, r, N, "horizontal", t)
+        if autoreset == ob.AUTORESET_SAME_STEP and r["final_obs"] is not None:
+            d = r["terminated"] | r["truncated"]
+            close(b.final_obs.cpu().numpy()[d], r["final_obs"][d], f"final_obs t={t}")
+    # device asin/atan2 vs host libm: the waypoint agrees to a few ulp (~1e-14 deg)
+    np.testing.assert_allclose(b.envs["env_wpt_lat"].cpu().numpy(), o.wpt_lat, rtol=0, atol=1e-12)
+    np.testing.assert_allclose(b.envs["env_wpt_lon"].cpu().numpy(), o.wpt_lon, rtol=0, atol=1e-12)
 
 
 def test_descent_batch_autoreset_parity(bg):

@@ -81,6 +81,25 @@ def test_descent_oracle_matches_reference():
     assert np.array_equal(r["state"][nt], g["state"][nt])
 
 
+@pytest.mark.parametrize("name", ["horizontal_N6", "horizontal_N16"])
+def test_horizontal_oracle_matches_reference(name):
+    g = load(name)
+    r = rp.replay_horizontal(g)
+    m = rp.step_mask(g)
+    assert np.array_equal(r["obs0"], g["obs0"])
+    assert np.array_equal(r["wpt"], g["wpt"])
+    for k in ("obs", "reward"):
+        assert np.array_equal(r[k][m], g[k][m]), k
+    assert np.array_equal(r["terminated"][m].astype(np.int8), g["terminated"][m])
+    ri, gi = r["info"][m], g["info"][m]
+    for c in (0, 1):
+        assert np.array_equal(ri[:, c], gi[:, c])
+    np.testing.assert_allclose(ri[:, 2], gi[:, 2], rtol=1e-14, atol=0)   # average_drift
+    nt = _nonterminal(g)
+    assert np.array_equal(r["state"][nt], g["state"][nt])
+    assert np.array_equal(r["intr"][nt], g["intr"][nt])
+
+
 def test_merge_distribution_sanity():
     """Random-policy Merge episodes land in the published untrained-policy band
     (~1.3-1.5 intrusions, ~-9 return, average drift ~1.5 rad)."""
