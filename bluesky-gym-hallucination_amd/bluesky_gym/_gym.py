@@ -4,7 +4,8 @@ Uses the real ``gymnasium`` when it is importable (the reference pins gymnasium=
 pyproject.toml:11).  This image has no gymnasium, so a minimal stand-in with the same
 names and semantics for the pieces this package uses is provided: ``Env``,
 ``spaces.Box``, ``spaces.Dict`` (sorted keys), ``register`` / ``make`` / ``make_vec`` /
-``registry`` (incl. ``vector_entry_point``), ``TimeLimit`` and ``vector.VectorEnv``.
+``registry`` (incl. ``vector_entry_point``), ``TimeLimit``, ``Wrapper`` and
+``vector.VectorEnv``.
 It carries no simulation code.
 """
 from __future__ import annotations
@@ -17,9 +18,10 @@ try:  # pragma: no cover - exercised only where gymnasium is installed
     import gymnasium as gym  # noqa: F401
     from gymnasium import spaces  # noqa: F401
     from gymnasium.envs.registration import register, registry  # noqa: F401
-    from gymnasium.vector import VectorEnv  # noqa: F401
+    from gymnasium.vector import VectorEnv, VectorWrapper  # noqa: F401
     from gymnasium.wrappers import TimeLimit  # noqa: F401
     Env = gym.Env
+    Wrapper = gym.Wrapper
     make = gym.make
     make_vec = gym.make_vec
     HAVE_GYMNASIUM = True
@@ -114,6 +116,46 @@ except ImportError:
         def close(self):
             pass
 
+    class Wrapper:
+        """gymnasium.Wrapper: forwards reset/step/close; observation_space and
+        action_space default to the wrapped env's unless assigned."""
+
+        def __init__(self, env):
+            self.env = env
+            self._observation_space = None
+            self._action_space = None
+
+        @property
+        def observation_space(self):
+            return self._observation_space if self._observation_space is not None \
+                else self.env.observation_space
+
+        @observation_space.setter
+        def observation_space(self, space):
+            self._observation_space = space
+
+        @property
+        def action_space(self):
+            return self._action_space if self._action_space is not None \
+                else self.env.action_space
+
+        @action_space.setter
+        def action_space(self, space):
+            self._action_space = space
+
+        @property
+        def unwrapped(self):
+            return self.env.unwrapped
+
+        def reset(self, **kw):
+            return self.env.reset(**kw)
+
+        def step(self, action):
+            return self.env.step(action)
+
+        def close(self):
+            return self.env.close()
+
     class TimeLimit:
         """gymnasium.wrappers.TimeLimit: truncated once elapsed >= max_episode_steps."""
 
@@ -144,8 +186,14 @@ except ImportError:
         metadata = {"autoreset_mode": "NextStep"}
         num_envs = 1
 
+        @property
+        def unwrapped(self):
+            return self
+
         def close(self):
             pass
+
+    VectorWrapper = Wrapper
 
     class EnvSpec:
         def __init__(self, id, entry_point, max_episode_steps=None, vector_entry_point=None,

@@ -12,8 +12,9 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("BSG_LIBRARY", os.path.join(_HERE, "_lib", "libbsg.so"))
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 MAX_ROUTE = 4
+WIND_NALT = 451
 
 ENV_MERGE, ENV_VERTICAL_CR, ENV_DESCENT, ENV_HORIZONTAL_CR = 0, 1, 2, 3
 AUTORESET_NONE, AUTORESET_NEXT_STEP, AUTORESET_SAME_STEP = 0, 1, 2
@@ -56,7 +57,7 @@ class BsgConfig(C.Structure):
 BUFFER_FIELDS = [
     ("lat", _dp), ("lon", _dp), ("alt", _dp), ("hdg", _dp), ("tas", _dp), ("cas", _dp),
     ("vs", _dp), ("ax", _dp), ("ap_trk", _dp), ("selspd", _dp), ("selalt", _dp),
-    ("selvs", _dp), ("nav", _i32p),
+    ("selvs", _dp), ("nav", _i32p), ("gs", _dp), ("trk", _dp),
     ("step_count", _i32p), ("flags", _i32p), ("episode", _u32p), ("wpt_reach", _i32p),
     ("faf_reached", _i32p), ("total_intrusions", _i32p), ("total_reward", _dp),
     ("drift_sum", _dp), ("target_alt", _dp), ("final_altitude", _dp),
@@ -72,10 +73,20 @@ class BsgBuffers(C.Structure):
     _fields_ = [(n, t) for n, t in BUFFER_FIELDS]
 
 
+class BsgWind(C.Structure):
+    _fields_ = [
+        ("num_points", C.c_int32),
+        ("num_levels", C.c_int32),
+        ("augment_obs", C.c_int32),
+        ("reserved", C.c_int32),
+        ("lat", _dp), ("lon", _dp), ("vnorth", _dp), ("veast", _dp),
+    ]
+
+
 EXPORTED_SYMBOLS = (
     "bsg_abi_version", "bsg_last_error", "bsg_obs_dim", "bsg_action_dim", "bsg_spawn_width",
     "bsg_create", "bsg_destroy", "bsg_bind", "bsg_reset", "bsg_step", "bsg_set_timing",
-    "bsg_step_timing", "bsg_set_stamps",
+    "bsg_step_timing", "bsg_set_stamps", "bsg_set_wind", "bsg_ctx_obs_dim",
 )
 
 _lib = None
@@ -123,6 +134,10 @@ def load_library(path: str | None = None):
     lib.bsg_step_timing.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_int32)]
     lib.bsg_set_stamps.restype = C.c_int32
     lib.bsg_set_stamps.argtypes = [C.c_void_p, C.c_void_p]
+    lib.bsg_set_wind.restype = C.c_int32
+    lib.bsg_set_wind.argtypes = [C.c_void_p, C.POINTER(BsgWind)]
+    lib.bsg_ctx_obs_dim.restype = C.c_int32
+    lib.bsg_ctx_obs_dim.argtypes = [C.c_void_p]
     if lib.bsg_abi_version() != ABI_VERSION:
         raise BsgError(f"libbsg ABI {lib.bsg_abi_version()} != expected {ABI_VERSION}")
     if path is None:

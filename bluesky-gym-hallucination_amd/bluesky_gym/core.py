@@ -39,6 +39,8 @@ class DeviceBatch:
         self.spawn_width = self.lib.bsg_spawn_width(cfg.kind, cfg.num_ac)
         self.env_offset = int(env_offset)
         self.seed = int(seed)
+        self.wind = None
+        self.wind_augment = False
         ccfg = cfg.to_c(self.E, autoreset, self.compute_cd, seed, self.device.index, env_offset)
         ctx = C.c_void_p()
         nat.check(self.lib.bsg_create(C.byref(ccfg), C.byref(ctx)), "bsg_create")
@@ -76,6 +78,40 @@ class DeviceBatch:
             self.min_sep = z((E,), torch.float32)
         else:
             self.conf_mask = self.los_mask = self.tcpamax = self.min_sep = None
+
+    def set_wind(self, table, augment_obs=False):
+        """Apply a wind field (bluesky_gym.wind.WindTable, or None to clear) to every env
+        from the next launch on (wrappers/wind.py).  augment_obs widens the obs rows by
+        wind_u / wind_v; the obs buffers are reallocated then (call reset afterwards)."""
+        d = self.device
+        w = nat.BsgWind()
+        if table is not None:
+            self._wind_tabs = [torch.as_tensor(a, dtype=torch.float64).to(d).contiguous()
+                               for a in (table.lat, table.lon, table.vnorth, table.veast)]
+            w.num_points = table.num_points
+            w.num_levels = table.num_levels
+            w.augment_obs = int(bool(augment_obs))
+            w.lat, w.lon, w.vnorth, w.veast = (C.cast(C.c_void_p(t.data_ptr()), nat._dp)
+                                               for t in self._wind_tabs)
+            if "gs" not in self.state:
+                # without wind gs = tas and trk = hdg exactly (Traffic.update_groundspeed)
+                self.state["gs"] = self.state["tas"].clone()
+                self.state["trk"] = self.state["hdg"].clone()
+        else:
+            self._wind_tabs = None
+        nat.check(self.lib.bsg_set_wind(self._ctx, C.byref(w)), "bsg_set_wind")
+        od = self.lib.bsg_ctx_obs_dim(self._ctx)
+        if od != self.obs_dim:
+            self.obs_dim = od
+            z = lambda shape: torch.zeros(shape, dtype=torch.float32, device=d)
+            self.obs = z((self.E, od))
+            if self.final_obs is not None:
+                self.final_obs = z((self.E, od))
+            if self.learner is not None:
+                self.learner = z((self.E, od + 3))
+        self.wind = table
+        self.wind_augment = table is not None and bool(augment_obs)
+        self._bind()
 
     def _bind(self):
         b = nat.BsgBuffers()

@@ -33,6 +33,13 @@ class SingleEnvBase(_gym.Env):
         self.batch = DeviceBatch(kind_cfg, 1, autoreset=nat.AUTORESET_NONE,
                                  compute_cd=compute_cd, device=device)
 
+    def set_wind(self, table, augment_obs=False):
+        """Wind field for this env (bluesky_gym.wrappers.wind.WindFieldWrapper)."""
+        k = self.kind_cfg
+        self.batch.set_wind(table, augment_obs)
+        self.layout = ObsLayout(k.kind, k.num_ac, k.num_ac_state, wind=self.batch.wind_augment)
+        self.observation_space = self.layout.observation_space(_gym.spaces)
+
     def _spawn(self):
         raise NotImplementedError
 

@@ -40,8 +40,28 @@ def descent_sizes():
 _BOUNDS = {"cos(drift)": (-1, 1), "sin(drift)": (-1, 1), "faf_reached": (0, 1)}
 
 
+WIND_KEYS = ("wind_u", "wind_v")     # bluesky_gym/wrappers/wind.py:21-22
+
+# insertion order of the observation dict each reference _get_obs builds (merge_env.py:222-
+# 235, vertical_cr_env.py:162-178, descent_env.py:110-116, horizontal_cr_env.py:205-214);
+# the dicts handed to users keep it (wrappers such as NoisyObservationWrapper draw their
+# noise in this order), the flat rows use the sorted order
+REF_ORDER = {
+    nat.ENV_MERGE: ("cos(drift)", "sin(drift)", "airspeed", "waypoint_dist", "faf_reached",
+                    "x_r", "y_r", "vx_r", "vy_r", "cos(track)", "sin(track)", "distances"),
+    nat.ENV_VERTICAL_CR: ("altitude", "vz", "target_altitude", "runway_distance",
+                          "intruder_distance", "cos_difference_pos", "sin_difference_pos",
+                          "altitude_difference", "x_difference_speed", "y_difference_speed",
+                          "z_difference_speed"),
+    nat.ENV_DESCENT: ("altitude", "vz", "target_altitude", "runway_distance"),
+    nat.ENV_HORIZONTAL_CR: ("intruder_distance", "cos_difference_pos", "sin_difference_pos",
+                            "x_difference_speed", "y_difference_speed", "waypoint_distance",
+                            "cos_drift", "sin_drift"),
+}
+
+
 class ObsLayout:
-    def __init__(self, kind, num_ac, num_ac_state):
+    def __init__(self, kind, num_ac, num_ac_state, wind=False):
         if kind == nat.ENV_MERGE:
             sizes = merge_sizes(num_ac_state)
         elif kind == nat.ENV_VERTICAL_CR:
@@ -50,7 +70,10 @@ class ObsLayout:
             sizes = horizontal_sizes(num_ac - 1)
         else:
             sizes = descent_sizes()
+        if wind:
+            sizes.update({k: 1 for k in WIND_KEYS})
         self.keys = tuple(sorted(sizes))
+        self.ref_order = REF_ORDER[kind] + (WIND_KEYS if wind else ())
         self.sizes = {k: sizes[k] for k in self.keys}
         off = 0
         self.slices = {}
@@ -60,9 +83,10 @@ class ObsLayout:
         self.dim = off
 
     def split(self, flat) -> dict:
-        """[..., dim] -> {key: [..., size]} (float64 numpy, like the reference obs)."""
+        """[..., dim] -> {key: [..., size]} (float64 numpy, like the reference obs, in the
+        reference's key insertion order)."""
         flat = np.asarray(flat, np.float64)
-        return {k: flat[..., s] for k, s in self.slices.items()}
+        return {k: flat[..., self.slices[k]] for k in self.ref_order}
 
     def observation_space(self, spaces):
         return spaces.Dict({k: spaces.Box(*_BOUNDS.get(k, (-np.inf, np.inf)), shape=(n,),

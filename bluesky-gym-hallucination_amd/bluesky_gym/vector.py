@@ -54,8 +54,20 @@ class BlueSkyVectorEnv(_gym.VectorEnv):
         self.action_space = _gym.spaces.Box(-1, 1, shape=(self.num_envs, act), dtype=np.float64)
         self._seed = seed
         self._host_rngs = None
+        self._wind = None
         self.batch = DeviceBatch(kind_cfg, self.num_envs, autoreset=autoreset, compute_cd=compute_cd,
                                  seed=seed, device=device, learner=learner, env_offset=env_offset)
+
+    def set_wind(self, table, augment_obs=False):
+        """Wind field for every env of the batch (bluesky_gym.wrappers.wind)."""
+        k = self.kind_cfg
+        self._wind = (table, augment_obs)
+        self.batch.set_wind(table, augment_obs)
+        self.layout = ObsLayout(k.kind, k.num_ac, k.num_ac_state, wind=self.batch.wind_augment)
+        self.single_observation_space = self.layout.observation_space(_gym.spaces)
+        self.observation_space = _gym.spaces.Dict(
+            {key: _gym.spaces.Box(-np.inf, np.inf, shape=(self.num_envs, n), dtype=np.float64)
+             for key, n in self.layout.sizes.items()})
 
     # ---------------------------------------------------------------- spawns
     def _host_spawn(self, mask=None):
@@ -90,6 +102,8 @@ class BlueSkyVectorEnv(_gym.VectorEnv):
             self.batch = DeviceBatch(self.kind_cfg, self.num_envs, autoreset=self.autoreset,
                                      compute_cd=self.compute_cd, seed=seed, device=self.device,
                                      learner=self.learner, env_offset=self.env_offset)
+            if self._wind is not None:
+                self.batch.set_wind(*self._wind)
         sp = self._host_spawn() if self.spawn_mode == "host" else None
         self.batch.reset(spawn=sp)
         return self.layout.split(self.batch.obs.cpu().numpy()), self._infos(done=None)

@@ -21,6 +21,7 @@ struct bsg_ctx {
   int obs_dim = 0;
   int spawn_width = 0;
   bsg::Route route{};
+  bsg::WindDev wind{};
   // optional per-launch timing (bsg_set_timing)
   bool timing = false;
   unsigned long long* stamps = nullptr;
@@ -56,6 +57,19 @@ hipEvent_t take_event(bsg_ctx* c) {
   return e;
 }
 
+// sorted-key position of wind_u among the env kind's observation keys (wind.py:18-24 adds
+// wind_u/wind_v; gymnasium spaces.Dict sorts): right before the first key > "wind_v"
+int wind_obs_pos(const bsg_config& cfg) {
+  const int K = cfg.num_ac_state, NI = cfg.num_ac - 1;
+  switch (cfg.env_kind) {
+    case BSG_ENV_MERGE: return 5 + 5 * K;          // ... waypoint_dist | x_r, y_r
+    case BSG_ENV_VERTICAL_CR: return 4 + 4 * NI;   // ... vz | x_/y_/z_difference_speed
+    case BSG_ENV_DESCENT: return 4;                 // all keys sort before "wind"
+    case BSG_ENV_HORIZONTAL_CR: return 3 * NI + 3; // ... waypoint_distance | x_/y_...
+    default: return 0;
+  }
+}
+
 bsg::KParams make_params(const bsg_ctx* c, int mode) {
   bsg::KParams p;
   std::memset(&p, 0, sizeof(p));
@@ -71,6 +85,8 @@ bsg::KParams make_params(const bsg_ctx* c, int mode) {
   p.seed = c->cfg.seed;
   p.stamps = c->stamps;
   p.lds_pad = c->lds_pad;
+  p.wind = c->wind;
+  p.wpos = wind_obs_pos(c->cfg);
   return p;
 }
 
@@ -199,6 +215,8 @@ int32_t bsg_bind(bsg_ctx* c, const bsg_buffers* b) {
     return fail(BSG_E_INVALID_ARG, "bsg_bind: Merge needs topk%s%lld");
   if (c->cfg.autoreset_mode == BSG_AUTORESET_SAME_STEP && !b->final_obs)
     return fail(BSG_E_INVALID_ARG, "bsg_bind: SAME_STEP autoreset needs final_obs%s%lld");
+  if (c->wind.np > 0 && (!b->gs || !b->trk))
+    return fail(BSG_E_INVALID_ARG, "bsg_bind: a wind field needs gs/trk%s%lld");
   if (c->cfg.compute_cd && c->cfg.env_kind != BSG_ENV_DESCENT &&
       (!b->conf_mask || !b->los_mask || !b->tcpamax || !b->min_sep))
     return fail(BSG_E_INVALID_ARG, "bsg_bind: compute_cd needs conf_mask/los_mask/tcpamax/min_sep%s%lld");
@@ -224,6 +242,35 @@ int32_t bsg_step(bsg_ctx* c, const double* actions, const double* spawn, void* s
   p.actions = actions;
   p.spawn = spawn;
   return launch(c, p, stream);
+}
+
+int32_t bsg_set_wind(bsg_ctx* c, const bsg_wind* w) {
+  if (!c) return fail(BSG_E_INVALID_ARG, "bsg_set_wind: null ctx%s%lld");
+  const int base = bsg_obs_dim(c->cfg.env_kind, c->cfg.num_ac, c->cfg.num_ac_state);
+  bsg::WindDev d{};
+  if (w && w->num_points > 0) {
+    if (w->num_points > 4096)
+      return fail(BSG_E_INVALID_ARG, "bsg_set_wind: num_points must be <= 4096%s (got %lld)", "", w->num_points);
+    if (w->num_levels != 1 && w->num_levels != BSG_WIND_NALT)
+      return fail(BSG_E_INVALID_ARG, "bsg_set_wind: num_levels must be 1 or BSG_WIND_NALT%s (got %lld)", "",
+                  w->num_levels);
+    if (!w->lat || !w->lon || !w->vnorth || !w->veast)
+      return fail(BSG_E_INVALID_ARG, "bsg_set_wind: null table pointer%s%lld");
+    d.np = w->num_points;
+    d.nlev = w->num_levels;
+    d.dim = d.nlev > 1 ? 3 : (d.np == 1 ? 1 : 2);
+    d.augment = w->augment_obs != 0;
+    d.lat = w->lat; d.lon = w->lon; d.vn = w->vnorth; d.ve = w->veast;
+  }
+  c->wind = d;
+  c->obs_dim = base + (d.augment ? 2 : 0);
+  c->bound = false;
+  return BSG_OK;
+}
+
+int32_t bsg_ctx_obs_dim(const bsg_ctx* c) {
+  if (!c) return fail(BSG_E_INVALID_ARG, "bsg_ctx_obs_dim: null ctx%s%lld");
+  return c->obs_dim;
 }
 
 int32_t bsg_set_stamps(bsg_ctx* c, void* buf) {

@@ -16,6 +16,14 @@ struct Route {
   double lat[BSG_MAX_ROUTE], lon[BSG_MAX_ROUTE], next_qdr[BSG_MAX_ROUTE];
 };
 
+struct WindDev {
+  int np;                    // points (0: wind off)
+  int nlev;                  // 1 or BSG_WIND_NALT
+  int dim;                   // 1 constant, 2 horizontal IDW, 3 IDW + altitude levels
+  int augment;               // obs carries wind_u / wind_v
+  const double *lat, *lon, *vn, *ve;
+};
+
 // Passed by value to every launch (kernarg segment).
 struct KParams {
   bsg_config cfg;
@@ -29,6 +37,8 @@ struct KParams {
   const uint8_t* env_mask;   // [E] or nullptr (all)  -- reset mode only
   unsigned long long* stamps; // diagnostics (BSG_STAMPS builds only)
   unsigned lds_pad;          // extra dynamic LDS per workgroup (occupancy shaping)
+  WindDev wind;
+  int wpos;                  // obs offset of wind_u (sorted-key position) when augmenting
 };
 
 hipError_t launch_step(const KParams& p, hipStream_t stream);

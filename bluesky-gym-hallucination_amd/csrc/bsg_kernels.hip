@@ -42,21 +42,26 @@ namespace bsg {
 struct AC {
   double lat, lon, alt, hdg, tas, cas, vs, ax;
   double ap_trk, selspd, selalt, selvs;
+  double gs, trk;                  // carried only with a wind field (else gs = tas, trk = hdg)
   int nav;
 };
 
+template <bool WIND>
 __device__ __forceinline__ void load_ac(const Buffers& b, size_t a, AC& s) {
   s.lat = b.lat[a]; s.lon = b.lon[a]; s.alt = b.alt[a]; s.hdg = b.hdg[a];
   s.tas = b.tas[a]; s.cas = b.cas[a]; s.vs = b.vs[a]; s.ax = b.ax[a];
   s.ap_trk = b.ap_trk[a]; s.selspd = b.selspd[a]; s.selalt = b.selalt[a]; s.selvs = b.selvs[a];
   s.nav = b.nav[a];
+  if constexpr (WIND) { s.gs = b.gs[a]; s.trk = b.trk[a]; }
 }
 
+template <bool WIND>
 __device__ __forceinline__ void store_ac(const Buffers& b, size_t a, const AC& s) {
   b.lat[a] = s.lat; b.lon[a] = s.lon; b.alt[a] = s.alt; b.hdg[a] = s.hdg;
   b.tas[a] = s.tas; b.cas[a] = s.cas; b.vs[a] = s.vs; b.ax[a] = s.ax;
   b.ap_trk[a] = s.ap_trk; b.selspd[a] = s.selspd; b.selalt[a] = s.selalt; b.selvs[a] = s.selvs;
   b.nav[a] = s.nav;
+  if constexpr (WIND) { b.gs[a] = s.gs; b.trk[a] = s.trk; }
 }
 
 // Traffic.cre (bluesky/traffic/traffic.py): creation state + autopilot holding it
@@ -67,7 +72,94 @@ __device__ __forceinline__ void cre(AC& s, double lat, double lon, double hdg, d
   casormach_at(spd, at, &tas, &cas);
   s.lat = lat; s.lon = lon; s.alt = alt; s.hdg = hdg; s.tas = tas; s.cas = cas;
   s.vs = 0.0; s.ax = 0.0; s.ap_trk = hdg; s.selspd = cas; s.selalt = alt; s.selvs = 0.0;
+  s.gs = tas; s.trk = hdg;
   s.nav = 0;
+}
+
+// ---- wind field (bluesky.traffic.windfield; oracle: bluesky_subset.WindField.getdata) ----
+constexpr double WIND_ALTSTEP = 100.0 * FT;
+constexpr double WIND_ALTMAX = 45000.0 * FT;
+
+__device__ __forceinline__ double idw_weight(double lat, double lon, double latp, double lonp) {
+  const double cavelat = cos((0.5 * (lat + latp)) * kD2R);
+  const double dy = (lat - latp) * kD2R;
+  const double dx = cavelat * ((lon - lonp) * kD2R);
+  return 1.0 / (1e-16 + dx * dx + dy * dy);
+}
+
+__device__ __forceinline__ void wind_column(const WindDev& w, int q, int ia, double fa,
+                                            double* cn, double* ce) {
+  if (w.dim == 3) {
+    const int P = w.np;
+    *cn = (1.0 - fa) * w.vn[ia * P + q] + fa * w.vn[(ia + 1) * P + q];
+    *ce = (1.0 - fa) * w.ve[ia * P + q] + fa * w.ve[(ia + 1) * P + q];
+  } else {
+    *cn = w.vn[q];
+    *ce = w.ve[q];
+  }
+}
+
+// getdata(lat, lon, alt): constant (one point), or inverse-distance-squared weights summed
+// in point order, with linear interpolation between the fixed altitude levels (dim 3)
+__device__ __forceinline__ void wind_at(const WindDev& w, double lat, double lon, double alt,
+                                     double* vn, double* ve) {
+  if (w.dim == 1) { *vn = w.vn[0]; *ve = w.ve[0]; return; }
+  const int P = w.np;
+  int ia = 0;
+  double fa = 0.0;
+  if (w.dim == 3) {
+    const double idx = npmin(npmax(alt, 0.0), WIND_ALTMAX) / WIND_ALTSTEP;
+    ia = (int)floor(idx);
+    if (ia > BSG_WIND_NALT - 2) ia = BSG_WIND_NALT - 2;
+    fa = idx - (double)ia;
+  }
+  double S = 0.0, an = 0.0, ae = 0.0;
+  constexpr int R = 8;             // points whose weights stay in registers
+  if (P <= R) {
+    double wr[R];
+#pragma unroll
+    for (int q = 0; q < R; ++q) {
+      if (q < P) { wr[q] = idw_weight(lat, lon, w.lat[q], w.lon[q]); S = S + wr[q]; }
+    }
+#pragma unroll
+    for (int q = 0; q < R; ++q) {
+      if (q < P) {
+        const double h = wr[q] / S;
+        double cn, ce;
+        wind_column(w, q, ia, fa, &cn, &ce);
+        an = an + cn * h;
+        ae = ae + ce * h;
+      }
+    }
+  } else {
+    for (int q = 0; q < P; ++q) S = S + idw_weight(lat, lon, w.lat[q], w.lon[q]);
+    for (int q = 0; q < P; ++q) {
+      const double h = idw_weight(lat, lon, w.lat[q], w.lon[q]) / S;
+      double cn, ce;
+      wind_column(w, q, ia, fa, &cn, &ce);
+      an = an + cn * h;
+      ae = ae + ce * h;
+    }
+  }
+  *vn = an;
+  *ve = ae;
+}
+
+// Autopilot.selhdgcmd with wind: the HDG command becomes the track flown through the wind
+// triangle at the current position when airborne (alt > 50 ft)
+template <bool WIND>
+__device__ __forceinline__ double hdg_command_track(const WindDev& w, const AC& s, double hdg) {
+  if constexpr (WIND) {
+    if (s.alt > 50.0 * FT) {
+      double wn, we;
+      wind_at(w, s.lat, s.lon, s.alt, &wn, &we);
+      double sh, ch;
+      sincos(hdg * kD2R, &sh, &ch);
+      const double tasnorth = s.tas * ch, taseast = s.tas * sh;
+      return pymod(atan2(taseast + we, tasnorth + wn) * kR2D, 360.0);
+    }
+  }
+  return hdg;
 }
 
 // ---- exact memo of pure functions across substeps ---------------------------------------
@@ -123,17 +215,23 @@ __device__ __forceinline__ void memo_wp(Memo& m, const RouteRegs& rt, int k) {
   sincos(m.wp_lat * kD2R, &m.wp_sin, &m.wp_cos);
 }
 
-// ---- one BlueSky substep of one aircraft (Traffic.update, wind off, RESO OFF) ---------
-// oracle/bluesky_subset.py: traffic_update
-__device__ __forceinline__ void substep(AC& s, Memo& m, double dt, const RouteRegs& rt) {
-  // Autopilot.update -- LNAV direct-to + ActiveWaypoint.reached (gs = tas, trk = hdg)
+// ---- one BlueSky substep of one aircraft (Traffic.update, RESO OFF) ------------------
+// oracle/bluesky_subset.py: traffic_update.  WIND: a wind field is set (wrappers/wind.py).
+template <bool WIND>
+__device__ __forceinline__ void substep(AC& s, Memo& m, double dt, const RouteRegs& rt,
+                                        const WindDev& w) {
+  double vwn = 0.0, vwe = 0.0;
+  if constexpr (WIND) wind_at(w, s.lat, s.lon, s.alt, &vwn, &vwe);
+  const double gsv = WIND ? s.gs : s.tas;     // without wind gs = tas and trk = hdg
+  const double trkv = WIND ? s.trk : s.hdg;
+  // Autopilot.update -- LNAV direct-to + ActiveWaypoint.reached
   if (s.nav & 1) {
     int k = (s.nav >> 8) & 0xff;
     if (k != m.wp_k) memo_wp(m, rt, k);
     // the waypoint distance only feeds `dist < turndist` (turndist <= turnrad while the
     // leg change is <= 90 deg) and `dist/|gs| < 4 s`; beyond both it need not be exact
     const double turnrad = s.tas * s.tas / (npmax(0.01, TAN_BANKDEF) * G0);
-    const double far_m = npmax(turnrad, 4.0 * fabs(s.tas)) * 1.000001 + 1.0;
+    const double far_m = npmax(turnrad, 4.0 * fabs(gsv)) * 1.000001 + 1.0;
     double qdr, dnm;
     qdrdist_cached(s.lat, s.lon, m.coslat, m.sinlat, m.wp_lat, m.wp_lon, m.wp_cos, m.wp_sin,
                    far_m, &qdr, &dnm);
@@ -152,11 +250,11 @@ __device__ __forceinline__ void substep(AC& s, Memo& m, double dt, const RouteRe
         const double turndist = fabs(turnrad * tan(half * kD2R));
         reached_turn = dist < turndist;
       }
-      const double g = npmax(0.0001, fabs(s.tas));
+      const double g = npmax(0.0001, fabs(gsv));
       // dist/g < 4, decided without the division outside a 1e-6 band around 4*g
       const bool close2wp = dist < 4.0 * g * 0.999999 ? true
                           : (dist > 4.0 * g * 1.000001 ? false : dist / g < 4.0);
-      const bool tooclose = close2wp && (fabs(degto180(pymod(s.hdg, 360.0) - pymod(qdr, 360.0))) > 90.0);
+      const bool tooclose = close2wp && (fabs(degto180(pymod(trkv, 360.0) - pymod(qdr, 360.0))) > 90.0);
       reached = reached_turn || tooclose;
     }
     if (reached) {
@@ -183,7 +281,17 @@ __device__ __forceinline__ void substep(AC& s, Memo& m, double dt, const RouteRe
   }
   // aporasas
   const double vs_cmd0 = fabs(ap_vs);
-  const double hdg_cmd = pymod(s.ap_trk, 360.0);
+  double hdg_cmd;
+  if constexpr (WIND) {
+    // ActivePilot: heading that flies the commanded track through the wind
+    const double Vw = sqrt(vwn * vwn + vwe * vwe);
+    const double winddir = atan2(vwe, vwn);
+    const double drift = s.ap_trk * kD2R - winddir;
+    const double steer = asin(npmin(1.0, npmax(-1.0, Vw * sin(drift) / npmax(0.001, s.tas))));
+    hdg_cmd = pymod(s.ap_trk + steer * kR2D, 360.0);
+  } else {
+    hdg_cmd = pymod(s.ap_trk, 360.0);
+  }
   // PerfModel.limits (frozen A320 envelope)
   const double allow_h = ap_alt > HMAX ? HMAX : ap_alt;
   const uint64_t hb = bits(allow_h);
@@ -224,11 +332,23 @@ __device__ __forceinline__ void substep(AC& s, Memo& m, double dt, const RouteRe
   const double az = (double)need_az * sgn(delta_vs) * (300 * FPM);
   s.vs = need_az ? s.vs + az * dt : target_vs;
   if (!isfinite(s.vs)) s.vs = 0.0;
-  // update_groundspeed (no wind) + update_pos
+  // update_groundspeed + update_pos
   double shdg, chdg;
   sincos(s.hdg * kD2R, &shdg, &chdg);
-  const double gsnorth = s.tas * chdg;
-  const double gseast = s.tas * shdg;
+  double gsnorth = s.tas * chdg;
+  double gseast = s.tas * shdg;
+  if constexpr (WIND) {
+    const bool applywind = s.alt > 50.0 * FT;     // airborne (altitude before update_pos)
+    gsnorth = gsnorth + vwn * (double)applywind;
+    gseast = gseast + vwe * (double)applywind;
+    if (applywind) {
+      s.gs = sqrt(gsnorth * gsnorth + gseast * gseast);
+      s.trk = pymod(atan2(gseast, gsnorth) * kR2D, 360.0);
+    } else {
+      s.gs = s.tas;
+      s.trk = s.hdg;
+    }
+  }
   s.alt = swaltsel ? rint((s.alt + s.vs * dt) * 1e6) / 1e6 : allow_h;
   s.lat = s.lat + (dt * gsnorth / Rearth) * kR2D;
   sincos(s.lat * kD2R, &m.sinlat, &m.coslat);
@@ -236,21 +356,56 @@ __device__ __forceinline__ void substep(AC& s, Memo& m, double dt, const RouteRe
 }
 
 // ---- LDS staging (one wave per block; GS lanes per env) -------------------------------
-struct Lds {
+template <bool WIND> struct LdsWind {};
+template <> struct LdsWind<true> {
+  double gs[64];                   // ground speed (Vertical/Horizontal obs)
+  double cu[64], cv[64];           // StateBased gs*sin(trk), gs*cos(trk)
+};
+
+template <bool WIND>
+struct Lds : LdsWind<WIND> {
+  static constexpr bool kWind = WIND;
+  // u = tas*sin(hdg), v = tas*cos(hdg): the Merge obs velocities, and StateBased's
+  // gs*sin(trk) / gs*cos(trk) when there is no wind
   double lat[64], lon[64], alt[64], hdg[64], tas[64], vs[64], u[64], v[64], d[64];
   int done[64];
   // StateBased assembly (LDS atomics)
   unsigned long long cm[64], lm[64], tmax[64], gmin[64];
 };
 
-__device__ __forceinline__ void stage(Lds& L, int lane, const AC& s) {
+template <class LT>
+__device__ __forceinline__ void stage(LT& L, int lane, const AC& s) {
   L.lat[lane] = s.lat; L.lon[lane] = s.lon; L.alt[lane] = s.alt; L.hdg[lane] = s.hdg;
   L.tas[lane] = s.tas; L.vs[lane] = s.vs;
-  // StateBased: u = gs*sin(trk), v = gs*cos(trk)  (gs = tas, trk = hdg, no wind)
   double st, ct;
   sincos(s.hdg * kD2R, &st, &ct);
   L.u[lane] = s.tas * st;
   L.v[lane] = s.tas * ct;
+  if constexpr (LT::kWind) {
+    L.gs[lane] = s.gs;
+    double sk, ck;
+    sincos(s.trk * kD2R, &sk, &ck);
+    L.cu[lane] = s.gs * sk;
+    L.cv[lane] = s.gs * ck;
+  }
+}
+
+template <class LT>
+__device__ __forceinline__ double gs_of(const LT& L, int i) {
+  if constexpr (LT::kWind) return L.gs[i];
+  else return L.tas[i];
+}
+
+// StateBased velocity components u = gs*sin(trk), v = gs*cos(trk)
+template <class LT>
+__device__ __forceinline__ double cd_u(const LT& L, int i) {
+  if constexpr (LT::kWind) return L.cu[i];
+  else return L.u[i];
+}
+template <class LT>
+__device__ __forceinline__ double cd_v(const LT& L, int i) {
+  if constexpr (LT::kWind) return L.cv[i];
+  else return L.v[i];
 }
 
 // ---- StateBased.detect (oracle: statebased_detect), wave-compacted -------------------
@@ -277,7 +432,8 @@ struct CdOut {
 };
 
 // exact StateBased terms of pair (i, k) (i != k), oracle operation order
-__device__ __forceinline__ CdOut cd_pair(const Lds& L, int i, int k) {
+template <class LT>
+__device__ __forceinline__ CdOut cd_pair(const LT& L, int i, int k) {
   CdOut r{false, false, 0.0, 0.0, false};
   const double lati = L.lat[i], loni = L.lon[i];
   const double latk = L.lat[k], lonk = L.lon[k];
@@ -286,8 +442,8 @@ __device__ __forceinline__ CdOut cd_pair(const Lds& L, int i, int k) {
   const double cavelat = cos(((lati + latk) * kD2R) * 0.5);
   const double dangle = sqrt(dlat * dlat + (dlon * dlon) * (cavelat * cavelat));
   const double dist = (6371000.0 * dangle / NM) * NM + 0.0;     // + 1e9*I, I = 0
-  const double du = L.u[k] - L.u[i];
-  const double dv = L.v[k] - L.v[i];
+  const double du = cd_u(L, k) - cd_u(L, i);
+  const double dv = cd_v(L, k) - cd_v(L, i);
   double dv2 = du * du + dv * dv;
   dv2 = fabs(dv2) < 1e-6 ? 1e-6 : dv2;
   const double vrel = sqrt(dv2);
@@ -531,8 +687,8 @@ __device__ __forceinline__ void reset_scalars(EnvScalars& v, const double aux[2]
 // Per-lane observation terms of aircraft j (j >= 1) relative to the ownship (LDS).
 // o[0..6] per kind (see the writers below); returns the intrusion predicate.
 // ---------------------------------------------------------------------------------------
-template <int KIND>
-__device__ __forceinline__ bool lane_obs(const Lds& L, int base, int lane, double o[7],
+template <int KIND, class LT>
+__device__ __forceinline__ bool lane_obs(const LT& L, int base, int lane, double o[7],
                                          double* sortkey) {
   const double lat0 = L.lat[base], lon0 = L.lon[base], hdg0 = L.hdg[base];
   const double latj = L.lat[lane], lonj = L.lon[lane];
@@ -560,8 +716,8 @@ __device__ __forceinline__ bool lane_obs(const Lds& L, int base, int lane, doubl
     return dist < 4;                                       // _check_intrusion :280-281
   } else {
     // vertical_cr_env.py:133-156 / horizontal_cr_env.py:172-188 (gs == tas: no wind)
-    const double alt0 = L.alt[base], vs0 = L.vs[base], gs0 = L.tas[base];
-    const double altj = L.alt[lane], tasj = L.tas[lane];
+    const double alt0 = L.alt[base], vs0 = L.vs[base], gs0 = gs_of(L, base);
+    const double altj = L.alt[lane], tasj = gs_of(L, lane);
     const double bearing = bound180(hdg0 - qdr);
     const double hd = hdg0 - L.hdg[lane];
     double sbr, cbr, shd, chd;
@@ -580,10 +736,14 @@ __device__ __forceinline__ bool lane_obs(const Lds& L, int base, int lane, doubl
   }
 }
 
+// ws = 2 shifts every key sorted after "wind_v" (offset >= wpos) when the obs carries the
+// wind keys (wrappers/wind.py augment_obs)
 template <int KIND>
 __device__ __forceinline__ void write_lane_obs(float* obs, float* fobs, float* lrn, int K, int N,
-                                               int j, int rank, const double o[7]) {
+                                               int j, int rank, const double o[7], int wpos,
+                                               int ws) {
   auto put = [&](int off, double v) {
+    off += off >= wpos ? ws : 0;
     const float f = (float)v;
     obs[off] = f;
     if (fobs) fobs[off] = f;
@@ -620,10 +780,20 @@ __device__ __forceinline__ void write_lane_obs(float* obs, float* fobs, float* l
 
 // Ownship scalar obs (lane j == 0).  Merge: merge_env.py:175-191 with the pre-reward
 // wpt_reach; Vertical/Descent: vertical_cr_env.py:129-164 / descent_env.py:100-108.
-template <int KIND>
-__device__ __forceinline__ void own_obs(const KParams& p, const Lds& L, int lane, const EnvScalars& ev,
-                                        double sc[5], double* wdist, double* drift, double* rwd) {
+template <int KIND, class LT>
+__device__ __forceinline__ void own_obs(const KParams& p, const LT& L, int lane, const EnvScalars& ev,
+                                        double sc[7], double* wdist, double* drift, double* rwd) {
   const double lat = L.lat[lane], lon = L.lon[lane];
+  if constexpr (LT::kWind) {
+    // wrappers/wind.py:56-66 (_get_wind_observation) -> sc[5], sc[6]
+    if (p.wind.augment) {
+      double wn, we, sh, ch;
+      wind_at(p.wind, lat, lon, L.alt[lane], &wn, &we);
+      sincos(L.hdg[lane] * kD2R, &sh, &ch);
+      sc[5] = (wn * ch + we * sh) / 50;
+      sc[6] = (-wn * sh + we * ch) / 50;
+    }
+  }
   if constexpr (KIND == BSG_ENV_MERGE) {
     const int w = ev.wpt_reach == 0 ? 0 : 1;
     double wqdr;
@@ -651,13 +821,15 @@ __device__ __forceinline__ void own_obs(const KParams& p, const Lds& L, int lane
 
 template <int KIND>
 __device__ __forceinline__ void write_own_obs(float* obs, float* fobs, float* lrn, int K, int N,
-                                              const double sc[5]) {
-  auto put = [&](int off, double v) {
+                                              const double sc[7], int wpos, int ws) {
+  auto raw = [&](int off, double v) {
     const float f = (float)v;
     obs[off] = f;
     if (fobs) fobs[off] = f;
     if (lrn) lrn[off] = f;
   };
+  auto put = [&](int off, double v) { raw(off + (off >= wpos ? ws : 0), v); };
+  if (ws) { raw(wpos, sc[5]); raw(wpos + 1, sc[6]); }      // wind_u, wind_v
   if constexpr (KIND == BSG_ENV_MERGE) {
     put(0, sc[0]);                          // airspeed
     put(1, sc[1]);                          // cos(drift)
@@ -680,7 +852,8 @@ __device__ __forceinline__ void write_own_obs(float* obs, float* fobs, float* lr
   }
 }
 
-__device__ __forceinline__ int rank_in_group(const Lds& L, int base, int lane, int j, int N) {
+template <class LT>
+__device__ __forceinline__ int rank_in_group(const LT& L, int base, int lane, int j, int N) {
   const double dj = L.d[lane];
   int r = 0;
   for (int k = 1; k < N; ++k) {
@@ -705,14 +878,15 @@ __device__ __forceinline__ unsigned long long stamp_clock() {
 #define BSG_STAMP(slot, val) do { } while (0)
 #endif
 
-template <int KIND, int GS>
+template <int KIND, int GS, bool WIND>
 __global__ __launch_bounds__(64) void step_kernel(KParams p) {
 #if defined(BSG_STAMPS) && BSG_STAMPS
   BSG_STAMP(0, __builtin_amdgcn_s_memrealtime());
   BSG_STAMP(1, stamp_clock());
 #endif
-  __shared__ Lds L;
+  __shared__ Lds<WIND> L;
   const int lane = threadIdx.x;
+  const int ws = (WIND && p.wind.augment) ? 2 : 0;   // obs carries wind_u / wind_v
   const int g = lane / GS;
   const int j = lane % GS;
   const int base = g * GS;
@@ -743,7 +917,7 @@ __global__ __launch_bounds__(64) void step_kernel(KParams p) {
       if (resetting) {
         spawn<KIND>(p, e, j, ev.episode, s, aux);
       } else {
-        load_ac(b, a, s);
+        load_ac<WIND>(b, a, s);
       }
       if (stepping) {
         if (j == 0) {
@@ -753,12 +927,12 @@ __global__ __launch_bounds__(64) void step_kernel(KParams p) {
             const double dv = p.actions[(size_t)e * 2 + 1] * 20;
             const double heading_new = bound180(s.hdg + dh);
             const double speed_new = (s.cas + dv) * 1.94384;
-            s.ap_trk = heading_new;
+            s.ap_trk = hdg_command_track<WIND>(p.wind, s, heading_new);
             s.nav &= ~1;
             s.selspd = speed_new >= 1.0 ? speed_new * KTS : speed_new;
           } else if constexpr (KIND == BSG_ENV_HORIZONTAL_CR) {
             // horizontal_cr_env.py:272-275: HDG KL001 {hdg + a*45} (no wrap)
-            s.ap_trk = s.hdg + p.actions[e] * 45;
+            s.ap_trk = hdg_command_track<WIND>(p.wind, s, s.hdg + p.actions[e] * 45);
             s.nav &= ~1;
           } else {
             // vertical_cr_env.py:242-256 / descent_env.py:146-160
@@ -774,13 +948,13 @@ __global__ __launch_bounds__(64) void step_kernel(KParams p) {
           RouteRegs rt;
           rt.load(p.route);
           const double dt = p.cfg.simdt;
-          for (int it = 0; it < S; ++it) substep(s, m, dt, rt);
+          for (int it = 0; it < S; ++it) substep<WIND>(s, m, dt, rt, p.wind);
           // update_airspeed's cas = vtas2cas(tas, alt) of the LAST substep (its alt is the
           // one before that substep's update_pos, i.e. m.at's key)
           s.cas = tas2cas_at(s.tas, m.at);
         }
       }
-      if (active) store_ac(b, a, s);
+      if (active) store_ac<WIND>(b, a, s);
     }
     if (resetting && j == 0) reset_scalars<KIND>(ev, aux);
     stage(L, lane, s);
@@ -821,11 +995,11 @@ __global__ __launch_bounds__(64) void step_kernel(KParams p) {
     // phase 1: candidate pairs of row j (no transcendentals)
     uint64_t cand = 0;
     if (ok) {
-      const double lati = L.lat[lane], ui = L.u[lane], vi = L.v[lane];
+      const double lati = L.lat[lane], ui = cd_u(L, lane), vi = cd_v(L, lane);
       for (int k = 0; k < N; ++k) {
         const int lk = base + k;
         const double dlat = (L.lat[lk] - lati) * kD2R;
-        const double du = L.u[lk] - ui, dv = L.v[lk] - vi;
+        const double du = cd_u(L, lk) - ui, dv = cd_v(L, lk) - vi;
         double dv2 = du * du + dv * dv;
         dv2 = fabs(dv2) < 1e-6 ? 1e-6 : dv2;
         if (k != j && cd_candidate(dlat, dv2)) cand |= 1ull << k;
@@ -869,7 +1043,7 @@ __global__ __launch_bounds__(64) void step_kernel(KParams p) {
   }
 
   // lane 0: scalar obs, reward, termination (per env)
-  double sc[5] = {0, 0, 0, 0, 0};
+  double sc[7] = {0, 0, 0, 0, 0, 0, 0};
   float reward = 0.0f;
   bool term = false, trunc = false, done = false;
   if (ok && j == 0) {
@@ -928,7 +1102,7 @@ __global__ __launch_bounds__(64) void step_kernel(KParams p) {
     float* fobs = same_step_reset ? b.final_obs + (size_t)e * O : nullptr;
     float* lrn = (b.learner && !same_step_reset) ? b.learner + (size_t)e * (O + 3) : nullptr;
     if (j == 0) {
-      write_own_obs<KIND>(obs, fobs, lrn, K, N, sc);
+      write_own_obs<KIND>(obs, fobs, lrn, K, N, sc, p.wpos, ws);
       b.reward[e] = reward;
       b.terminated[e] = term ? 1 : 0;
       b.truncated[e] = trunc ? 1 : 0;
@@ -955,7 +1129,7 @@ __global__ __launch_bounds__(64) void step_kernel(KParams p) {
         }
       }
     } else {
-      write_lane_obs<KIND>(obs, fobs, lrn, K, N, j, rank, o);
+      write_lane_obs<KIND>(obs, fobs, lrn, K, N, j, rank, o, p.wpos, ws);
       if constexpr (KIND == BSG_ENV_MERGE) {
         if (rank < K) b.topk[(size_t)e * K + rank] = j;
       }
@@ -976,7 +1150,7 @@ __global__ __launch_bounds__(64) void step_kernel(KParams p) {
       double aux[2] = {ev.target_alt, 0.0};
       if (same_step_reset && ok) {
         spawn<KIND>(p, e, j, ev.episode, s, aux);
-        store_ac(b, a, s);
+        store_ac<WIND>(b, a, s);
       }
       if (same_step_reset && j == 0) reset_scalars<KIND>(ev, aux);
       if (same_step_reset) stage(L, lane, s);
@@ -994,11 +1168,11 @@ __global__ __launch_bounds__(64) void step_kernel(KParams p) {
       if (j == 0) {
         double wdist, drift, rwd;
         own_obs<KIND>(p, L, lane, ev, sc, &wdist, &drift, &rwd);
-        write_own_obs<KIND>(obs, nullptr, lrn, K, N, sc);
+        write_own_obs<KIND>(obs, nullptr, lrn, K, N, sc, p.wpos, ws);
       } else {
         int r = 0x7fffffff;
         if constexpr (KIND == BSG_ENV_MERGE) r = rank_in_group(L, base, lane, j, N);
-        write_lane_obs<KIND>(obs, nullptr, lrn, K, N, j, r, o);
+        write_lane_obs<KIND>(obs, nullptr, lrn, K, N, j, r, o, p.wpos, ws);
       }
     }
   }
@@ -1012,20 +1186,25 @@ __global__ __launch_bounds__(64) void step_kernel(KParams p) {
 }
 
 // ---------------------------------------------------------------------------------------
-template <int KIND>
-static hipError_t launch_kind(const KParams& p, hipStream_t st) {
+template <int KIND, bool WIND>
+static hipError_t launch_kind_w(const KParams& p, hipStream_t st) {
   int gs = 1;
   while (gs < p.N) gs <<= 1;
   const int epb = 64 / gs;
   const int grid = (p.E + epb - 1) / epb;
   switch (gs) {
 #define BSG_CASE(G) \
-    case G: hipLaunchKernelGGL((step_kernel<KIND, G>), dim3(grid), dim3(64), p.lds_pad, st, p); break;
+    case G: hipLaunchKernelGGL((step_kernel<KIND, G, WIND>), dim3(grid), dim3(64), p.lds_pad, st, p); break;
     BSG_CASE(1) BSG_CASE(2) BSG_CASE(4) BSG_CASE(8) BSG_CASE(16) BSG_CASE(32) BSG_CASE(64)
 #undef BSG_CASE
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
+}
+
+template <int KIND>
+static hipError_t launch_kind(const KParams& p, hipStream_t st) {
+  return p.wind.np > 0 ? launch_kind_w<KIND, true>(p, st) : launch_kind_w<KIND, false>(p, st);
 }
 
 hipError_t launch_step(const KParams& p, hipStream_t st) {

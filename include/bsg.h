@@ -27,9 +27,10 @@
 extern "C" {
 #endif
 
-#define BSG_ABI_VERSION 1
+#define BSG_ABI_VERSION 2
 #define BSG_MAX_AC 64          /* aircraft per env (one wavefront) */
 #define BSG_MAX_ROUTE 4
+#define BSG_WIND_NALT 451      /* wind profile levels: 0..45000 ft every 100 ft */
 
 enum {
   BSG_OK = 0,
@@ -78,6 +79,9 @@ typedef struct bsg_buffers {
   double *lat, *lon, *alt, *hdg, *tas, *cas, *vs, *ax;
   double *ap_trk, *selspd, *selalt, *selvs;   /* autopilot targets */
   int32_t *nav;                               /* bit0 swlnav, bits 8..15 active waypoint */
+  double *gs, *trk;          /* ground speed / track (bs.traf.gs, .trk); required only while
+                                a wind field is set (bsg_set_wind) -- without wind gs = tas
+                                and trk = hdg, and these may be NULL */
   /* ---- per-env state [E] ----------------------------------------------------------- */
   int32_t *step_count;       /* TimeLimit elapsed steps */
   int32_t *flags;            /* bit0: reset pending (NEXT_STEP autoreset) */
@@ -112,6 +116,22 @@ typedef struct bsg_buffers {
                                 the multi-GPU path all-gathers over RCCL (NULL = off) */
 } bsg_buffers;
 
+/* Wind field (bluesky_gym/wrappers/wind.py:8-24 -> bs.traf.wind.addpointvne): P points with
+ * wind components constant in altitude (num_levels = 1) or sampled on the fixed altitude
+ * axis (num_levels = BSG_WIND_NALT, level l at l*100 ft).  Interpolation: inverse distance
+ * squared over the points (one point and one level: constant everywhere), linear between
+ * altitude levels (docs/BLUESKY_SUBSET_SPEC.md §A.7).  All pointers are device pointers
+ * owned by the caller; vnorth/veast are [num_levels][P] (m/s). */
+typedef struct bsg_wind {
+  int32_t num_points;        /* P >= 1; 0 turns the wind off */
+  int32_t num_levels;        /* 1 or BSG_WIND_NALT */
+  int32_t augment_obs;       /* 1: obs rows carry wind_u, wind_v (wind.py:18-24, 56-66) at
+                                their sorted-key position; obs_dim grows by 2 */
+  int32_t reserved;
+  const double *lat, *lon;   /* [P] deg */
+  const double *vnorth, *veast;
+} bsg_wind;
+
 typedef struct bsg_ctx bsg_ctx;
 
 /* ABI version of the loaded library. */
@@ -123,7 +143,7 @@ const char* bsg_last_error(void);
 /* Flat observation length for an env kind (sum of the Box sizes of the reference
  * observation_space: merge_env.py:59-74 -> 5+7K; vertical_cr_env.py:67-83 -> 4+7(N-1);
  * descent_env.py:53-60 -> 4; horizontal_cr_env.py:49-60 -> 3+5(N-1)). Negative on
- * invalid input. */
+ * invalid input.  A wind field with augment_obs adds 2 (bsg_ctx_obs_dim). */
 int32_t bsg_obs_dim(int32_t env_kind, int32_t num_ac, int32_t num_ac_state);
 
 /* Action width (merge_env.py:76 -> 2; vertical_cr_env.py:85 / descent_env.py:62 /
@@ -158,6 +178,15 @@ int32_t bsg_reset(bsg_ctx* ctx, const uint8_t* env_mask, const double* spawn, vo
  * descent_env.py:184-206).  actions: device f64 [E, action_dim].  spawn: optional
  * device f64 [E, spawn_width] used by autoresets in this step (NULL = Philox). */
 int32_t bsg_step(bsg_ctx* ctx, const double* actions, const double* spawn, void* stream);
+
+/* Replaces: WindFieldWrapper(env, lat, lon, vnorth, veast, alt, augment_obs)
+ * (wind.py:8-24, addpointvne at :28): sets (or, with NULL / num_points 0, clears) the wind
+ * field applied to every env of the batch from the next launch on.  Unbinds the ctx:
+ * call bsg_bind again (gs/trk become required; obs rows may widen). */
+int32_t bsg_set_wind(bsg_ctx* ctx, const bsg_wind* wind);
+
+/* Observation row length of this ctx (bsg_obs_dim + 2 with an augmenting wind field). */
+int32_t bsg_ctx_obs_dim(const bsg_ctx* ctx);
 
 /* Kernel-time instrumentation: record a HIP event pair around each step launch on the
  * launch stream; bsg_last_step_ms() returns the elapsed time of the most recent

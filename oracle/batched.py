@@ -137,6 +137,24 @@ class _Base:
         self.total_reward = np.zeros(self.E, np.float64)
         self.total_intrusions = np.zeros(self.E, np.int32)
         self.env_ids = np.arange(self.E)     # global env ids (Philox counter word 0)
+        self.wind = None                     # bsx.WindField (wrappers/wind.py) or None
+        self.wind_augment = False
+
+    def set_wind(self, field, augment_obs=False):
+        """WindFieldWrapper (bluesky_gym/wrappers/wind.py:8-24): a wind field applied to
+        every env; augment_obs adds the wind_u / wind_v observation keys."""
+        if self.wind_augment != bool(augment_obs):
+            self.obs_dim += 2 if augment_obs else -2
+        self.wind = field
+        self.wind_augment = bool(augment_obs)
+
+    def _flat(self, obs, keys):
+        if self.wind_augment:
+            wu, wv = bsx.wind_obs(self.st, self.wind)
+            obs["wind_u"] = wu[:, None]
+            obs["wind_v"] = wv[:, None]
+            keys = tuple(sorted(tuple(keys) + ("wind_u", "wind_v")))
+        return flatten_obs(obs, keys)
 
     # -------- spawn parameters (host-supplied = parity mode; None = device Philox) -----
     def device_spawn_params(self, env_ids, episodes):
@@ -163,7 +181,7 @@ class _Base:
     def _substeps(self):
         for _ in range(self.S):
             bsx.traffic_update(self.st, self.dt, self.route_lat, self.route_lon,
-                               self.route_next_qdr)
+                               self.route_next_qdr, self.wind)
 
     def step(self, actions, spawn=None):
         """Vector step.  Returns dict: obs (flat f64), reward, terminated, truncated,
@@ -276,7 +294,7 @@ class MergeOracle(_Base):
         dv = actions[:, 1] * MERGE_D_SPEED
         heading_new = bsx.bound_angle_positive_negative_180(st.hdg[:, 0] + dh)
         speed_new = (st.cas[:, 0] + dv) * MPS2KT
-        st.ap_trk[:, 0] = heading_new
+        st.ap_trk[:, 0] = bsx.selhdg_track(st, (slice(None), 0), heading_new, self.wind)
         st.swlnav[:, 0] = False
         st.selspd[:, 0] = np.where(speed_new >= 1.0, speed_new * bsx.kts, speed_new)
 
@@ -324,7 +342,7 @@ class MergeOracle(_Base):
 
     def observe(self):
         obs, *_ = self._obs_core()
-        return {"obs": flatten_obs(obs, MERGE_OBS_KEYS), "obs_dict": obs}
+        return {"obs": self._flat(obs, MERGE_OBS_KEYS), "obs_dict": obs}
 
     def _observe_and_reward(self):
         obs, drift, wpt_dist, dist, topk = self._obs_core()
@@ -348,12 +366,12 @@ class MergeOracle(_Base):
         intr_mask = np.zeros(self.E, np.uint64)
         for i in range(self.N - 1):
             intr_mask |= intr[:, i].astype(np.uint64) << np.uint64(i + 1)
-        res = dict(obs=flatten_obs(obs, MERGE_OBS_KEYS), obs_dict=obs, reward=reward,
+        res = dict(obs=self._flat(obs, MERGE_OBS_KEYS), obs_dict=obs, reward=reward,
                    terminated=done, topk=topk, intr_mask=intr_mask, nintr=nintr,
                    _new_wr=new_wr, _new_faf=new_faf, _d=d)
         if self.compute_cd:
-            cd = bsx.statebased_detect(self.st.lat, self.st.lon, self.st.alt, self.st.hdg,
-                                       self.st.tas, self.st.vs)
+            cd = bsx.statebased_detect(self.st.lat, self.st.lon, self.st.alt, self.st.trk,
+                                       self.st.gs, self.st.vs)
             res["conf_mask"] = _rows_to_u64(cd["swconfl"])
             res["los_mask"] = _rows_to_u64(cd["swlos"])
             res["tcpamax"] = cd["tcpamax"]
@@ -505,7 +523,7 @@ class VerticalOracle(_VertBase):
 
     def observe(self):
         obs, *_ = self._obs_core()
-        return {"obs": flatten_obs(obs, VERTICAL_OBS_KEYS), "obs_dict": obs}
+        return {"obs": self._flat(obs, VERTICAL_OBS_KEYS), "obs_dict": obs}
 
     def _observe_and_reward(self):
         obs, altitude, runway_distance, int_dis = self._obs_core()
@@ -519,10 +537,10 @@ class VerticalOracle(_VertBase):
         intr_mask = np.zeros(self.E, np.uint64)
         for i in range(self.NI):
             intr_mask |= intr[:, i].astype(np.uint64) << np.uint64(i + 1)
-        res = dict(obs=flatten_obs(obs, VERTICAL_OBS_KEYS), obs_dict=obs, reward=reward,
+        res = dict(obs=self._flat(obs, VERTICAL_OBS_KEYS), obs_dict=obs, reward=reward,
                    terminated=done, intr_mask=intr_mask, nintr=nintr, _fin=fin)
         if self.compute_cd:
-            cd = bsx.statebased_detect(st.lat, st.lon, st.alt, st.hdg, st.tas, st.vs)
+            cd = bsx.statebased_detect(st.lat, st.lon, st.alt, st.trk, st.gs, st.vs)
             res["conf_mask"] = _rows_to_u64(cd["swconfl"])
             res["los_mask"] = _rows_to_u64(cd["swlos"])
             res["tcpamax"] = cd["tcpamax"]
@@ -601,12 +619,12 @@ class DescentOracle(_VertBase):
 
     def observe(self):
         obs, *_ = self._obs_core()
-        return {"obs": flatten_obs(obs, DESCENT_OBS_KEYS), "obs_dict": obs}
+        return {"obs": self._flat(obs, DESCENT_OBS_KEYS), "obs_dict": obs}
 
     def _observe_and_reward(self):
         obs, altitude, runway_distance = self._obs_core()
         alt_pen, done, fin = self._alt_reward(altitude, runway_distance)
-        return dict(obs=flatten_obs(obs, DESCENT_OBS_KEYS), obs_dict=obs, reward=alt_pen,
+        return dict(obs=self._flat(obs, DESCENT_OBS_KEYS), obs_dict=obs, reward=alt_pen,
                     terminated=done, _fin=fin)
 
     def _commit(self, res, live):
@@ -620,7 +638,7 @@ class DescentOracle(_VertBase):
 
 def _cd_fill(o, res, mask):
     st = o.st
-    cd = bsx.statebased_detect(st.lat, st.lon, st.alt, st.hdg, st.tas, st.vs)
+    cd = bsx.statebased_detect(st.lat, st.lon, st.alt, st.trk, st.gs, st.vs)
     res["conf_mask"] = np.where(mask[:, None], _rows_to_u64(cd["swconfl"]), res["conf_mask"])
     res["los_mask"] = np.where(mask[:, None], _rows_to_u64(cd["swlos"]), res["los_mask"])
     res["tcpamax"] = np.where(mask[:, None], cd["tcpamax"], res["tcpamax"])
@@ -691,7 +709,8 @@ class HorizontalOracle(_Base):
     def _apply_action(self, actions):
         """horizontal_cr_env.py:272-275: HDG = hdg + a*45 (no wrap), LNAV off."""
         st = self.st
-        st.ap_trk[:, 0] = st.hdg[:, 0] + actions[:, 0] * H_D_HEADING
+        st.ap_trk[:, 0] = bsx.selhdg_track(st, (slice(None), 0),
+                                           st.hdg[:, 0] + actions[:, 0] * H_D_HEADING, self.wind)
         st.swlnav[:, 0] = False
 
     def _obs_core(self):
@@ -719,7 +738,7 @@ class HorizontalOracle(_Base):
 
     def observe(self):
         obs, *_ = self._obs_core()
-        return {"obs": flatten_obs(obs, HORIZONTAL_OBS_KEYS), "obs_dict": obs}
+        return {"obs": self._flat(obs, HORIZONTAL_OBS_KEYS), "obs_dict": obs}
 
     def _observe_and_reward(self):
         obs, int_dis, wpt_km, drift = self._obs_core()
@@ -733,11 +752,11 @@ class HorizontalOracle(_Base):
         intr_mask = np.zeros(self.E, np.uint64)
         for i in range(self.NI):
             intr_mask |= intr[:, i].astype(np.uint64) << np.uint64(i + 1)
-        res = dict(obs=flatten_obs(obs, HORIZONTAL_OBS_KEYS), obs_dict=obs, reward=reward,
+        res = dict(obs=self._flat(obs, HORIZONTAL_OBS_KEYS), obs_dict=obs, reward=reward,
                    terminated=new_wr == 1, intr_mask=intr_mask, nintr=nintr, _new_wr=new_wr, _d=d)
         if self.compute_cd:
             st = self.st
-            cd = bsx.statebased_detect(st.lat, st.lon, st.alt, st.hdg, st.tas, st.vs)
+            cd = bsx.statebased_detect(st.lat, st.lon, st.alt, st.trk, st.gs, st.vs)
             res["conf_mask"] = _rows_to_u64(cd["swconfl"])
             res["los_mask"] = _rows_to_u64(cd["swlos"])
             res["tcpamax"] = cd["tcpamax"]

@@ -19,6 +19,9 @@ published algorithm of the subset those call sites use (fr
                               selalt/selvs), OpenAP-style perf limits, update_airspeed,
                               update_groundspeed (no wind), update_pos
 * ``bluesky.traffic.asas.statebased`` -- StateBased.detect (all-pairs CPA)
+* ``bluesky.traffic.windfield``        -- WindField.addpointvne / getdata, and the wind
+                              branches of ActivePilot (heading for a commanded track),
+                              update_groundspeed and the HDG command (wind path, §8(f) 3)
 * ``Traffic.cre`` / ``Traffic.creconfs`` (spawn)
 
 Parity status: the SIM layer is "parity unpinned" (no upstream source or fixture is
@@ -298,12 +301,141 @@ def perf_limits(intent_tas, intent_vs, intent_h, ax):
     return allow_tas, allow_vs, allow_h
 
 
-def traffic_update(st, dt, route_lat, route_lon, route_next_qdr):
-    """One simulation substep (Traffic.update with wind off, ASAS resolution off).
+# --------------------------------------------------------------------------------------
+# Wind field (bluesky.traffic.windfield.Windfield; used by bluesky_gym/wrappers/wind.py:26)
+# Frozen definition (docs/BLUESKY_SUBSET_SPEC.md §A.7): profiles live on a fixed altitude
+# axis 0..45000 ft in 100 ft steps; horizontal interpolation is inverse-distance-squared
+# weighting, summed in point order.
+# --------------------------------------------------------------------------------------
+WIND_ALTSTEP = 100.0 * ft
+WIND_ALTMAX = 45000.0 * ft
+WIND_NALT = 451
+WIND_ALTAXIS = np.arange(WIND_NALT, dtype=np.float64) * WIND_ALTSTEP
+
+
+class WindField:
+    def __init__(self):
+        self.clear()
+
+    def clear(self):
+        self.lat = np.zeros(0)
+        self.lon = np.zeros(0)
+        self.vnorth = np.zeros((1, 0))      # [levels][P]; levels = 1 (2-D) or WIND_NALT
+        self.veast = np.zeros((1, 0))
+        self.winddim = 0
+
+    def addpointvne(self, lat, lon, vnorth, veast, windalt=None):
+        """Add P points.  vnorth/veast: [P] or [1, P] (constant in altitude) or
+        [len(windalt), P] profiles over windalt (interpolated onto the fixed axis)."""
+        lat = np.atleast_1d(np.asarray(lat, np.float64)).ravel()
+        lon = np.atleast_1d(np.asarray(lon, np.float64)).ravel()
+        P = lat.size
+        vn = np.asarray(vnorth, np.float64)
+        ve = np.asarray(veast, np.float64)
+        if windalt is None:
+            vn = vn.reshape(-1)[-P:].reshape(1, P) if vn.size != P else vn.reshape(1, P)
+            ve = ve.reshape(-1)[-P:].reshape(1, P) if ve.size != P else ve.reshape(1, P)
+            prof3d = False
+        else:
+            wa = np.atleast_1d(np.asarray(windalt, np.float64))
+            vn = vn.reshape(len(wa), P)
+            ve = ve.reshape(len(wa), P)
+            vn = np.stack([np.interp(WIND_ALTAXIS, wa, vn[:, p]) for p in range(P)], 1)
+            ve = np.stack([np.interp(WIND_ALTAXIS, wa, ve[:, p]) for p in range(P)], 1)
+            prof3d = True
+        if self.winddim == 3 or prof3d:
+            # bring every table to the full axis
+            def full(t):
+                return t if t.shape[0] == WIND_NALT else np.repeat(t[:1], WIND_NALT, 0)
+            self.vnorth = np.concatenate([full(self.vnorth), full(vn)], 1)
+            self.veast = np.concatenate([full(self.veast), full(ve)], 1)
+        else:
+            self.vnorth = np.concatenate([self.vnorth, vn], 1)
+            self.veast = np.concatenate([self.veast, ve], 1)
+        self.lat = np.concatenate([self.lat, lat])
+        self.lon = np.concatenate([self.lon, lon])
+        self.winddim = 3 if (prof3d or self.winddim == 3) else min(2, self.lat.size)
+        return self.lat.size - 1
+
+    def getdata(self, lat, lon, alt):
+        lat = np.asarray(lat, np.float64)
+        lon = np.asarray(lon, np.float64)
+        alt = np.asarray(alt, np.float64)
+        shape = np.broadcast(lat, lon, alt).shape
+        if self.winddim == 0:
+            return np.zeros(shape), np.zeros(shape)
+        if self.winddim == 1:
+            return np.full(shape, self.vnorth[0, 0]), np.full(shape, self.veast[0, 0])
+        P = self.lat.size
+        w = []
+        S = np.zeros(shape)
+        for p in range(P):
+            cavelat = np.cos(np.radians(0.5 * (lat + self.lat[p])))
+            dy = np.radians(lat - self.lat[p])
+            dx = cavelat * np.radians(lon - self.lon[p])
+            wp = 1.0 / (1e-16 + dx * dx + dy * dy)
+            w.append(wp)
+            S = S + wp
+        if self.winddim == 3:
+            idx = np.minimum(np.maximum(alt, 0.0), WIND_ALTMAX) / WIND_ALTSTEP
+            ialt = np.minimum(np.floor(idx).astype(np.int64), WIND_NALT - 2)
+            falt = idx - ialt
+        vn = np.zeros(shape)
+        ve = np.zeros(shape)
+        for p in range(P):
+            h = w[p] / S
+            if self.winddim == 3:
+                cn = (1.0 - falt) * self.vnorth[ialt, p] + falt * self.vnorth[ialt + 1, p]
+                ce = (1.0 - falt) * self.veast[ialt, p] + falt * self.veast[ialt + 1, p]
+            else:
+                cn, ce = self.vnorth[0, p], self.veast[0, p]
+            vn = vn + cn * h
+            ve = ve + ce * h
+        return vn, ve
+
+    def table(self):
+        """(lat[P], lon[P], vnorth[levels][P], veast[levels][P]) for the device."""
+        return self.lat.copy(), self.lon.copy(), self.vnorth.copy(), self.veast.copy()
+
+
+def wind_active(wind):
+    return wind is not None and wind.winddim > 0
+
+
+def selhdg_track(st, idx, hdg, wind):
+    """Autopilot.selhdgcmd: the commanded heading becomes a track through the wind
+    triangle at the current position when airborne (alt > 50 ft)."""
+    hdg = np.asarray(hdg, np.float64)
+    if not wind_active(wind):
+        return hdg
+    alt, tas = st.alt[idx], st.tas[idx]
+    vn, ve = wind.getdata(st.lat[idx], st.lon[idx], alt)
+    tasnorth = tas * np.cos(np.radians(hdg))
+    taseast = tas * np.sin(np.radians(hdg))
+    trk = np.degrees(np.arctan2(taseast + ve, tasnorth + vn)) % 360.0
+    return np.where(alt > 50.0 * ft, trk, hdg)
+
+
+def wind_obs(st, wind, max_wind=50.0):
+    """bluesky_gym/wrappers/wind.py:56-66 (_get_wind_observation), ownship = index 0."""
+    lat, lon, alt = st.lat[..., 0], st.lon[..., 0], st.alt[..., 0]
+    wn, we = wind.getdata(lat, lon, alt)
+    hdg = np.deg2rad(st.hdg[..., 0])
+    wind_u = (wn * np.cos(hdg) + we * np.sin(hdg)) / max_wind
+    wind_v = (-wn * np.sin(hdg) + we * np.cos(hdg)) / max_wind
+    return wind_u, wind_v
+
+
+def traffic_update(st, dt, route_lat, route_lon, route_next_qdr, wind=None):
+    """One simulation substep (Traffic.update, ASAS resolution off).
 
     route_lat/route_lon: 1-D arrays of the shared route's waypoints (may be empty).
     route_next_qdr[k]: bearing from waypoint k to waypoint k+1 (-999 for the last).
+    wind: WindField or None.
     """
+    windy = wind_active(wind)
+    if windy:
+        vwn, vwe = wind.getdata(st.lat, st.lon, st.alt)
     nwp = len(route_lat)
     # ---- autopilot (Autopilot.update) --------------------------------------------
     if nwp > 0:
@@ -338,7 +470,16 @@ def traffic_update(st, dt, route_lat, route_lon, route_next_qdr):
     # ---- aporasas (no active resolution) ------------------------------------------
     trk_cmd = st.ap_trk
     vs_cmd = np.abs(ap_vs)
-    hdg_cmd = pymod(trk_cmd, 360.0)
+    if windy:
+        # ActivePilot: heading that flies the commanded track through the wind
+        Vw = np.sqrt(vwn * vwn + vwe * vwe)
+        winddir = np.arctan2(vwe, vwn)
+        drift = np.radians(trk_cmd) - winddir
+        steer = np.arcsin(np.minimum(1.0, np.maximum(-1.0, Vw * np.sin(drift) /
+                                                     np.maximum(0.001, st.tas))))
+        hdg_cmd = pymod(trk_cmd + np.degrees(steer), 360.0)
+    else:
+        hdg_cmd = pymod(trk_cmd, 360.0)
     # ---- performance limits ------------------------------------------------------------
     tas_cmd, vs_cmd, alt_cmd = perf_limits(ap_tas, vs_cmd, ap_alt, st.ax)
     # ---- update_airspeed ------------------------------------------------------------
@@ -359,11 +500,20 @@ def traffic_update(st, dt, route_lat, route_lon, route_next_qdr):
     az = need_az * np.sign(delta_vs) * (300 * fpm)
     st.vs = np.where(need_az, st.vs + az * dt, target_vs)
     st.vs = np.where(np.isfinite(st.vs), st.vs, 0)
-    # ---- update_groundspeed (no wind) --------------------------------------------------
-    st.gsnorth = st.tas * np.cos(np.radians(st.hdg))
-    st.gseast = st.tas * np.sin(np.radians(st.hdg))
-    st.gs = st.tas.copy()
-    st.trk = st.hdg.copy()
+    # ---- update_groundspeed ------------------------------------------------------------
+    if windy:
+        applywind = st.alt > 50.0 * ft
+        st.gsnorth = st.tas * np.cos(np.radians(st.hdg)) + vwn * applywind
+        st.gseast = st.tas * np.sin(np.radians(st.hdg)) + vwe * applywind
+        st.gs = np.where(applywind, np.sqrt(st.gsnorth * st.gsnorth + st.gseast * st.gseast),
+                         st.tas)
+        st.trk = np.where(applywind, pymod(np.degrees(np.arctan2(st.gseast, st.gsnorth)), 360.0),
+                          st.hdg)
+    else:
+        st.gsnorth = st.tas * np.cos(np.radians(st.hdg))
+        st.gseast = st.tas * np.sin(np.radians(st.hdg))
+        st.gs = st.tas.copy()
+        st.trk = st.hdg.copy()
     # ---- update_pos -------------------------------------------------------------------
     st.alt = np.where(swaltsel, np.round(st.alt + st.vs * dt, 6), alt_cmd)
     st.lat = st.lat + np.degrees(dt * st.gsnorth / Rearth)

@@ -5,7 +5,8 @@ Used only by ``tests/golden/make_golden.py`` in the build container (where
 reference imports but that are absent offline (gymnasium, pygame, bluesky,
 stable_baselines3) and binds ``bluesky`` to a BlueSky-shaped singleton
 whose arithmetic is ``oracle.bluesky_subset``.  The reference's own env classes
-(MergeEnv, VerticalCREnv, DescentEnv) then run unmodified and their outputs become the
+(MergeEnv, VerticalCREnv, DescentEnv, HorizontalCREnv) and the WindFieldWrapper then run
+unmodified and their outputs become the
 golden vectors that pin ``oracle.batched``.
 
 Nothing here is imported by the product, and nothing here runs on the GPU box.
@@ -46,6 +47,7 @@ class Traffic:
     """Subset of bluesky.traffic.Traffic backed by an oracle TrafState of length N."""
 
     def __init__(self):
+        self.wind = bsx.WindField()
         self.reset()
         self.ap = _AP(self)
 
@@ -57,6 +59,7 @@ class Traffic:
         raise AttributeError(name)
 
     def reset(self):
+        self.wind.clear()                 # Traffic.reset clears the wind field
         self.st = bsx.TrafState((0,))
         self.id = []
         self.swvnav = np.zeros(0, bool)
@@ -139,7 +142,7 @@ class Traffic:
         else:
             rlat = rlon = np.zeros(0)
             nq = []
-        bsx.traffic_update(self.st, dt, rlat, rlon, np.array(nq))
+        bsx.traffic_update(self.st, dt, rlat, rlon, np.array(nq), self.wind)
 
 
 class Stack:
@@ -165,7 +168,7 @@ class Stack:
                 pass
             elif head == "HDG":
                 idx = traf.id2idx(w[1])
-                traf.st.ap_trk[idx] = float(w[2])
+                traf.st.ap_trk[idx] = bsx.selhdg_track(traf.st, idx, float(w[2]), traf.wind)
                 traf.st.swlnav[idx] = False
             elif head == "SPD":
                 idx = traf.id2idx(w[1])
@@ -257,6 +260,29 @@ def _gym_stub():
         def reset(self, seed=None, options=None):
             return None
     gym.Env = Env
+
+    class Wrapper:
+        def __init__(self, env):
+            self.env = env
+            self._obs_space = None
+
+        @property
+        def observation_space(self):
+            return self._obs_space if self._obs_space is not None else self.env.observation_space
+
+        @observation_space.setter
+        def observation_space(self, v):
+            self._obs_space = v
+
+        def reset(self, **kw):
+            return self.env.reset(**kw)
+
+        def step(self, action):
+            return self.env.step(action)
+
+        def __getattr__(self, name):
+            return getattr(self.__dict__["env"], name)
+    gym.Wrapper = Wrapper
     gym.spaces = spaces
     envs = types.ModuleType("gymnasium.envs")
     envs.__path__ = []
@@ -308,11 +334,16 @@ def load_reference_envs(reference_root="/root/reference"):
     envs_pkg = types.ModuleType("bluesky_gym.envs")
     envs_pkg.__path__ = [reference_root + "/bluesky_gym/envs"]
     sys.modules["bluesky_gym.envs"] = envs_pkg
+    wr_pkg = types.ModuleType("bluesky_gym.wrappers")
+    wr_pkg.__path__ = [reference_root + "/bluesky_gym/wrappers"]
+    sys.modules["bluesky_gym.wrappers"] = wr_pkg
     out = {
         "merge": importlib.import_module("bluesky_gym.envs.merge_env"),
         "vertical": importlib.import_module("bluesky_gym.envs.vertical_cr_env"),
         "descent": importlib.import_module("bluesky_gym.envs.descent_env"),
         "horizontal": importlib.import_module("bluesky_gym.envs.horizontal_cr_env"),
         "functions": importlib.import_module("bluesky_gym.envs.common.functions"),
+        "wind": importlib.import_module("bluesky_gym.wrappers.wind"),
+        "uncertainty": importlib.import_module("bluesky_gym.wrappers.uncertainty"),
     }
     return bs, out

@@ -41,12 +41,36 @@ def snap(bs):
     return np.stack([np.array(getattr(bs.traf, f), np.float64) for f in STATE_FIELDS], 0)
 
 
-def gen_merge(bs, mods, num_ac, episodes, seed, max_steps=50):
+def _wrap(mods, env, keys, wind):
+    """Optionally wrap with the reference WindFieldWrapper (bluesky_gym/wrappers/wind.py)."""
+    if wind is None:
+        return env, tuple(keys)
+    env = mods["wind"].WindFieldWrapper(env, augment_obs=True, **wind)
+    return env, tuple(sorted(tuple(keys) + ("wind_u", "wind_v")))
+
+
+def _step(env, a):
+    """env.step; for a WindFieldWrapper, its step (wind.py:43-54) inlined so that the
+    terminal step of the envs that delete their aircraft (vertical_cr_env.py:300-303,
+    descent_env.py:201-204, horizontal_cr_env.py:119-122) -- where the reference wrapper
+    raises IndexError in _get_wind_observation -- is recorded with NaN wind keys."""
+    if not hasattr(env, "_get_wind_observation"):
+        return env.step(a)
+    out = env.env.step(a)
+    try:
+        wu, wv = env._get_wind_observation()
+    except IndexError:
+        wu = wv = np.nan
+    obs = {**out[0], "wind_u": np.array([wu]), "wind_v": np.array([wv])}
+    return (obs,) + tuple(out[1:])
+
+
+def gen_merge(bs, mods, num_ac, episodes, seed, max_steps=50, wind=None):
     m = mods["merge"]
     m.NUM_AC = num_ac
     random.seed(seed)
     rng_act = np.random.default_rng(seed)
-    env = m.MergeEnv()
+    env, keys = _wrap(mods, m.MergeEnv(), ob.MERGE_OBS_KEYS, wind)
     K = m.NUM_AC_STATE
     rec = {k: [] for k in ("spawn", "obs0", "actions", "obs", "reward", "terminated",
                            "truncated", "topk", "intr", "state", "info", "length")}
@@ -58,13 +82,13 @@ def gen_merge(bs, mods, num_ac, episodes, seed, max_steps=50):
         acts = rng_act.uniform(-1, 1, (max_steps, 2))
         O, R, T, TR, TK, IN, ST, INF = [], [], [], [], [], [], [], []
         for t in range(max_steps):
-            obs, rew, term, trunc, info = env.step(acts[t])
+            obs, rew, term, trunc, info = _step(env, acts[t])
             trunc = (t + 1) >= max_steps            # gymnasium TimeLimit(50)
             lat, lon = bs.traf.lat, bs.traf.lon
             d = bs.tools.geo.kwikdist_matrix(lat[0], lon[0], lat[1:], lon[1:])
             topk = np.argsort(d)[:K] + 1
             _, di = bs.tools.geo.kwikqdrdist(lat[0], lon[0], lat[1:], lon[1:])
-            O.append(flat(obs, ob.MERGE_OBS_KEYS)); R.append(rew); T.append(int(term))
+            O.append(flat(obs, keys)); R.append(rew); T.append(int(term))
             TR.append(trunc); TK.append(topk); IN.append(di < m.INTRUSION_DISTANCE)
             ST.append(snap(bs))
             INF.append([info["total_reward"], info["faf_reach"], info["average_drift"],
@@ -74,7 +98,7 @@ def gen_merge(bs, mods, num_ac, episodes, seed, max_steps=50):
         L = len(O)
         pad = lambda a, shape, dt: np.concatenate([np.asarray(a, dt), np.zeros((max_steps - L,) + shape, dt)])
         rec["spawn"].append(spawn)
-        rec["obs0"].append(flat(obs0, ob.MERGE_OBS_KEYS))
+        rec["obs0"].append(flat(obs0, keys))
         rec["actions"].append(acts)
         rec["obs"].append(pad(O, (len(O[0]),), np.float64))
         rec["reward"].append(pad(R, (), np.float64))
@@ -92,12 +116,12 @@ def gen_merge(bs, mods, num_ac, episodes, seed, max_steps=50):
     return out
 
 
-def gen_vertical(bs, mods, num_intruders, episodes, seed, max_steps=300):
+def gen_vertical(bs, mods, num_intruders, episodes, seed, max_steps=300, wind=None):
     m = mods["vertical"]
     m.NUM_INTRUDERS = num_intruders
     np.random.seed(seed)
     rng_act = np.random.default_rng(seed)
-    env = m.VerticalCREnv()
+    env, keys = _wrap(mods, m.VerticalCREnv(), ob.VERTICAL_OBS_KEYS, wind)
     rec = {k: [] for k in ("spawn", "obs0", "actions", "obs", "reward", "terminated",
                            "truncated", "intr", "state", "info", "length")}
     for ep in range(episodes):
@@ -110,9 +134,9 @@ def gen_vertical(bs, mods, num_intruders, episodes, seed, max_steps=300):
         O, R, T, TR, IN, ST, INF = [], [], [], [], [], [], []
         for t in range(max_steps):
             # snapshot state BEFORE a terminal step deletes the aircraft
-            obs, rew, term, trunc, info = env.step(acts[t])
+            obs, rew, term, trunc, info = _step(env, acts[t])
             trunc = (t + 1) >= max_steps
-            O.append(flat(obs, ob.VERTICAL_OBS_KEYS)); R.append(rew); T.append(int(term))
+            O.append(flat(obs, keys)); R.append(rew); T.append(int(term))
             TR.append(trunc)
             INF.append([info["total_reward"], info["total_intrusions"], info["final_altitude"]])
             if term or trunc:
@@ -126,7 +150,7 @@ def gen_vertical(bs, mods, num_intruders, episodes, seed, max_steps=300):
         L = len(O)
         pad = lambda a, shape, dt: np.concatenate([np.asarray(a, dt), np.zeros((max_steps - L,) + shape, dt)])
         rec["spawn"].append(spawn)
-        rec["obs0"].append(flat(obs0, ob.VERTICAL_OBS_KEYS))
+        rec["obs0"].append(flat(obs0, keys))
         rec["actions"].append(acts)
         rec["obs"].append(pad(O, (len(O[0]),), np.float64))
         rec["reward"].append(pad(R, (), np.float64))
@@ -142,12 +166,12 @@ def gen_vertical(bs, mods, num_intruders, episodes, seed, max_steps=300):
     return out
 
 
-def gen_horizontal(bs, mods, num_intruders, episodes, seed, max_steps=300):
+def gen_horizontal(bs, mods, num_intruders, episodes, seed, max_steps=300, wind=None):
     m = mods["horizontal"]
     m.NUM_INTRUDERS = num_intruders
     np.random.seed(seed)
     rng_act = np.random.default_rng(seed)
-    env = m.HorizontalCREnv()
+    env, keys = _wrap(mods, m.HorizontalCREnv(), ob.HORIZONTAL_OBS_KEYS, wind)
     rec = {k: [] for k in ("spawn", "obs0", "actions", "obs", "reward", "terminated",
                            "truncated", "intr", "state", "info", "length", "wpt")}
     for ep in range(episodes):
@@ -158,9 +182,9 @@ def gen_horizontal(bs, mods, num_intruders, episodes, seed, max_steps=300):
         acts = rng_act.uniform(-1, 1, (max_steps, 1))
         O, R, T, TR, IN, ST, INF = [], [], [], [], [], [], []
         for t in range(max_steps):
-            obs, rew, term, trunc, info = env.step(acts[t])
+            obs, rew, term, trunc, info = _step(env, acts[t])
             trunc = (t + 1) >= max_steps
-            O.append(flat(obs, ob.HORIZONTAL_OBS_KEYS)); R.append(rew); T.append(int(term))
+            O.append(flat(obs, keys)); R.append(rew); T.append(int(term))
             TR.append(trunc)
             INF.append([info["total_reward"], info["total_intrusions"], info["average_drift"]])
             if term:        # the env deleted every aircraft (horizontal_cr_env.py:119-122)
@@ -176,7 +200,7 @@ def gen_horizontal(bs, mods, num_intruders, episodes, seed, max_steps=300):
         L = len(O)
         pad = lambda a, shape, dt: np.concatenate([np.asarray(a, dt), np.zeros((max_steps - L,) + shape, dt)])
         rec["spawn"].append(spawn)
-        rec["obs0"].append(flat(obs0, ob.HORIZONTAL_OBS_KEYS))
+        rec["obs0"].append(flat(obs0, keys))
         rec["actions"].append(acts)
         rec["obs"].append(pad(O, (len(O[0]),), np.float64))
         rec["reward"].append(pad(R, (), np.float64))
@@ -193,11 +217,11 @@ def gen_horizontal(bs, mods, num_intruders, episodes, seed, max_steps=300):
     return out
 
 
-def gen_descent(bs, mods, episodes, seed, max_steps=300):
+def gen_descent(bs, mods, episodes, seed, max_steps=300, wind=None):
     m = mods["descent"]
     np.random.seed(seed)
     rng_act = np.random.default_rng(seed)
-    env = m.DescentEnv()
+    env, keys = _wrap(mods, m.DescentEnv(), ob.DESCENT_OBS_KEYS, wind)
     rec = {k: [] for k in ("spawn", "obs0", "actions", "obs", "reward", "terminated",
                            "truncated", "state", "info", "length")}
     for ep in range(episodes):
@@ -210,9 +234,9 @@ def gen_descent(bs, mods, episodes, seed, max_steps=300):
         O, R, T, TR, ST, INF = [], [], [], [], [], []
         for t in range(max_steps):
             pre = snap(bs)
-            obs, rew, term, trunc, info = env.step(acts[t])
+            obs, rew, term, trunc, info = _step(env, acts[t])
             trunc = (t + 1) >= max_steps
-            O.append(flat(obs, ob.DESCENT_OBS_KEYS)); R.append(rew); T.append(int(term))
+            O.append(flat(obs, keys)); R.append(rew); T.append(int(term))
             TR.append(trunc)
             INF.append([info["total_reward"], info["final_altitude"]])
             ST.append(snap(bs) if bs.traf.ntraf else pre)
@@ -221,9 +245,9 @@ def gen_descent(bs, mods, episodes, seed, max_steps=300):
         L = len(O)
         pad = lambda a, shape, dt: np.concatenate([np.asarray(a, dt), np.zeros((max_steps - L,) + shape, dt)])
         rec["spawn"].append(spawn)
-        rec["obs0"].append(flat(obs0, ob.DESCENT_OBS_KEYS))
+        rec["obs0"].append(flat(obs0, keys))
         rec["actions"].append(acts)
-        rec["obs"].append(pad(O, (4,), np.float64))
+        rec["obs"].append(pad(O, (len(O[0]),), np.float64))
         rec["reward"].append(pad(R, (), np.float64))
         rec["terminated"].append(pad(T, (), np.int8))
         rec["truncated"].append(pad(TR, (), np.int8))
@@ -233,6 +257,60 @@ def gen_descent(bs, mods, episodes, seed, max_steps=300):
     out = {k: np.stack(v) if k != "length" else np.array(v) for k, v in rec.items()}
     out["seed"] = np.array(seed)
     return out
+
+
+# Wind fields for the WindFieldWrapper goldens (README of bluesky_gym/wrappers: a static
+# field of 4 points; here also one placed on the Merge approach, a 3-D profile and a
+# constant single point).
+WIND_MERGE = dict(lat=np.array([52.5, 52.5, 54.2, 54.2]), lon=np.array([4.2, 5.3, 4.2, 5.3]),
+                  vnorth=np.array([[16.0, 12.0, 14.0, 15.0]]), veast=np.array([[3.0, 7.0, 9.0, 4.0]]))
+WIND_README = dict(lat=np.array([51.9, 51.9, 52.1, 52.1]), lon=np.array([3.9, 4.1, 3.9, 4.1]),
+                   vnorth=np.array([[16.0, 12.0, 14.0, 15.0]]), veast=np.array([[3.0, 7.0, 9.0, 4.0]]))
+WIND_3D = dict(lat=np.array([51.9, 51.9, 52.1, 52.1]), lon=np.array([3.9, 4.1, 3.9, 4.1]),
+               vnorth=np.array([[2.0, -3.0, 4.0, 1.0], [16.0, 12.0, 14.0, 15.0], [30.0, 25.0, 28.0, 20.0]]),
+               veast=np.array([[1.0, 2.0, -2.0, 0.5], [3.0, 7.0, 9.0, 4.0], [-10.0, -6.0, -8.0, -12.0]]),
+               alt=np.array([0.0, 2000.0, 5000.0]))
+WIND_ONE = dict(lat=52.0, lon=4.0, vnorth=np.array([[-12.0]]), veast=np.array([[8.0]]))
+WINDS = {"merge": WIND_MERGE, "readme": WIND_README, "3d": WIND_3D, "one": WIND_ONE}
+
+
+def wind_record(w):
+    out = {"wind_lat": np.atleast_1d(np.asarray(w["lat"], np.float64)),
+           "wind_lon": np.atleast_1d(np.asarray(w["lon"], np.float64)),
+           "wind_vnorth": np.asarray(w["vnorth"], np.float64),
+           "wind_veast": np.asarray(w["veast"], np.float64)}
+    if w.get("alt") is not None:
+        out["wind_alt"] = np.asarray(w["alt"], np.float64)
+    return out
+
+
+def gen_noisy_merge(bs, mods, num_ac, episodes, seed, noise, max_steps=50):
+    """Reference NoisyObservationWrapper (wrappers/uncertainty.py) around MergeEnv: records
+    the noisy observations (noise drawn from the global np.random in the env's dict order)."""
+    m = mods["merge"]
+    m.NUM_AC = num_ac
+    random.seed(seed)
+    np.random.seed(seed + 1000)
+    rng_act = np.random.default_rng(seed)
+    env = mods["uncertainty"].NoisyObservationWrapper(m.MergeEnv(), noise_level=noise)
+    O0, O, L = [], [], []
+    acts_all = []
+    for ep in range(episodes):
+        obs0, _ = env.reset()
+        acts = rng_act.uniform(-1, 1, (max_steps, 2))
+        acts_all.append(acts)
+        OO = []
+        for t in range(max_steps):
+            obs, rew, term, trunc, info = env.step(acts[t])
+            OO.append(flat(obs, ob.MERGE_OBS_KEYS))
+            if term or (t + 1) >= max_steps:
+                break
+        O0.append(flat(obs0, ob.MERGE_OBS_KEYS))
+        L.append(len(OO))
+        O.append(np.concatenate([np.asarray(OO), np.zeros((max_steps - len(OO), len(OO[0])))]))
+    return {"obs0": np.stack(O0), "obs": np.stack(O), "length": np.array(L),
+            "actions": np.stack(acts_all), "num_ac": np.array(num_ac), "seed": np.array(seed),
+            "noise": np.array(noise)}
 
 
 def main():
@@ -255,6 +333,15 @@ def main():
         ("descent", lambda: gen_descent(bs, mods, 4, 6)),
         ("horizontal_N6", lambda: gen_horizontal(bs, mods, 5, 3, 7)),
         ("horizontal_N16", lambda: gen_horizontal(bs, mods, 15, 2, 8)),
+        ("wind_merge_N16", lambda: {**gen_merge(bs, mods, 16, 3, 9, wind=WIND_MERGE),
+                                    **wind_record(WIND_MERGE)}),
+        ("wind_vertical_N6", lambda: {**gen_vertical(bs, mods, 5, 3, 10, wind=WIND_3D),
+                                      **wind_record(WIND_3D)}),
+        ("wind_descent", lambda: {**gen_descent(bs, mods, 3, 11, wind=WIND_ONE),
+                                  **wind_record(WIND_ONE)}),
+        ("noisy_merge_N8", lambda: gen_noisy_merge(bs, mods, 8, 2, 13, 0.2)),
+        ("wind_horizontal_N6", lambda: {**gen_horizontal(bs, mods, 5, 2, 12, wind=WIND_README),
+                                        **wind_record(WIND_README)}),
     ]
     for name, job in jobs:
         out = job()

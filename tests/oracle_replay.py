@@ -5,6 +5,23 @@ from __future__ import annotations
 import numpy as np
 
 from oracle import batched as ob
+from oracle import bluesky_subset as bsx
+
+
+def wind_from_golden(g):
+    """The WindField a wind_* fixture was recorded with (None for the others)."""
+    if "wind_lat" not in g:
+        return None
+    f = bsx.WindField()
+    f.addpointvne(g["wind_lat"], g["wind_lon"], g["wind_vnorth"], g["wind_veast"],
+                  g["wind_alt"] if "wind_alt" in g else None)
+    return f
+
+
+def _apply_wind(o, g):
+    f = wind_from_golden(g)
+    if f is not None:
+        o.set_wind(f, augment_obs=True)
 
 
 def replay_merge(g, autoreset=ob.AUTORESET_NONE):
@@ -12,6 +29,7 @@ def replay_merge(g, autoreset=ob.AUTORESET_NONE):
     N = int(g["num_ac"])
     T = g["actions"].shape[1]
     o = ob.MergeOracle(n_ep, num_ac=N, autoreset=autoreset, compute_cd=False)
+    _apply_wind(o, g)
     r0 = o.reset(spawn=g["spawn"])
     out = {"obs0": r0["obs"], "obs": [], "reward": [], "terminated": [], "truncated": [],
            "topk": [], "intr": [], "state": [], "info": []}
@@ -35,6 +53,7 @@ def replay_vertical(g, autoreset=ob.AUTORESET_NONE):
     N = int(g["num_ac"])
     T = g["actions"].shape[1]
     o = ob.VerticalOracle(n_ep, num_ac=N, autoreset=autoreset, compute_cd=False)
+    _apply_wind(o, g)
     r0 = o.reset(spawn=g["spawn"])
     out = {"obs0": r0["obs"], "obs": [], "reward": [], "terminated": [], "truncated": [],
            "intr": [], "state": [], "info": []}
@@ -56,6 +75,7 @@ def replay_descent(g, autoreset=ob.AUTORESET_NONE):
     n_ep = len(g["length"])
     T = g["actions"].shape[1]
     o = ob.DescentOracle(n_ep, autoreset=autoreset)
+    _apply_wind(o, g)
     r0 = o.reset(spawn=g["spawn"])
     out = {"obs0": r0["obs"], "obs": [], "reward": [], "terminated": [], "truncated": [],
            "state": [], "info": []}
@@ -75,6 +95,7 @@ def replay_horizontal(g, autoreset=ob.AUTORESET_NONE):
     N = int(g["num_ac"])
     T = g["actions"].shape[1]
     o = ob.HorizontalOracle(n_ep, num_ac=N, autoreset=autoreset, compute_cd=False)
+    _apply_wind(o, g)
     r0 = o.reset(spawn=g["spawn"])
     out = {"obs0": r0["obs"], "obs": [], "reward": [], "terminated": [], "truncated": [],
            "intr": [], "state": [], "info": []}

@@ -47,7 +47,8 @@ def test_shape_helpers_match_reference_spaces():
     assert lib.bsg_action_dim(nat.ENV_DESCENT) == 1
     assert lib.bsg_spawn_width(nat.ENV_MERGE, 32) == 64
     assert lib.bsg_spawn_width(nat.ENV_VERTICAL_CR, 6) == 22
-    for kind, n, k in ((nat.ENV_MERGE, 32, 5), (nat.ENV_VERTICAL_CR, 32, 0), (nat.ENV_DESCENT, 1, 0)):
+    for kind, n, k in ((nat.ENV_MERGE, 32, 5), (nat.ENV_VERTICAL_CR, 32, 0), (nat.ENV_DESCENT, 1, 0),
+                       (nat.ENV_HORIZONTAL_CR, 6, 0), (nat.ENV_HORIZONTAL_CR, 32, 0)):
         assert ObsLayout(kind, n, k).dim == lib.bsg_obs_dim(kind, n, k)
 
 
@@ -55,10 +56,12 @@ def test_ctypes_struct_layout_matches_c(tmp_path):
     prog = tmp_path / "layout.c"
     fields_c = [f[0] for f in nat.BsgConfig._fields_]
     fields_b = [f[0] for f in nat.BsgBuffers._fields_]
+    fields_w = [f[0] for f in nat.BsgWind._fields_]
     lines = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{HDR}"', "int main(void){",
-             'printf("%zu %zu\\n", sizeof(bsg_config), sizeof(bsg_buffers));']
+             'printf("%zu %zu %zu\\n", sizeof(bsg_config), sizeof(bsg_buffers), sizeof(bsg_wind));']
     lines += [f'printf("%zu\\n", offsetof(bsg_config, {f}));' for f in fields_c]
     lines += [f'printf("%zu\\n", offsetof(bsg_buffers, {f}));' for f in fields_b]
+    lines += [f'printf("%zu\\n", offsetof(bsg_wind, {f}));' for f in fields_w]
     lines += ["return 0;}"]
     prog.write_text("\n".join(lines))
     exe = tmp_path / "layout"
@@ -66,9 +69,12 @@ def test_ctypes_struct_layout_matches_c(tmp_path):
     vals = subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()
     assert int(vals[0]) == C.sizeof(nat.BsgConfig)
     assert int(vals[1]) == C.sizeof(nat.BsgBuffers)
-    offs = [int(v) for v in vals[2:]]
-    assert offs[:len(fields_c)] == [getattr(nat.BsgConfig, f).offset for f in fields_c]
-    assert offs[len(fields_c):] == [getattr(nat.BsgBuffers, f).offset for f in fields_b]
+    assert int(vals[2]) == C.sizeof(nat.BsgWind)
+    offs = [int(v) for v in vals[3:]]
+    nc, nb = len(fields_c), len(fields_b)
+    assert offs[:nc] == [getattr(nat.BsgConfig, f).offset for f in fields_c]
+    assert offs[nc:nc + nb] == [getattr(nat.BsgBuffers, f).offset for f in fields_b]
+    assert offs[nc + nb:] == [getattr(nat.BsgWind, f).offset for f in fields_w]
 
 
 def test_create_fails_cleanly_without_device_or_bad_config():

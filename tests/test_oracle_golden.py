@@ -100,6 +100,55 @@ def test_horizontal_oracle_matches_reference(name):
     assert np.array_equal(r["intr"][nt], g["intr"][nt])
 
 
+def _eq_obs(r, g, m):
+    """Equal observations; the NaN wind keys of a terminal step (the reference wrapper
+    raises there, tests/golden/make_golden.py:_step) are excluded."""
+    a, b = r["obs"][m], g["obs"][m]
+    fin = np.isfinite(b)
+    assert np.array_equal(a[fin], b[fin])
+    assert (~fin).sum() <= 2 * int(g["terminated"].sum())
+
+
+@pytest.mark.parametrize("name", ["wind_merge_N16", "wind_vertical_N6", "wind_descent",
+                                  "wind_horizontal_N6"])
+def test_wind_wrapper_oracle_matches_reference(name):
+    """WindFieldWrapper(augment_obs=True) around each env (wrappers/wind.py)."""
+    g = load(name)
+    kind = name.split("_")[1]
+    r = {"merge": rp.replay_merge, "vertical": rp.replay_vertical, "descent": rp.replay_descent,
+         "horizontal": rp.replay_horizontal}[kind](g)
+    m = rp.step_mask(g)
+    assert np.array_equal(r["obs0"], g["obs0"])
+    _eq_obs(r, g, m)
+    assert np.array_equal(r["reward"][m], g["reward"][m])
+    assert np.array_equal(r["terminated"][m].astype(np.int8), g["terminated"][m])
+    nt = _nonterminal(g)
+    assert np.array_equal(r["state"][nt], g["state"][nt])
+
+
+def test_wind_field_interpolation_properties():
+    f = bsx.WindField()
+    assert f.getdata(52.0, 4.0, 1000.0) == (0.0, 0.0) or f.winddim == 0
+    f.addpointvne(52.0, 4.0, np.array([[-12.0]]), np.array([[8.0]]))
+    assert f.winddim == 1
+    vn, ve = f.getdata(np.array([50.0, 55.0]), np.array([3.0, 9.0]), np.array([0.0, 9000.0]))
+    assert np.all(vn == -12.0) and np.all(ve == 8.0)
+    g = bsx.WindField()
+    g.addpointvne(np.array([51.9, 52.1]), np.array([4.0, 4.0]), np.array([[10.0, 20.0]]),
+                  np.array([[0.0, 0.0]]))
+    assert g.winddim == 2
+    vn, _ = g.getdata(np.array([51.9, 52.0, 52.1]), np.array([4.0, 4.0, 4.0]), 0.0)
+    assert abs(vn[0] - 10.0) < 1e-9 and abs(vn[2] - 20.0) < 1e-9 and abs(vn[1] - 15.0) < 1e-6
+    h = bsx.WindField()
+    h.addpointvne(52.0, 4.0, np.array([[0.0], [30.0]]), np.array([[0.0], [0.0]]),
+                  np.array([0.0, 3000.0]))
+    assert h.winddim == 3
+    # profiles are sampled on the fixed 100 ft axis: exact at axis levels, linear between
+    lv = 50 * 100 * 0.3048
+    vn, _ = h.getdata(52.0, 4.0, np.array([0.0, lv, lv + 0.5 * 30.48, 3048.0, 20000.0]))
+    np.testing.assert_allclose(vn, [0.0, 15.24, 15.24 + 0.5 * 0.3048, 30.0, 30.0], atol=1e-9)
+
+
 def test_merge_distribution_sanity():
     """Random-policy Merge episodes land in the published untrained-policy band
     (~1.3-1.5 intrusions, ~-9 return, average drift ~1.5 rad)."""
