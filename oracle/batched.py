@@ -205,6 +205,8 @@ class _Base:
         term = res["terminated"] & live
         trunc = (self.step_count >= self.max_steps) & live if self.max_steps > 0 \
             else np.zeros(self.E, bool)
+        if "truncated_env" in res:          # SectorCR: ownship left the sector
+            trunc = trunc | (res["truncated_env"] & live)
         reward = np.where(live, res["reward"], 0.0)
         obs = res["obs"].copy()
         done = term | trunc

@@ -524,10 +524,13 @@ def traffic_update(st, dt, route_lat, route_lon, route_next_qdr, wind=None):
 # --------------------------------------------------------------------------------------
 # StateBased conflict detection (bluesky/traffic/asas/statebased.py: detect)
 # --------------------------------------------------------------------------------------
-def statebased_detect(lat, lon, alt, trk, gs, vs, rpz=RPZ, hpz=HPZ, dtlookahead=DTLOOKAHEAD):
+def statebased_detect(lat, lon, alt, trk, gs, vs, rpz=RPZ, hpz=HPZ, dtlookahead=DTLOOKAHEAD,
+                      active=None):
     """All-pairs CPA over the last axis (N aircraft).  Returns a dict with
     swconfl[..., i, j], swlos[..., i, j], inconf[..., i], tcpamax[..., i],
-    dist (m), tcpa, dcpa2, tinconf, toutconf.  [i, j] = aircraft j relative to i."""
+    dist (m), tcpa, dcpa2, tinconf, toutconf.  [i, j] = aircraft j relative to i.
+    active[..., N] (optional): aircraft that exist (SectorCR's per-episode count); pairs
+    with an absent aircraft are neither conflicts, LoS nor part of min_sep."""
     n = lat.shape[-1]
     eye = np.eye(n, dtype=bool)
     I = eye.astype(np.float64)
@@ -564,9 +567,14 @@ def statebased_detect(lat, lon, alt, trk, gs, vs, rpz=RPZ, hpz=HPZ, dtlookahead=
     toutconf = np.minimum(toutver, touthor)
     swconfl = swhorconf & (tinconf <= toutconf) & (toutconf > 0.0) & \
         (tinconf < dtlookahead) & ~eye
+    swlos = (dist < rpz) & (np.abs(dalt) < hpz)
+    if active is not None:
+        pair = active[..., :, None] & active[..., None, :]
+        swconfl = swconfl & pair
+        swlos = swlos & pair
+        eye = eye | ~pair
     inconf = np.any(swconfl, -1)
     tcpamax = np.max(tcpa * swconfl, -1)
-    swlos = (dist < rpz) & (np.abs(dalt) < hpz)
     # minimum separation among the pairs inside the StateBased horizon (the pairs whose
     # conflict state can be true): dist <= (RPZ + DTLOOKAHEAD*vrel)(1+1e-9) + 1 m
     horizon = (rpz + dtlookahead * vrel) * (1.0 + 1e-9) + 1.0

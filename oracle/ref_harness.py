@@ -19,6 +19,7 @@ import types
 
 import numpy as np
 
+from . import areas
 from . import bluesky_subset as bsx
 
 
@@ -28,6 +29,11 @@ from . import bluesky_subset as bsx
 class _AP:
     def __init__(self, traf):
         self._traf = traf
+
+    @property
+    def trk(self):
+        """Autopilot.trk (view of the commanded track)."""
+        return self._traf.st.ap_trk
 
     def selaltcmd(self, idx, alt, vspd=None):
         """Autopilot.selaltcmd(idx, alt, vspd)."""
@@ -220,6 +226,12 @@ def make_bluesky_module():
     for name in ("kwikqdrdist", "kwikdist", "kwikdist_matrix", "kwikqdrdist_matrix",
                  "kwikpos", "qdrdist", "rwgs84"):
         setattr(geo, name, getattr(bsx, name))
+    areafilter = areas.AreaFilter()
+    af = types.ModuleType("bluesky.tools.areafilter")
+    af.defineArea = areafilter.defineArea
+    af.deleteArea = areafilter.deleteArea
+    af.checkInside = areafilter.checkInside
+    tools.areafilter = af
     aero = types.ModuleType("bluesky.tools.aero")
     aero.kts = bsx.kts
     aero.nm = bsx.nm
@@ -235,7 +247,8 @@ def make_bluesky_module():
     simulation.ScreenIO = ScreenIO
     bs.simulation = simulation
     return bs, {"bluesky": bs, "bluesky.tools": tools, "bluesky.tools.geo": geo,
-                "bluesky.tools.aero": aero, "bluesky.simulation": simulation}
+                "bluesky.tools.aero": aero, "bluesky.tools.areafilter": af,
+                "bluesky.simulation": simulation}
 
 
 def _gym_stub():
@@ -342,6 +355,8 @@ def load_reference_envs(reference_root="/root/reference"):
         "vertical": importlib.import_module("bluesky_gym.envs.vertical_cr_env"),
         "descent": importlib.import_module("bluesky_gym.envs.descent_env"),
         "horizontal": importlib.import_module("bluesky_gym.envs.horizontal_cr_env"),
+        "static": importlib.import_module("bluesky_gym.envs.static_obstacle_env"),
+        "sector": importlib.import_module("bluesky_gym.envs.sector_cr_env"),
         "functions": importlib.import_module("bluesky_gym.envs.common.functions"),
         "wind": importlib.import_module("bluesky_gym.wrappers.wind"),
         "uncertainty": importlib.import_module("bluesky_gym.wrappers.uncertainty"),

@@ -26,7 +26,9 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(os.path.dirname(HERE))
 sys.path.insert(0, REPO)
 
+from oracle import areas as oa              # noqa: E402
 from oracle import batched as ob            # noqa: E402
+from oracle import batched_areas as oba     # noqa: E402
 from oracle import bluesky_subset as bsx    # noqa: E402
 from oracle.ref_harness import load_reference_envs  # noqa: E402
 
@@ -259,6 +261,114 @@ def gen_descent(bs, mods, episodes, seed, max_steps=300, wind=None):
     return out
 
 
+def gen_static(bs, mods, episodes, seed, max_steps=100):
+    """StaticObstacleEnv (static_obstacle_env.py) with the legacy np.random seeded; records
+    the obstacle geometry the reference built (pins the host spawn rows)."""
+    m = mods["static"]
+    np.random.seed(seed)
+    rng_act = np.random.default_rng(seed)
+    env = m.StaticObstacleEnv()
+    keys = oba.STATIC_OBS_KEYS
+    rec = {k: [] for k in ("spawn", "obs0", "actions", "obs", "reward", "terminated",
+                           "truncated", "state", "info", "length", "clat", "clon", "R",
+                           "wpt", "poly_lat", "poly_lon", "nvert")}
+    for ep in range(episodes):
+        rs = np.random.RandomState()
+        rs.set_state(np.random.get_state())
+        spawn = oa.static_spawn_from_np_random(rs)
+        obs0, _ = env.reset()
+        acts = rng_act.uniform(-1, 1, (max_steps, 2))
+        O, R, T, TR, ST, INF = [], [], [], [], [], []
+        for t in range(max_steps):
+            obs, rew, term, trunc, info = _step(env, acts[t])
+            trunc = (t + 1) >= max_steps
+            O.append(flat(obs, keys)); R.append(rew); T.append(int(term)); TR.append(trunc)
+            ST.append(snap(bs))
+            INF.append([info["total_reward"], info["waypoint_reached"], info["crashed"],
+                        info["average_drift"]])
+            if term or trunc:
+                break
+        L = len(O)
+        pad = lambda a, shape, dt: np.concatenate([np.asarray(a, dt), np.zeros((max_steps - L,) + shape, dt)])
+        rec["spawn"].append(spawn)
+        rec["obs0"].append(flat(obs0, keys))
+        rec["actions"].append(acts)
+        rec["obs"].append(pad(O, (len(O[0]),), np.float64))
+        rec["reward"].append(pad(R, (), np.float64))
+        rec["terminated"].append(pad(T, (), np.int8))
+        rec["truncated"].append(pad(TR, (), np.int8))
+        rec["state"].append(pad(ST, ST[0].shape, np.float64))
+        rec["info"].append(pad(INF, (4,), np.float64))
+        rec["length"].append(L)
+        rec["clat"].append(env.obstacle_centre_lat)
+        rec["clon"].append(env.obstacle_centre_lon)
+        rec["R"].append(env.obstacle_radius)
+        rec["wpt"].append([env.wpt_lat[0], env.wpt_lon[0]])
+        pl = np.zeros((oa.STATIC_NUM_OBSTACLES, oa.STATIC_VMAX))
+        pn = np.zeros((oa.STATIC_NUM_OBSTACLES, oa.STATIC_VMAX))
+        nv = []
+        for o, verts in enumerate(env.obstacle_vertices):
+            v = np.asarray(verts)
+            pl[o, :len(v)], pn[o, :len(v)] = v[:, 0], v[:, 1]
+            nv.append(len(v))
+        rec["poly_lat"].append(pl); rec["poly_lon"].append(pn); rec["nvert"].append(nv)
+    out = {k: np.stack(v) if k != "length" else np.array(v) for k, v in rec.items()}
+    out["seed"] = np.array(seed)
+    return out
+
+
+def gen_sector(bs, mods, episodes, seed, N=32, max_steps=200):
+    """SectorCREnv (sector_cr_env.py, density mode "normal") with np.random seeded."""
+    m = mods["sector"]
+    np.random.seed(seed)
+    rng_act = np.random.default_rng(seed)
+    env = m.SectorCREnv()
+    keys = oba.SECTOR_OBS_KEYS
+    rec = {k: [] for k in ("spawn", "obs0", "actions", "obs", "reward", "terminated",
+                           "truncated", "state", "info", "length", "intr", "num_ac_ep")}
+    for ep in range(episodes):
+        rs = np.random.RandomState()
+        rs.set_state(np.random.get_state())
+        spawn = oa.sector_spawn_from_np_random(rs, N)
+        obs0, _ = env.reset()
+        assert env.num_ac == int(spawn[0])
+        acts = rng_act.uniform(-1, 1, (max_steps, 2))
+        O, R, T, TR, ST, INF, IN = [], [], [], [], [], [], []
+        for t in range(max_steps):
+            obs, rew, term, trunc, info = _step(env, acts[t])
+            trunc = bool(trunc) or (t + 1) >= max_steps
+            O.append(flat(obs, keys)); R.append(rew); T.append(int(term)); TR.append(trunc)
+            st = np.zeros((len(STATE_FIELDS), N))
+            st[:, :env.num_ac] = snap(bs)
+            ST.append(st)
+            lat, lon = bs.traf.lat, bs.traf.lon
+            _, di = bs.tools.geo.kwikqdrdist(lat[0], lon[0], lat[1:], lon[1:])
+            inn = np.zeros(N - 1, bool)
+            inn[:env.num_ac - 1] = di < m.INTRUSION_DISTANCE
+            IN.append(inn)
+            INF.append([info["total_reward"], info["total_intrusions"], info["average_drift"]])
+            if term or trunc:
+                break
+        L = len(O)
+        pad = lambda a, shape, dt: np.concatenate([np.asarray(a, dt), np.zeros((max_steps - L,) + shape, dt)])
+        rec["spawn"].append(spawn)
+        rec["obs0"].append(flat(obs0, keys))
+        rec["actions"].append(acts)
+        rec["obs"].append(pad(O, (len(O[0]),), np.float64))
+        rec["reward"].append(pad(R, (), np.float64))
+        rec["terminated"].append(pad(T, (), np.int8))
+        rec["truncated"].append(pad(TR, (), np.int8))
+        rec["state"].append(pad(ST, ST[0].shape, np.float64))
+        rec["info"].append(pad(INF, (3,), np.float64))
+        rec["intr"].append(pad(IN, (N - 1,), np.int8))
+        rec["length"].append(L)
+        rec["num_ac_ep"].append(env.num_ac)
+    out = {k: np.stack(v) if k != "length" else np.array(v) for k, v in rec.items()}
+    out["num_ac"] = np.array(N)
+    out["seed"] = np.array(seed)
+    return out
+
+
 # Wind fields for the WindFieldWrapper goldens (README of bluesky_gym/wrappers: a static
 # field of 4 points; here also one placed on the Merge approach, a 3-D profile and a
 # constant single point).
@@ -339,6 +449,8 @@ def main():
                                       **wind_record(WIND_3D)}),
         ("wind_descent", lambda: {**gen_descent(bs, mods, 3, 11, wind=WIND_ONE),
                                   **wind_record(WIND_ONE)}),
+        ("static", lambda: gen_static(bs, mods, 3, 14)),
+        ("sector_N32", lambda: gen_sector(bs, mods, 3, 15)),
         ("noisy_merge_N8", lambda: gen_noisy_merge(bs, mods, 8, 2, 13, 0.2)),
         ("wind_horizontal_N6", lambda: {**gen_horizontal(bs, mods, 5, 2, 12, wind=WIND_README),
                                         **wind_record(WIND_README)}),

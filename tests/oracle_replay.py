@@ -114,6 +114,56 @@ def replay_horizontal(g, autoreset=ob.AUTORESET_NONE):
     return {k: (np.stack(v, 1) if k not in ("obs0", "wpt") else v) for k, v in out.items()}
 
 
+def replay_static(g, autoreset=ob.AUTORESET_NONE):
+    from oracle import batched_areas as oba
+    n_ep = len(g["length"])
+    T = g["actions"].shape[1]
+    o = oba.StaticOracle(n_ep, autoreset=autoreset)
+    _apply_wind(o, g)
+    r0 = o.reset(spawn=g["spawn"])
+    out = {"obs0": r0["obs"], "obs": [], "reward": [], "terminated": [], "truncated": [],
+           "state": [], "info": []}
+    geo = {"clat": o.clat.copy(), "clon": o.clon.copy(), "R": o.R.copy(),
+           "wpt": np.stack([o.wlat, o.wlon], 1), "polys": [list(p) for p in o.polys]}
+    for t in range(T):
+        r = o.step(g["actions"][:, t])
+        out["obs"].append(r["obs"]); out["reward"].append(r["reward"])
+        out["terminated"].append(r["terminated"]); out["truncated"].append(r["truncated"])
+        out["state"].append(np.stack([o.st.lat, o.st.lon, o.st.alt, o.st.hdg, o.st.tas,
+                                      o.st.cas, o.st.vs], 1))
+        inf = o.info()
+        out["info"].append(np.stack([inf["total_reward"], inf["waypoint_reached"],
+                                     inf["crashed"], inf["average_drift"]], 1))
+    res = {k: (np.stack(v, 1) if k != "obs0" else v) for k, v in out.items()}
+    res["geo"] = geo
+    return res
+
+
+def replay_sector(g, autoreset=ob.AUTORESET_NONE):
+    from oracle import batched_areas as oba
+    n_ep = len(g["length"])
+    N = int(g["num_ac"])
+    T = g["actions"].shape[1]
+    o = oba.SectorOracle(n_ep, num_ac=N, autoreset=autoreset, compute_cd=False)
+    _apply_wind(o, g)
+    r0 = o.reset(spawn=g["spawn"])
+    out = {"obs0": r0["obs"], "obs": [], "reward": [], "terminated": [], "truncated": [],
+           "intr": [], "state": [], "info": []}
+    for t in range(T):
+        r = o.step(g["actions"][:, t])
+        out["obs"].append(r["obs"]); out["reward"].append(r["reward"])
+        out["terminated"].append(r["terminated"]); out["truncated"].append(r["truncated"])
+        out["intr"].append(np.stack([(r["intr_mask"] >> np.uint64(i + 1)) & np.uint64(1)
+                                     for i in range(N - 1)], 1).astype(np.int8))
+        st = np.stack([o.st.lat, o.st.lon, o.st.alt, o.st.hdg, o.st.tas, o.st.cas, o.st.vs], 1)
+        st = np.where(o.active()[:, None, :], st, 0.0)
+        out["state"].append(st)
+        inf = o.info()
+        out["info"].append(np.stack([inf["total_reward"], inf["total_intrusions"],
+                                     inf["average_drift"]], 1))
+    return {k: (np.stack(v, 1) if k != "obs0" else v) for k, v in out.items()}
+
+
 def step_mask(g):
     """[n_ep, T] bool: steps inside each recorded episode."""
     T = g["actions"].shape[1]

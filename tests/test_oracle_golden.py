@@ -149,6 +149,48 @@ def test_wind_field_interpolation_properties():
     np.testing.assert_allclose(vn, [0.0, 15.24, 15.24 + 0.5 * 0.3048, 30.0, 30.0], atol=1e-9)
 
 
+def test_static_oracle_matches_reference():
+    """StaticObstacleEnv: geometry built from the host spawn rows equals the reference's,
+    and obs / reward / done / info / state replay bit for bit (per-substep reward with the
+    previous observation's waypoint distance and drift, static_obstacle_env.py:132-150)."""
+    g = load("static")
+    r = rp.replay_static(g)
+    geo = r["geo"]
+    assert np.array_equal(geo["clat"], g["clat"]) and np.array_equal(geo["clon"], g["clon"])
+    assert np.array_equal(geo["R"], g["R"]) and np.array_equal(geo["wpt"], g["wpt"])
+    for e in range(len(g["length"])):
+        for o in range(len(geo["polys"][e])):
+            n = int(g["nvert"][e, o])
+            assert np.array_equal(geo["polys"][e][o][0], g["poly_lat"][e, o, :n])
+            assert np.array_equal(geo["polys"][e][o][1], g["poly_lon"][e, o, :n])
+    m = rp.step_mask(g)
+    assert np.array_equal(r["obs0"], g["obs0"])
+    for k in ("obs", "reward", "state"):
+        assert np.array_equal(r[k][m], g[k][m]), k
+    assert np.array_equal(r["terminated"][m].astype(np.int8), g["terminated"][m])
+    ri, gi = r["info"][m], g["info"][m]
+    for c in (0, 1, 2):
+        assert np.array_equal(ri[:, c], gi[:, c])
+    np.testing.assert_allclose(ri[:, 3], gi[:, 3], rtol=1e-14, atol=0)
+
+
+def test_sector_oracle_matches_reference():
+    g = load("sector_N32")
+    r = rp.replay_sector(g)
+    m = rp.step_mask(g)
+    assert np.array_equal(g["spawn"][:, 0].astype(int), g["num_ac_ep"])
+    assert np.array_equal(r["obs0"], g["obs0"])
+    for k in ("obs", "reward", "state"):
+        assert np.array_equal(r[k][m], g[k][m]), k
+    assert np.array_equal(r["terminated"][m].astype(np.int8), g["terminated"][m])
+    assert np.array_equal(r["truncated"][m].astype(np.int8), g["truncated"][m])
+    assert np.array_equal(r["intr"][m], g["intr"][m])
+    ri, gi = r["info"][m], g["info"][m]
+    for c in (0, 1):
+        assert np.array_equal(ri[:, c], gi[:, c])
+    np.testing.assert_allclose(ri[:, 2], gi[:, 2], rtol=1e-14, atol=0)
+
+
 def test_merge_distribution_sanity():
     """Random-policy Merge episodes land in the published untrained-policy band
     (~1.3-1.5 intrusions, ~-9 return, average drift ~1.5 rad)."""
