@@ -17,6 +17,7 @@ MAX_ROUTE = 4
 WIND_NALT = 451
 
 ENV_MERGE, ENV_VERTICAL_CR, ENV_DESCENT, ENV_HORIZONTAL_CR = 0, 1, 2, 3
+ENV_STATIC_OBSTACLE, ENV_SECTOR_CR = 4, 5
 AUTORESET_NONE, AUTORESET_NEXT_STEP, AUTORESET_SAME_STEP = 0, 1, 2
 
 E_CODES = {-1: "BSG_E_INVALID_ARG", -2: "BSG_E_HIP", -3: "BSG_E_STATE", -4: "BSG_E_UNSUPPORTED"}
@@ -45,6 +46,8 @@ class BsgConfig(C.Structure):
         ("seed", C.c_uint64),
         ("route_len", C.c_int32),
         ("env_offset", C.c_int32),
+        ("kind_option", C.c_int32),
+        ("reserved0", C.c_int32),
         ("route_lat", C.c_double * MAX_ROUTE),
         ("route_lon", C.c_double * MAX_ROUTE),
         ("route_next_qdr", C.c_double * MAX_ROUTE),
@@ -61,7 +64,7 @@ BUFFER_FIELDS = [
     ("step_count", _i32p), ("flags", _i32p), ("episode", _u32p), ("wpt_reach", _i32p),
     ("faf_reached", _i32p), ("total_intrusions", _i32p), ("total_reward", _dp),
     ("drift_sum", _dp), ("target_alt", _dp), ("final_altitude", _dp),
-    ("env_wpt_lat", _dp), ("env_wpt_lon", _dp),
+    ("env_wpt_lat", _dp), ("env_wpt_lon", _dp), ("env_geom", _dp), ("env_aux", _dp),
     ("obs", _fp), ("final_obs", _fp), ("reward", _fp), ("terminated", _u8p),
     ("truncated", _u8p), ("topk", _i32p), ("intr_mask", _u64p), ("conf_mask", _u64p),
     ("los_mask", _u64p), ("tcpamax", _fp), ("min_sep", _fp), ("ep_info", _dp),
@@ -86,7 +89,7 @@ class BsgWind(C.Structure):
 EXPORTED_SYMBOLS = (
     "bsg_abi_version", "bsg_last_error", "bsg_obs_dim", "bsg_action_dim", "bsg_spawn_width",
     "bsg_create", "bsg_destroy", "bsg_bind", "bsg_reset", "bsg_step", "bsg_set_timing",
-    "bsg_step_timing", "bsg_set_stamps", "bsg_set_wind", "bsg_ctx_obs_dim",
+    "bsg_step_timing", "bsg_set_stamps", "bsg_set_wind", "bsg_ctx_obs_dim", "bsg_geom_width",
 )
 
 _lib = None
@@ -118,6 +121,8 @@ def load_library(path: str | None = None):
     lib.bsg_action_dim.argtypes = [C.c_int32]
     lib.bsg_spawn_width.restype = C.c_int32
     lib.bsg_spawn_width.argtypes = [C.c_int32, C.c_int32]
+    lib.bsg_geom_width.restype = C.c_int32
+    lib.bsg_geom_width.argtypes = [C.c_int32, C.c_int32]
     lib.bsg_create.restype = C.c_int32
     lib.bsg_create.argtypes = [C.POINTER(BsgConfig), C.POINTER(C.c_void_p)]
     lib.bsg_destroy.restype = C.c_int32

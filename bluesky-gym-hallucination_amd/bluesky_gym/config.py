@@ -8,6 +8,11 @@ Descent:  bluesky_gym/envs/descent_env.py:10-30 (ACTION_FREQUENCY=30, 'DT 1' at 
           TimeLimit 300 at __init__.py:9)
 HorizontalCR: bluesky_gym/envs/horizontal_cr_env.py:11-30 (NUM_INTRUDERS=5,
           ACTION_FREQUENCY=10, 'DT 5' at :71, TimeLimit 300 at __init__.py:19-22)
+StaticObstacle: bluesky_gym/envs/static_obstacle_env.py:12-41 (ACTION_FREQUENCY=10,
+          'DT 1' at :85, TimeLimit 100 at __init__.py:36-40)
+SectorCR: bluesky_gym/envs/sector_cr_env.py:11-38 (ACTION_FREQUENCY=5, NUM_AC_STATE=4,
+          'DT 1' at :78, TimeLimit 200 at __init__.py:30-34); the aircraft count is drawn
+          per episode, num_ac is the capacity of an env (default 32)
 """
 from __future__ import annotations
 
@@ -61,6 +66,7 @@ class EnvKindConfig:
     action_frequency: int
     simdt: float
     max_episode_steps: int
+    kind_option: int = 0
 
     def to_c(self, num_envs, autoreset, compute_cd, seed, device, env_offset=0) -> nat.BsgConfig:
         c = nat.BsgConfig()
@@ -77,6 +83,7 @@ class EnvKindConfig:
         c.device = int(device)
         c.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
         c.env_offset = int(env_offset)
+        c.kind_option = int(self.kind_option)
         if self.kind == nat.ENV_MERGE:
             # ADDWPT FIX ; DEST RWY (merge_env.py:155-156)
             c.route_len = 2
@@ -103,6 +110,18 @@ def vertical_config(num_intruders=5, action_frequency=30, simdt=1.0, max_episode
 def horizontal_config(num_intruders=5, action_frequency=10, simdt=5.0, max_episode_steps=300):
     return EnvKindConfig(nat.ENV_HORIZONTAL_CR, num_intruders + 1, 0, action_frequency, simdt,
                          max_episode_steps)
+
+
+def static_config(action_frequency=10, simdt=1.0, max_episode_steps=100):
+    return EnvKindConfig(nat.ENV_STATIC_OBSTACLE, 1, 0, action_frequency, simdt, max_episode_steps)
+
+
+def sector_config(num_ac=32, action_frequency=5, simdt=1.0, max_episode_steps=200,
+                  density_mode="normal"):
+    if density_mode not in ("normal", "uniform"):
+        raise ValueError("density_mode must be 'normal' or 'uniform' (sector_cr_env.py:95-100)")
+    return EnvKindConfig(nat.ENV_SECTOR_CR, num_ac, 4, action_frequency, simdt, max_episode_steps,
+                         0 if density_mode == "normal" else 1)
 
 
 def descent_config(action_frequency=30, simdt=1.0, max_episode_steps=300):

@@ -31,7 +31,8 @@ class DeviceBatch:
                                    else torch.device(device).index or 0)
         self.autoreset = autoreset
         self.want_learner = bool(learner)
-        self.compute_cd = bool(compute_cd) and cfg.kind != nat.ENV_DESCENT
+        self.compute_cd = bool(compute_cd) and cfg.kind not in (nat.ENV_DESCENT,
+                                                                 nat.ENV_STATIC_OBSTACLE)
         self.obs_dim = self.lib.bsg_obs_dim(cfg.kind, cfg.num_ac, cfg.num_ac_state)
         if self.obs_dim < 0:
             raise nat.BsgError(f"invalid env config {cfg}")
@@ -69,6 +70,11 @@ class DeviceBatch:
         if self.cfg.kind == nat.ENV_HORIZONTAL_CR:
             self.envs["env_wpt_lat"] = z((E,), torch.float64)
             self.envs["env_wpt_lon"] = z((E,), torch.float64)
+        gw = self.lib.bsg_geom_width(self.cfg.kind, N)
+        if gw > 0:
+            self.envs["env_geom"] = z((E, gw), torch.float64)
+        if self.cfg.kind == nat.ENV_STATIC_OBSTACLE:
+            self.envs["env_aux"] = z((E, 4), torch.float64)
         # learner hand-off rows [obs, reward, terminated, truncated] (RCCL all-gather payload)
         self.learner = z((E, self.obs_dim + 3), torch.float32) if self.want_learner else None
         if self.compute_cd:

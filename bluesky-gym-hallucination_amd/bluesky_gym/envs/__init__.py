@@ -3,4 +3,6 @@ from .descent_env import DescentEnv  # noqa: F401
 from .merge_env import MergeEnv  # noqa: F401
 from .vertical_cr_env import VerticalCREnv  # noqa: F401
 from .horizontal_cr_env import HorizontalCREnv  # noqa: F401
-from ._out_of_scope import PlanWaypointEnv, SectorCREnv, StaticObstacleEnv  # noqa: F401
+from .sector_cr_env import SectorCREnv  # noqa: F401
+from .static_obstacle_env import StaticObstacleEnv  # noqa: F401
+from ._out_of_scope import PlanWaypointEnv  # noqa: F401

@@ -28,10 +28,9 @@ class SingleEnvBase(_gym.Env):
         self.kind_cfg = kind_cfg
         self.layout = ObsLayout(kind_cfg.kind, kind_cfg.num_ac, kind_cfg.num_ac_state)
         self.observation_space = self.layout.observation_space(_gym.spaces)
-        act = 2 if kind_cfg.kind == nat.ENV_MERGE else 1
-        self.action_space = _gym.spaces.Box(-1, 1, shape=(act,), dtype=np.float64)
         self.batch = DeviceBatch(kind_cfg, 1, autoreset=nat.AUTORESET_NONE,
                                  compute_cd=compute_cd, device=device)
+        self.action_space = _gym.spaces.Box(-1, 1, shape=(self.batch.act_dim,), dtype=np.float64)
 
     def set_wind(self, table, augment_obs=False):
         """Wind field for this env (bluesky_gym.wrappers.wind.WindFieldWrapper)."""
@@ -59,7 +58,9 @@ class SingleEnvBase(_gym.Env):
         obs = self._obs()
         reward = float(self.batch.reward.cpu().numpy()[0])
         terminated = int(self.batch.terminated.cpu().numpy()[0])
-        return obs, reward, terminated, False, self._info()
+        # only SectorCR truncates by itself (ownship left the sector, sector_cr_env.py:146)
+        truncated = bool(self.batch.truncated.cpu().numpy()[0])
+        return obs, reward, terminated, truncated, self._info()
 
     def render(self):
         if self.render_mode == "human":

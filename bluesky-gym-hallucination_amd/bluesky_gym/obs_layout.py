@@ -32,12 +32,26 @@ def horizontal_sizes(ni):
             "x_difference_speed": ni, "y_difference_speed": ni}
 
 
+def static_sizes(nobst=10):
+    return {"cos_difference_restricted_area_pos": nobst, "destination_waypoint_cos_drift": 1,
+            "destination_waypoint_distance": 1, "destination_waypoint_sin_drift": 1,
+            "restricted_area_distance": nobst, "restricted_area_radius": nobst,
+            "sin_difference_restricted_area_pos": nobst}
+
+
+def sector_sizes(k=4):
+    return {"airspeed": 1, "cos(drift)": 1, "cos(track)": k, "distances": k, "sin(drift)": 1,
+            "sin(track)": k, "vx_r": k, "vy_r": k, "x_r": k, "y_r": k}
+
+
 def descent_sizes():
     return {"altitude": 1, "runway_distance": 1, "target_altitude": 1, "vz": 1}
 
 
 # reference Box bounds (low, high) per key
 _BOUNDS = {"cos(drift)": (-1, 1), "sin(drift)": (-1, 1), "faf_reached": (0, 1)}
+_KIND_BOUNDS = {nat.ENV_SECTOR_CR: {"airspeed": (-1, 1)},
+                nat.ENV_STATIC_OBSTACLE: {"restricted_area_radius": (0, 1)}}
 
 
 WIND_KEYS = ("wind_u", "wind_v")     # bluesky_gym/wrappers/wind.py:21-22
@@ -57,6 +71,12 @@ REF_ORDER = {
     nat.ENV_HORIZONTAL_CR: ("intruder_distance", "cos_difference_pos", "sin_difference_pos",
                             "x_difference_speed", "y_difference_speed", "waypoint_distance",
                             "cos_drift", "sin_drift"),
+    nat.ENV_STATIC_OBSTACLE: ("destination_waypoint_distance", "destination_waypoint_cos_drift",
+                              "destination_waypoint_sin_drift", "restricted_area_radius",
+                              "restricted_area_distance", "cos_difference_restricted_area_pos",
+                              "sin_difference_restricted_area_pos"),
+    nat.ENV_SECTOR_CR: ("cos(drift)", "sin(drift)", "airspeed", "x_r", "y_r", "vx_r", "vy_r",
+                        "cos(track)", "sin(track)", "distances"),
 }
 
 
@@ -68,12 +88,17 @@ class ObsLayout:
             sizes = vertical_sizes(num_ac - 1)
         elif kind == nat.ENV_HORIZONTAL_CR:
             sizes = horizontal_sizes(num_ac - 1)
+        elif kind == nat.ENV_STATIC_OBSTACLE:
+            sizes = static_sizes()
+        elif kind == nat.ENV_SECTOR_CR:
+            sizes = sector_sizes(num_ac_state)
         else:
             sizes = descent_sizes()
         if wind:
             sizes.update({k: 1 for k in WIND_KEYS})
         self.keys = tuple(sorted(sizes))
         self.ref_order = REF_ORDER[kind] + (WIND_KEYS if wind else ())
+        self.bounds = {**_BOUNDS, **_KIND_BOUNDS.get(kind, {})}
         self.sizes = {k: sizes[k] for k in self.keys}
         off = 0
         self.slices = {}
@@ -89,6 +114,6 @@ class ObsLayout:
         return {k: flat[..., self.slices[k]] for k in self.ref_order}
 
     def observation_space(self, spaces):
-        return spaces.Dict({k: spaces.Box(*_BOUNDS.get(k, (-np.inf, np.inf)), shape=(n,),
+        return spaces.Dict({k: spaces.Box(*self.bounds.get(k, (-np.inf, np.inf)), shape=(n,),
                                           dtype=np.float64)
                             for k, n in self.sizes.items()})

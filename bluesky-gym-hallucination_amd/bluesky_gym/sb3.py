@@ -84,9 +84,13 @@ class SB3VecEnv(_SB3Base):
                 elif self._kind == nat.ENV_VERTICAL_CR:
                     d["total_intrusions"] = int(ep[i, 1])
                     d["final_altitude"] = float(ep[i, 2])
-                elif self._kind == nat.ENV_HORIZONTAL_CR:
+                elif self._kind in (nat.ENV_HORIZONTAL_CR, nat.ENV_SECTOR_CR):
                     d["total_intrusions"] = int(ep[i, 1])
                     d["average_drift"] = float(ep[i, 2])
+                elif self._kind == nat.ENV_STATIC_OBSTACLE:
+                    d["waypoint_reached"] = int(ep[i, 1])
+                    d["crashed"] = int(ep[i, 2])
+                    d["average_drift"] = float(ep[i, 3])
                 else:
                     d["final_altitude"] = float(ep[i, 2])
                 d["TimeLimit.truncated"] = bool(trunc[i] and not term[i])

@@ -1,6 +1,6 @@
 """Gymnasium VectorEnv front-ends of the device batch (the ``vector_entry_point`` of
-MergeEnv-v0 / VerticalCREnv-v0 / DescentEnv-v0 / HorizontalCREnv-v0, registered by
-``register_envs``).
+MergeEnv-v0 / VerticalCREnv-v0 / DescentEnv-v0 / HorizontalCREnv-v0 / StaticObstacleEnv-v0 /
+SectorCREnv-v0, registered by ``register_envs``).
 
 ``gym.make_vec("MergeEnv-v0", num_envs=4096, vectorization_mode="vector_entry_point",
 num_ac=32)`` returns a :class:`MergeVectorEnv` whose E envs live on one HIP device and
@@ -16,7 +16,7 @@ from __future__ import annotations
 import numpy as np
 import torch
 
-from . import _gym, _native as nat, config as cfgmod, spawn as spawnmod
+from . import _gym, _native as nat, areas, config as cfgmod, spawn as spawnmod
 from .core import DeviceBatch
 from .obs_layout import ObsLayout
 
@@ -25,6 +25,8 @@ _INFO_KEYS = {
     nat.ENV_VERTICAL_CR: ("total_reward", "total_intrusions", "final_altitude"),
     nat.ENV_DESCENT: ("total_reward", "final_altitude"),
     nat.ENV_HORIZONTAL_CR: ("total_reward", "total_intrusions", "average_drift"),
+    nat.ENV_STATIC_OBSTACLE: ("total_reward", "waypoint_reached", "crashed", "average_drift"),
+    nat.ENV_SECTOR_CR: ("total_reward", "total_intrusions", "average_drift"),
 }
 
 
@@ -46,7 +48,7 @@ class BlueSkyVectorEnv(_gym.VectorEnv):
         self.learner = learner
         self.layout = ObsLayout(kind_cfg.kind, kind_cfg.num_ac, kind_cfg.num_ac_state)
         self.single_observation_space = self.layout.observation_space(_gym.spaces)
-        act = 2 if kind_cfg.kind == nat.ENV_MERGE else 1
+        act = 2 if kind_cfg.kind in (nat.ENV_MERGE, nat.ENV_STATIC_OBSTACLE, nat.ENV_SECTOR_CR) else 1
         self.single_action_space = _gym.spaces.Box(-1, 1, shape=(act,), dtype=np.float64)
         self.observation_space = _gym.spaces.Dict(
             {k: _gym.spaces.Box(-np.inf, np.inf, shape=(self.num_envs, n), dtype=np.float64)
@@ -89,6 +91,11 @@ class BlueSkyVectorEnv(_gym.VectorEnv):
                 rows.append(spawnmod.vertical_spawn(k.num_ac - 1, rs))
             elif k.kind == nat.ENV_HORIZONTAL_CR:
                 rows.append(spawnmod.horizontal_spawn(k.num_ac - 1, rs))
+            elif k.kind == nat.ENV_STATIC_OBSTACLE:
+                rows.append(areas.static_spawn(rs))
+            elif k.kind == nat.ENV_SECTOR_CR:
+                rows.append(areas.sector_spawn(k.num_ac, rs,
+                                               "normal" if k.kind_option == 0 else "uniform"))
             else:
                 rows.append(spawnmod.descent_spawn(rs))
         return torch.from_numpy(np.stack(rows))
@@ -143,7 +150,14 @@ class BlueSkyVectorEnv(_gym.VectorEnv):
         elif kind == nat.ENV_VERTICAL_CR:
             out = {"total_reward": tr, "total_intrusions": b.envs["total_intrusions"].cpu().numpy(),
                    "final_altitude": b.envs["final_altitude"].cpu().numpy()}
-        elif kind == nat.ENV_HORIZONTAL_CR:
+        elif kind == nat.ENV_STATIC_OBSTACLE:
+            aux = b.envs["env_aux"].cpu().numpy()
+            with np.errstate(invalid="ignore", divide="ignore"):
+                avg = b.envs["drift_sum"].cpu().numpy() / aux[:, 2]
+            out = {"total_reward": tr, "waypoint_reached": b.envs["wpt_reach"].cpu().numpy(),
+                   "crashed": aux[:, 3].astype(np.int32),
+                   "average_drift": np.where(aux[:, 2] > 0, avg, np.nan)}
+        elif kind in (nat.ENV_HORIZONTAL_CR, nat.ENV_SECTOR_CR):
             cnt = b.envs["step_count"].cpu().numpy()
             with np.errstate(invalid="ignore", divide="ignore"):
                 avg = b.envs["drift_sum"].cpu().numpy() / cnt
@@ -184,6 +198,20 @@ class HorizontalCRVectorEnv(BlueSkyVectorEnv):
             num_intruders = num_ac - 1
         super().__init__(cfgmod.horizontal_config(num_intruders, action_frequency, simdt,
                                                   max_episode_steps or 0), num_envs, **kw)
+
+
+class StaticObstacleVectorEnv(BlueSkyVectorEnv):
+    def __init__(self, num_envs=1, action_frequency=10, simdt=1.0, max_episode_steps=100, **kw):
+        kw.pop("compute_cd", None)
+        super().__init__(cfgmod.static_config(action_frequency, simdt, max_episode_steps or 0),
+                         num_envs, compute_cd=False, **kw)
+
+
+class SectorCRVectorEnv(BlueSkyVectorEnv):
+    def __init__(self, num_envs=1, num_ac=32, action_frequency=5, simdt=1.0, max_episode_steps=200,
+                 ac_density_mode="normal", **kw):
+        super().__init__(cfgmod.sector_config(num_ac, action_frequency, simdt, max_episode_steps or 0,
+                                              ac_density_mode), num_envs, **kw)
 
 
 class DescentVectorEnv(BlueSkyVectorEnv):

@@ -12,6 +12,7 @@
 #include <vector>
 
 #include "../../include/bsg.h"
+#include "bsg_areas.h"
 #include "bsg_internal.h"
 
 struct bsg_ctx {
@@ -66,6 +67,8 @@ int wind_obs_pos(const bsg_config& cfg) {
     case BSG_ENV_VERTICAL_CR: return 4 + 4 * NI;   // ... vz | x_/y_/z_difference_speed
     case BSG_ENV_DESCENT: return 4;                 // all keys sort before "wind"
     case BSG_ENV_HORIZONTAL_CR: return 3 * NI + 3; // ... waypoint_distance | x_/y_...
+    case BSG_ENV_STATIC_OBSTACLE: return 3 + 4 * bsg::SO_NOBST;  // all keys sort before "wind"
+    case BSG_ENV_SECTOR_CR: return 3 + 5 * K;      // ... vx_r, vy_r | x_r, y_r
     default: return 0;
   }
 }
@@ -124,13 +127,18 @@ int32_t bsg_obs_dim(int32_t kind, int32_t num_ac, int32_t k) {
     case BSG_ENV_VERTICAL_CR: return num_ac >= 2 ? 4 + 7 * (num_ac - 1) : BSG_E_INVALID_ARG;
     case BSG_ENV_DESCENT: return num_ac == 1 ? 4 : BSG_E_INVALID_ARG;
     case BSG_ENV_HORIZONTAL_CR: return num_ac >= 2 ? 3 + 5 * (num_ac - 1) : BSG_E_INVALID_ARG;
+    case BSG_ENV_STATIC_OBSTACLE: return num_ac == 1 ? 3 + 4 * bsg::SO_NOBST : BSG_E_INVALID_ARG;
+    case BSG_ENV_SECTOR_CR:        // at least NUM_AC_STATE + 1 aircraft (sector_cr_env.py:97)
+      return (num_ac >= 5 && k >= 1 && k <= 4) ? 3 + 7 * k : BSG_E_INVALID_ARG;
     default: return BSG_E_INVALID_ARG;
   }
 }
 
 int32_t bsg_action_dim(int32_t kind) {
   switch (kind) {
-    case BSG_ENV_MERGE: return 2;
+    case BSG_ENV_MERGE:
+    case BSG_ENV_STATIC_OBSTACLE:
+    case BSG_ENV_SECTOR_CR: return 2;
     case BSG_ENV_VERTICAL_CR:
     case BSG_ENV_DESCENT:
     case BSG_ENV_HORIZONTAL_CR: return 1;
@@ -144,7 +152,18 @@ int32_t bsg_spawn_width(int32_t kind, int32_t num_ac) {
     case BSG_ENV_VERTICAL_CR: return 2 + 4 * (num_ac - 1);
     case BSG_ENV_DESCENT: return 2;
     case BSG_ENV_HORIZONTAL_CR: return 3 * (num_ac - 1) + 1;
+    case BSG_ENV_STATIC_OBSTACLE: return bsg::SO_SPAWN_W;
+    case BSG_ENV_SECTOR_CR: return 4 + 2 * bsg::SC_VMAX + 3 * num_ac;
     default: return BSG_E_INVALID_ARG;
+  }
+}
+
+int32_t bsg_geom_width(int32_t kind, int32_t num_ac) {
+  (void)num_ac;
+  switch (kind) {
+    case BSG_ENV_STATIC_OBSTACLE: return bsg::SO_GEOM;
+    case BSG_ENV_SECTOR_CR: return bsg::SC_GEOM;
+    default: return 0;
   }
 }
 
@@ -166,6 +185,8 @@ int32_t bsg_create(const bsg_config* cfg, bsg_ctx** out) {
   if (cfg->route_len < 0 || cfg->route_len > BSG_MAX_ROUTE)
     return fail(BSG_E_INVALID_ARG, "bsg_create: route_len out of range%s%lld");
   if (cfg->env_offset < 0) return fail(BSG_E_INVALID_ARG, "bsg_create: env_offset < 0%s%lld");
+  if (cfg->kind_option != 0 && !(cfg->env_kind == BSG_ENV_SECTOR_CR && cfg->kind_option == 1))
+    return fail(BSG_E_INVALID_ARG, "bsg_create: invalid kind_option%s (%lld)", "", cfg->kind_option);
   if (cfg->env_kind == BSG_ENV_MERGE && cfg->route_len < 1)
     return fail(BSG_E_INVALID_ARG, "bsg_create: Merge needs the FIX/RWY route%s%lld");
   int ndev = 0;
@@ -211,6 +232,11 @@ int32_t bsg_bind(bsg_ctx* c, const bsg_buffers* b) {
     if (!required[i]) return fail(BSG_E_INVALID_ARG, "bsg_bind: required buffer #%s%lld is NULL", "", (long long)i);
   if (c->cfg.env_kind == BSG_ENV_HORIZONTAL_CR && (!b->env_wpt_lat || !b->env_wpt_lon))
     return fail(BSG_E_INVALID_ARG, "bsg_bind: HorizontalCR needs env_wpt_lat/env_wpt_lon%s%lld");
+  if ((c->cfg.env_kind == BSG_ENV_STATIC_OBSTACLE || c->cfg.env_kind == BSG_ENV_SECTOR_CR) &&
+      !b->env_geom)
+    return fail(BSG_E_INVALID_ARG, "bsg_bind: StaticObstacle/SectorCR need env_geom%s%lld");
+  if (c->cfg.env_kind == BSG_ENV_STATIC_OBSTACLE && !b->env_aux)
+    return fail(BSG_E_INVALID_ARG, "bsg_bind: StaticObstacle needs env_aux%s%lld");
   if (c->cfg.env_kind == BSG_ENV_MERGE && !b->topk)
     return fail(BSG_E_INVALID_ARG, "bsg_bind: Merge needs topk%s%lld");
   if (c->cfg.autoreset_mode == BSG_AUTORESET_SAME_STEP && !b->final_obs)
@@ -218,6 +244,7 @@ int32_t bsg_bind(bsg_ctx* c, const bsg_buffers* b) {
   if (c->wind.np > 0 && (!b->gs || !b->trk))
     return fail(BSG_E_INVALID_ARG, "bsg_bind: a wind field needs gs/trk%s%lld");
   if (c->cfg.compute_cd && c->cfg.env_kind != BSG_ENV_DESCENT &&
+      c->cfg.env_kind != BSG_ENV_STATIC_OBSTACLE &&
       (!b->conf_mask || !b->los_mask || !b->tcpamax || !b->min_sep))
     return fail(BSG_E_INVALID_ARG, "bsg_bind: compute_cd needs conf_mask/los_mask/tcpamax/min_sep%s%lld");
   c->bufs = *b;

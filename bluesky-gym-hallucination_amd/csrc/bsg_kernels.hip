@@ -33,6 +33,7 @@
 //     the distance as well.  min_sep is defined over the pairs inside the horizon.
 #include <hip/hip_runtime.h>
 
+#include "bsg_areas.h"
 #include "bsg_device.h"
 #include "bsg_internal.h"
 
@@ -631,7 +632,24 @@ __device__ __forceinline__ void spawn_horizontal(const KParams& p, int e, int j,
   s.selalt = 0.0;
 }
 
-// aux[0]: target altitude (Vertical/Descent); aux[0..1]: waypoint (HorizontalCR)
+// static_obstacle_env.py:96-124: obstacles + waypoint into env_geom, ownship at 52N 4E,
+// FL "350" (passed as 350 m), 150 kt CAS, heading (and commanded track) to the waypoint
+__device__ __forceinline__ void spawn_static(const KParams& p, int e, uint32_t episode, AC& s,
+                                             double* aux) {
+  double* geo = p.b.env_geom + (size_t)e * SO_GEOM;
+  const double* row = p.spawn ? p.spawn + (size_t)e * p.spawn_width : nullptr;
+  static_build(geo, row, (uint32_t)(e + p.cfg.env_offset), episode, p.seed);
+  cre(s, 52.0, 4.0, 0.0, 350.0, 150.0);
+  double qdr, d;
+  kwikqdrdist(s.lat, s.lon, geo[0], geo[1], &qdr, &d);
+  s.hdg = qdr;                                   // :121-123 (trk keeps the cre value)
+  s.ap_trk = qdr;
+  aux[0] = geo[0];
+  aux[1] = geo[1];
+}
+
+// aux[0]: target altitude (Vertical/Descent); aux[0..1]: waypoint (HorizontalCR);
+// aux[0..2]: lat, lon, hdg of this aircraft (SectorCR, from sector_reset_plan)
 template <int KIND>
 __device__ __forceinline__ void spawn(const KParams& p, int e, int j, uint32_t episode, AC& s,
                                       double* target) {
@@ -641,6 +659,11 @@ __device__ __forceinline__ void spawn(const KParams& p, int e, int j, uint32_t e
     spawn_vertical(p, e, j, episode, s, target);
   } else if constexpr (KIND == BSG_ENV_HORIZONTAL_CR) {
     spawn_horizontal(p, e, j, episode, s, target);
+  } else if constexpr (KIND == BSG_ENV_STATIC_OBSTACLE) {
+    spawn_static(p, e, episode, s, target);
+  } else if constexpr (KIND == BSG_ENV_SECTOR_CR) {
+    if (target[3] != 0.0) cre(s, target[0], target[1], target[2], 350.0, 150.0);
+    else s = AC{};                                 // slot beyond this episode's count
   } else {
     double alt_init;
     draw_alts(p, e, episode, TAG_DESC, &alt_init, target);
@@ -656,6 +679,9 @@ struct EnvScalars {
   uint32_t episode;
   double total_reward, drift_sum, target_alt, final_alt;
   double wpt_lat, wpt_lon;          // HorizontalCR waypoint
+  double aux[4];                    // env_aux (StaticObstacle: last obs waypoint distance km,
+                                    // last drift deg, drift samples, crashed)
+  int nac;                          // aircraft of this episode (SectorCR; else N)
 };
 
 __device__ __forceinline__ void load_env(const Buffers& b, int e, EnvScalars& v) {
@@ -664,6 +690,10 @@ __device__ __forceinline__ void load_env(const Buffers& b, int e, EnvScalars& v)
   v.episode = b.episode[e]; v.total_reward = b.total_reward[e]; v.drift_sum = b.drift_sum[e];
   v.target_alt = b.target_alt[e]; v.final_alt = b.final_altitude[e];
   if (b.env_wpt_lat) { v.wpt_lat = b.env_wpt_lat[e]; v.wpt_lon = b.env_wpt_lon[e]; }
+  if (b.env_aux) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v.aux[k] = b.env_aux[(size_t)e * 4 + k];
+  }
 }
 
 __device__ __forceinline__ void store_env(const Buffers& b, int e, const EnvScalars& v) {
@@ -672,14 +702,24 @@ __device__ __forceinline__ void store_env(const Buffers& b, int e, const EnvScal
   b.episode[e] = v.episode; b.total_reward[e] = v.total_reward; b.drift_sum[e] = v.drift_sum;
   b.target_alt[e] = v.target_alt; b.final_altitude[e] = v.final_alt;
   if (b.env_wpt_lat) { b.env_wpt_lat[e] = v.wpt_lat; b.env_wpt_lon[e] = v.wpt_lon; }
+  if (b.env_aux) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) b.env_aux[(size_t)e * 4 + k] = v.aux[k];
+  }
 }
 
 template <int KIND>
 __device__ __forceinline__ void reset_scalars(EnvScalars& v, const double aux[2]) {
   v.step_count = 0; v.flags = 0; v.wpt_reach = 0; v.faf_reached = 0; v.total_intr = 0;
   v.total_reward = 0.0; v.drift_sum = 0.0; v.final_alt = 0.0;
-  if constexpr (KIND == BSG_ENV_HORIZONTAL_CR) { v.wpt_lat = aux[0]; v.wpt_lon = aux[1]; }
-  else v.target_alt = aux[0];
+  v.aux[2] = 0.0; v.aux[3] = 0.0;
+  if constexpr (KIND == BSG_ENV_HORIZONTAL_CR || KIND == BSG_ENV_STATIC_OBSTACLE) {
+    v.wpt_lat = aux[0]; v.wpt_lon = aux[1];
+  } else if constexpr (KIND == BSG_ENV_SECTOR_CR) {
+    // waypoint and aircraft count were set by sector_reset_plan
+  } else {
+    v.target_alt = aux[0];
+  }
   v.episode += 1;
 }
 
@@ -714,6 +754,22 @@ __device__ __forceinline__ bool lane_obs(const LT& L, int base, int lane, double
     o[0] = x_r; o[1] = y_r; o[2] = vx_r; o[3] = vy_r; o[4] = ct; o[5] = st; o[6] = dmat;
     *sortkey = dmat;
     return dist < 4;                                       // _check_intrusion :280-281
+  } else if constexpr (KIND == BSG_ENV_SECTOR_CR) {
+    // sector_cr_env.py:245-278: positions in the flat NM frame about CENTER, in metres
+    const double cc = cos(SC_CLAT * kD2R);
+    const double x0 = (((lat0 - SC_CLAT) * 60) * 1.852) * 1000;
+    const double y0 = ((((lon0 - SC_CLON) * 60) * cc) * 1.852) * 1000;
+    const double xj = (((latj - SC_CLAT) * 60) * 1.852) * 1000;
+    const double yj = ((((lonj - SC_CLON) * 60) * cc) * 1.852) * 1000;
+    const double dx = xj - x0, dy = yj - y0;
+    const double d = sqrt(dx * dx + dy * dy);
+    const double vx_r = L.v[lane] - L.v[base], vy_r = L.u[lane] - L.u[base];
+    const double track = atan2(vy_r, vx_r);
+    double st, ct;
+    sincos(track, &st, &ct);
+    o[0] = dx; o[1] = dy; o[2] = vx_r; o[3] = vy_r; o[4] = ct; o[5] = st; o[6] = d;
+    *sortkey = d;
+    return dist < 5;                                       // _check_intrusion :329-338
   } else {
     // vertical_cr_env.py:133-156 / horizontal_cr_env.py:172-188 (gs == tas: no wind)
     const double alt0 = L.alt[base], vs0 = L.vs[base], gs0 = gs_of(L, base);
@@ -749,7 +805,17 @@ __device__ __forceinline__ void write_lane_obs(float* obs, float* fobs, float* l
     if (fobs) fobs[off] = f;
     if (lrn) lrn[off] = f;
   };
-  if constexpr (KIND == BSG_ENV_MERGE) {
+  if constexpr (KIND == BSG_ENV_SECTOR_CR) {
+    if (rank < K) {                         // sector_cr_env.py:280-291
+      put(2 + rank, o[4]);                  // cos(track)
+      put(2 + K + rank, (o[6] - 50000.) / 15000.);   // distances
+      put(3 + 2 * K + rank, o[5]);          // sin(track)
+      put(3 + 3 * K + rank, o[2] / 32);     // vx_r
+      put(3 + 4 * K + rank, o[3] / 66);     // vy_r
+      put(3 + 5 * K + rank, o[0] / 13000);  // x_r
+      put(3 + 6 * K + rank, o[1] / 13000);  // y_r
+    }
+  } else if constexpr (KIND == BSG_ENV_MERGE) {
     if (rank < K) {
       put(2 + rank, o[4]);                  // cos(track)
       put(2 + K + rank, o[6] / 250);        // distances
@@ -802,6 +868,23 @@ __device__ __forceinline__ void own_obs(const KParams& p, const LT& L, int lane,
     double sd, cd;
     sincos(*drift * kD2R, &sd, &cd);
     sc[0] = L.tas[lane]; sc[1] = cd; sc[2] = (double)ev.wpt_reach; sc[3] = sd; sc[4] = *wdist / 250;
+  } else if constexpr (KIND == BSG_ENV_SECTOR_CR) {
+    // sector_cr_env.py:233-243
+    double wqdr, wd;
+    kwikqdrdist(lat, lon, ev.wpt_lat, ev.wpt_lon, &wqdr, &wd);
+    *drift = bound180(L.hdg[lane] - wqdr);
+    double sd, cd;
+    sincos(*drift * kD2R, &sd, &cd);
+    sc[0] = (L.tas[lane] - 150) / 6; sc[1] = cd; sc[2] = sd; sc[3] = 0.0; sc[4] = 0.0;
+  } else if constexpr (KIND == BSG_ENV_STATIC_OBSTACLE) {
+    // static_obstacle_env.py:231-246 (waypoint terms; obstacles in static_obs_write)
+    double wqdr, wd;
+    kwikqdrdist(lat, lon, ev.wpt_lat, ev.wpt_lon, &wqdr, &wd);
+    *wdist = wd * 1.852;
+    *drift = bound180(L.hdg[lane] - wqdr);
+    double sd, cd;
+    sincos(*drift * kD2R, &sd, &cd);
+    sc[0] = *wdist / 170; sc[1] = cd; sc[2] = sd; sc[3] = 0.0; sc[4] = 0.0;
   } else if constexpr (KIND == BSG_ENV_HORIZONTAL_CR) {
     // horizontal_cr_env.py:191-203
     double wqdr, wd;
@@ -842,6 +925,14 @@ __device__ __forceinline__ void write_own_obs(float* obs, float* fobs, float* lr
     put(1 + 3 * NI, sc[3]);                 // runway_distance
     put(2 + 4 * NI, sc[2]);                 // target_altitude
     put(3 + 4 * NI, sc[1]);                 // vz
+  } else if constexpr (KIND == BSG_ENV_SECTOR_CR) {
+    put(0, sc[0]);                          // airspeed
+    put(1, sc[1]);                          // cos(drift)
+    put(2 + 2 * K, sc[2]);                  // sin(drift)
+  } else if constexpr (KIND == BSG_ENV_STATIC_OBSTACLE) {
+    put(SO_NOBST, sc[1]);                   // destination_waypoint_cos_drift
+    put(SO_NOBST + 1, sc[0]);               // destination_waypoint_distance
+    put(SO_NOBST + 2, sc[2]);               // destination_waypoint_sin_drift
   } else if constexpr (KIND == BSG_ENV_HORIZONTAL_CR) {
     const int NI = N - 1;
     put(NI, sc[0]);                         // cos_drift
@@ -849,6 +940,29 @@ __device__ __forceinline__ void write_own_obs(float* obs, float* fobs, float* lr
     put(3 * NI + 2, sc[2]);                 // waypoint_distance
   } else {
     put(0, sc[0]); put(1, sc[3]); put(2, sc[2]); put(3, sc[1]);
+  }
+}
+
+// static_obstacle_env.py:248-268: per obstacle centre distance / bearing and radius
+__device__ __forceinline__ void static_obs_write(const double* geo, double lat, double lon,
+                                                 double hdg, float* obs, float* fobs, float* lrn) {
+  auto put = [&](int off, double v) {
+    const float f = (float)v;
+    obs[off] = f;
+    if (fobs) fobs[off] = f;
+    if (lrn) lrn[off] = f;
+  };
+  for (int o = 0; o < SO_NOBST; ++o) {
+    const double* g = geo + 2 + o * SO_W;
+    double qdr, d;
+    kwikqdrdist(lat, lon, g[0], g[1], &qdr, &d);
+    const double bearing = bound180(hdg - qdr);
+    double sb, cb;
+    sincos(bearing * kD2R, &sb, &cb);
+    put(o, cb);                                         // cos_difference_restricted_area_pos
+    put(SO_NOBST + 3 + o, (d * 1.852) / 170);           // restricted_area_distance
+    put(2 * SO_NOBST + 3 + o, g[2] / 50);               // restricted_area_radius
+    put(3 * SO_NOBST + 3 + o, sb);                      // sin_difference_restricted_area_pos
   }
 }
 
@@ -878,6 +992,89 @@ __device__ __forceinline__ unsigned long long stamp_clock() {
 #define BSG_STAMP(slot, val) do { } while (0)
 #endif
 
+// SectorCR reset plan (block-uniform call; rs: this lane's env resets): the episode's
+// sector, aircraft count and, per aircraft slot j < count, the spawn (lat, lon, hdg) into
+// sp[0..2] with sp[3] = 1.  Host-drawn rows are copied; otherwise lane 0 of the env draws
+// the polygon and count, the slots draw their perimeter waypoints (ranked through LDS, as
+// sorted() does) and rejection-sample their positions in parallel.
+template <int GS>
+__device__ __forceinline__ void sector_reset_plan(const KParams& p, int e, int j, int g, bool rs,
+                                                  EnvScalars& ev, double sp[4]) {
+  __shared__ SectorPlan SP[64 / GS];
+  if (!__syncthreads_or(rs)) return;
+  double* geo = rs ? p.b.env_geom + (size_t)e * SC_GEOM : nullptr;
+  const uint32_t env = (uint32_t)(e + p.cfg.env_offset);
+  const int N = p.N;
+  if (p.spawn) {
+    if (rs) {
+      const double* row = p.spawn + (size_t)e * p.spawn_width;
+      const int nac = (int)row[0] < N ? (int)row[0] : N;
+      const int nv = (int)row[1];
+      if (j == 0) {
+        geo[0] = (double)nac;
+        geo[1] = (double)nv;
+        geo[2] = row[2 + 2 * SC_VMAX];
+        geo[3] = row[3 + 2 * SC_VMAX];
+        for (int k = 0; k < nv; ++k) {
+          geo[4 + k] = row[2 + k];
+          geo[4 + SC_VMAX + k] = row[2 + SC_VMAX + k];
+        }
+      }
+      ev.nac = nac;
+      ev.wpt_lat = row[2 + 2 * SC_VMAX];
+      ev.wpt_lon = row[3 + 2 * SC_VMAX];
+      if (j < nac) {
+        const double* q = row + 4 + 2 * SC_VMAX + 3 * j;
+        sp[0] = q[0]; sp[1] = q[1]; sp[2] = q[2]; sp[3] = 1.0;
+      }
+    }
+    return;
+  }
+  SectorPlan& P = SP[g];
+  if (rs && j == 0) sector_plan_polygon(P, geo, env, ev.episode, p.seed, N, p.cfg.kind_option);
+  __syncthreads();
+  const int nac = rs ? P.nac : 0;
+  double dj = 0.0;
+  if (rs && j < nac) {
+    U4 r = philox4x32_10(env, ev.episode, (uint32_t)(128 + j), TAG_SECT, p.seed);
+    dj = 0.0 + (P.perim - 0.0) * u01_53(r.x, r.y);
+    P.draw[j] = dj;
+  }
+  __syncthreads();
+  if (rs && j < nac) {
+    int rank = 0;
+    for (int k = 0; k < nac; ++k) rank += (P.draw[k] < dj) || (P.draw[k] == dj && k < j);
+    P.d[rank] = dj;
+  }
+  __syncthreads();
+  if (rs && j < nac) {
+    double wx, wy, wlat, wlon, la, lo;
+    sector_waypoint(P, P.d[j], &wx, &wy);
+    nm_to_latlong_sector(wx, wy, &wlat, &wlon);
+    if (j == 0) {
+      geo[2] = wlat;
+      geo[3] = wlon;
+      ev.wpt_lat = wlat;
+      ev.wpt_lon = wlon;
+    }
+    sector_position(P, geo, env, ev.episode, p.seed, j, &la, &lo);
+    sp[0] = la; sp[1] = lo; sp[2] = get_hdg(la, lo, wlat, wlon); sp[3] = 1.0;
+  }
+  if (rs) ev.nac = nac;
+}
+
+// HDG / SPD stack commands of the ownship: merge_env.py:286-293 (15 deg, 20 m/s),
+// static_obstacle_env.py:339-346 (45 deg, 20/3), sector_cr_env.py:313-320 (22.5 deg, 20/3)
+template <bool WIND>
+__device__ __forceinline__ void hdg_spd_action(const KParams& p, AC& s, double a0, double a1,
+                                               double d_heading, double d_speed) {
+  const double heading_new = bound180(s.hdg + a0 * d_heading);
+  const double speed_new = (s.cas + a1 * d_speed) * 1.94384;
+  s.ap_trk = hdg_command_track<WIND>(p.wind, s, heading_new);
+  s.nav &= ~1;
+  s.selspd = speed_new >= 1.0 ? speed_new * KTS : speed_new;
+}
+
 template <int KIND, int GS, bool WIND>
 __global__ __launch_bounds__(64) void step_kernel(KParams p) {
 #if defined(BSG_STAMPS) && BSG_STAMPS
@@ -901,6 +1098,21 @@ __global__ __launch_bounds__(64) void step_kernel(KParams p) {
 
   EnvScalars ev = {};
   if (env_ok) load_env(b, e, ev);
+  ev.nac = N;
+  if constexpr (KIND == BSG_ENV_SECTOR_CR) {
+    if (env_ok) {
+      const double* geo = b.env_geom + (size_t)e * SC_GEOM;
+      ev.nac = (int)geo[0];
+      ev.wpt_lat = geo[2];
+      ev.wpt_lon = geo[3];
+    }
+  } else if constexpr (KIND == BSG_ENV_STATIC_OBSTACLE) {
+    if (env_ok) {
+      const double* geo = b.env_geom + (size_t)e * SO_GEOM;
+      ev.wpt_lat = geo[0];
+      ev.wpt_lon = geo[1];
+    }
+  }
   bool resetting = false;
   if (env_ok) {
     if (p.mode == MODE_RESET) resetting = p.env_mask ? (p.env_mask[e] != 0) : true;
@@ -910,26 +1122,30 @@ __global__ __launch_bounds__(64) void step_kernel(KParams p) {
   const bool active = resetting || stepping;   // env produces outputs this launch
 
   // ---------------- A: spawn or propagate, store state ------------------------------
+  double sub_reward = 0.0;          // StaticObstacle: reward / done of the last substep
+  bool sub_done = false;
   {
     AC s = {};
-    double aux[2] = {ev.target_alt, 0.0};
+    double aux[4] = {ev.target_alt, 0.0, 0.0, 0.0};
+    if constexpr (KIND == BSG_ENV_SECTOR_CR) sector_reset_plan<GS>(p, e, j, g, resetting, ev, aux);
+    const bool on = ok && j < ev.nac;   // SectorCR: aircraft slot in use this episode
     if (ok) {
       if (resetting) {
         spawn<KIND>(p, e, j, ev.episode, s, aux);
       } else {
         load_ac<WIND>(b, a, s);
       }
-      if (stepping) {
+      if (stepping && on) {
         if (j == 0) {
           if constexpr (KIND == BSG_ENV_MERGE) {
-            // merge_env.py:286-293 -> HDG / SPD stack commands
-            const double dh = p.actions[(size_t)e * 2 + 0] * 15;
-            const double dv = p.actions[(size_t)e * 2 + 1] * 20;
-            const double heading_new = bound180(s.hdg + dh);
-            const double speed_new = (s.cas + dv) * 1.94384;
-            s.ap_trk = hdg_command_track<WIND>(p.wind, s, heading_new);
-            s.nav &= ~1;
-            s.selspd = speed_new >= 1.0 ? speed_new * KTS : speed_new;
+            hdg_spd_action<WIND>(p, s, p.actions[(size_t)e * 2 + 0], p.actions[(size_t)e * 2 + 1],
+                                 15.0, 20.0);
+          } else if constexpr (KIND == BSG_ENV_STATIC_OBSTACLE) {
+            hdg_spd_action<WIND>(p, s, p.actions[(size_t)e * 2 + 0], p.actions[(size_t)e * 2 + 1],
+                                 45.0, 20.0 / 3.0);
+          } else if constexpr (KIND == BSG_ENV_SECTOR_CR) {
+            hdg_spd_action<WIND>(p, s, p.actions[(size_t)e * 2 + 0], p.actions[(size_t)e * 2 + 1],
+                                 22.5, 20.0 / 3.0);
           } else if constexpr (KIND == BSG_ENV_HORIZONTAL_CR) {
             // horizontal_cr_env.py:272-275: HDG KL001 {hdg + a*45} (no wrap)
             s.ap_trk = hdg_command_track<WIND>(p.wind, s, s.hdg + p.actions[e] * 45);
@@ -948,7 +1164,25 @@ __global__ __launch_bounds__(64) void step_kernel(KParams p) {
           RouteRegs rt;
           rt.load(p.route);
           const double dt = p.cfg.simdt;
-          for (int it = 0; it < S; ++it) substep<WIND>(s, m, dt, rt, p.wind);
+          if constexpr (KIND == BSG_ENV_STATIC_OBSTACLE) {
+            // static_obstacle_env.py:132-150: _get_reward after every substep, with the
+            // waypoint distance and drift of the previous observation; stop when done
+            const double* geo = b.env_geom + (size_t)e * SO_GEOM;
+            for (int it = 0; it < S; ++it) {
+              substep<WIND>(s, m, dt, rt, p.wind);
+              int reach = 0;
+              if (ev.aux[0] < 5 && ev.wpt_reach != 1) { ev.wpt_reach = 1; reach = 1; }
+              const double dd = fabs(ev.aux[1] * kD2R);
+              ev.drift_sum += dd;
+              ev.aux[2] += 1.0;
+              const int nin = static_inside_count(geo, s.lat, s.lon);
+              if (nin > 0) ev.aux[3] = 1.0;
+              sub_reward = ((double)reach + dd * -0.01) + (double)(nin * -5);
+              if (ev.wpt_reach == 1 || nin > 0) { sub_done = true; break; }
+            }
+          } else {
+            for (int it = 0; it < S; ++it) substep<WIND>(s, m, dt, rt, p.wind);
+          }
           // update_airspeed's cas = vtas2cas(tas, alt) of the LAST substep (its alt is the
           // one before that substep's update_pos, i.e. m.at's key)
           s.cas = tas2cas_at(s.tas, m.at);
@@ -965,19 +1199,22 @@ __global__ __launch_bounds__(64) void step_kernel(KParams p) {
 #endif
 
   // ---------------- B: observation, reward, CD -----------------------------------------
+  constexpr bool kLaneObs = KIND != BSG_ENV_DESCENT && KIND != BSG_ENV_STATIC_OBSTACLE;
+  constexpr bool kRanked = KIND == BSG_ENV_MERGE || KIND == BSG_ENV_SECTOR_CR;
+  const bool on = ok && j < ev.nac;
   double o[7] = {0, 0, 0, 0, 0, 0, 0};
   double sortkey = __builtin_inf();
   bool intr = false;
-  if (ok && j > 0 && KIND != BSG_ENV_DESCENT) intr = lane_obs<KIND>(L, base, lane, o, &sortkey);
-  if constexpr (KIND == BSG_ENV_MERGE) {
+  if (kLaneObs && on && j > 0) intr = lane_obs<KIND>(L, base, lane, o, &sortkey);
+  if constexpr (kRanked) {
     L.d[lane] = sortkey;
   }
   __syncthreads();
   int rank = 0x7fffffff;
-  if constexpr (KIND == BSG_ENV_MERGE) {
-    if (ok && j > 0) rank = rank_in_group(L, base, lane, j, N);
+  if constexpr (kRanked) {
+    if (on && j > 0) rank = rank_in_group(L, base, lane, j, N);
   }
-  const uint64_t ib = group_bits<GS>(__ballot(ok && stepping && intr), g);
+  const uint64_t ib = group_bits<GS>(__ballot(on && stepping && intr), g);
   const int nintr = __popcll(ib);
 #if defined(BSG_STAMPS) && BSG_STAMPS
   BSG_STAMP(3, stamp_clock());
@@ -986,7 +1223,7 @@ __global__ __launch_bounds__(64) void step_kernel(KParams p) {
   // CD: StateBased all-pairs CPA, wave-compacted (see cd_candidate / cd_pair)
   uint64_t cmask = 0, lmask = 0;
   double tmax = 0.0, msep = __builtin_inf();
-  if (KIND != BSG_ENV_DESCENT && p.cfg.compute_cd) {
+  if (kLaneObs && p.cfg.compute_cd) {
     __shared__ unsigned short cd_list[64 * (GS > 1 ? GS - 1 : 1)];
     L.cm[lane] = 0ull;
     L.lm[lane] = 0ull;
@@ -994,9 +1231,9 @@ __global__ __launch_bounds__(64) void step_kernel(KParams p) {
     L.gmin[lane] = bits(__builtin_inf());
     // phase 1: candidate pairs of row j (no transcendentals)
     uint64_t cand = 0;
-    if (ok) {
+    if (on) {
       const double lati = L.lat[lane], ui = cd_u(L, lane), vi = cd_v(L, lane);
-      for (int k = 0; k < N; ++k) {
+      for (int k = 0; k < ev.nac; ++k) {
         const int lk = base + k;
         const double dlat = (L.lat[lk] - lati) * kD2R;
         const double du = cd_u(L, lk) - ui, dv = cd_v(L, lk) - vi;
@@ -1049,10 +1286,22 @@ __global__ __launch_bounds__(64) void step_kernel(KParams p) {
   if (ok && j == 0) {
     double wdist = 0, drift = 0, rwd = 0;
     own_obs<KIND>(p, L, lane, ev, sc, &wdist, &drift, &rwd);
+    bool trunc_env = false;
     if (stepping) {
       double r;
       int d = 0;
-      if constexpr (KIND == BSG_ENV_MERGE) {
+      if constexpr (KIND == BSG_ENV_STATIC_OBSTACLE) {
+        r = sub_reward;
+        d = sub_done ? 1 : 0;
+      } else if constexpr (KIND == BSG_ENV_SECTOR_CR) {
+        // _get_reward :295-302 (drift + intrusions); truncated once the ownship has left
+        // the sector (_check_inside_airspace :134-139)
+        const double dd = fabs(drift * kD2R);
+        r = dd * -0.1 + (double)(nintr * -1);
+        ev.drift_sum += dd;
+        const double* geo = b.env_geom + (size_t)e * SC_GEOM;
+        trunc_env = !point_in_ring(geo + 4, geo + 4 + SC_VMAX, (int)geo[1], L.lat[lane], L.lon[lane]);
+      } else if constexpr (KIND == BSG_ENV_MERGE) {
         // _check_waypoint :257-268 ; _check_drift :270-273 ; _check_intrusion :275-284
         const int wr = ev.wpt_reach;
         int reach = 0;
@@ -1087,8 +1336,11 @@ __global__ __launch_bounds__(64) void step_kernel(KParams p) {
       reward = (float)r;
       term = d != 0;
       ev.step_count += 1;
-      trunc = p.cfg.max_episode_steps > 0 && ev.step_count >= p.cfg.max_episode_steps;
+      trunc = (p.cfg.max_episode_steps > 0 && ev.step_count >= p.cfg.max_episode_steps) || trunc_env;
       done = term || trunc;
+    }
+    if constexpr (KIND == BSG_ENV_STATIC_OBSTACLE) {
+      if (active) { ev.aux[0] = wdist; ev.aux[1] = drift; }   // what the next step's reward sees
     }
     L.done[base] = done ? 1 : 0;
   }
@@ -1103,6 +1355,9 @@ __global__ __launch_bounds__(64) void step_kernel(KParams p) {
     float* lrn = (b.learner && !same_step_reset) ? b.learner + (size_t)e * (O + 3) : nullptr;
     if (j == 0) {
       write_own_obs<KIND>(obs, fobs, lrn, K, N, sc, p.wpos, ws);
+      if constexpr (KIND == BSG_ENV_STATIC_OBSTACLE)
+        static_obs_write(b.env_geom + (size_t)e * SO_GEOM, L.lat[lane], L.lon[lane], L.hdg[lane],
+                         obs, fobs, lrn);
       b.reward[e] = reward;
       b.terminated[e] = term ? 1 : 0;
       b.truncated[e] = trunc ? 1 : 0;
@@ -1120,21 +1375,25 @@ __global__ __launch_bounds__(64) void step_kernel(KParams p) {
         if constexpr (KIND == BSG_ENV_MERGE) {
           info[2] = (double)ev.faf_reached;
           info[3] = ev.drift_sum / (double)ev.step_count;
-        } else if constexpr (KIND == BSG_ENV_HORIZONTAL_CR) {
+        } else if constexpr (KIND == BSG_ENV_HORIZONTAL_CR || KIND == BSG_ENV_SECTOR_CR) {
           info[2] = ev.drift_sum / (double)ev.step_count;   // average_drift
           info[3] = 0.0;
+        } else if constexpr (KIND == BSG_ENV_STATIC_OBSTACLE) {
+          info[1] = (double)ev.wpt_reach;                   // waypoint_reached
+          info[2] = ev.aux[3];                              // crashed
+          info[3] = ev.drift_sum / ev.aux[2];               // average_drift (per substep)
         } else {
           info[2] = ev.final_alt;
           info[3] = 0.0;
         }
       }
-    } else {
+    } else if (on) {
       write_lane_obs<KIND>(obs, fobs, lrn, K, N, j, rank, o, p.wpos, ws);
       if constexpr (KIND == BSG_ENV_MERGE) {
         if (rank < K) b.topk[(size_t)e * K + rank] = j;
       }
     }
-    if (p.cfg.compute_cd && KIND != BSG_ENV_DESCENT) {
+    if (p.cfg.compute_cd && kLaneObs) {
       b.conf_mask[a] = cmask;
       b.los_mask[a] = lmask;
       b.tcpamax[a] = (float)tmax;
@@ -1147,7 +1406,9 @@ __global__ __launch_bounds__(64) void step_kernel(KParams p) {
   if (p.cfg.autoreset_mode == BSG_AUTORESET_SAME_STEP && __syncthreads_or(same_step_reset)) {
     {
       AC s = {};
-      double aux[2] = {ev.target_alt, 0.0};
+      double aux[4] = {ev.target_alt, 0.0, 0.0, 0.0};
+      if constexpr (KIND == BSG_ENV_SECTOR_CR)
+        sector_reset_plan<GS>(p, e, j, g, same_step_reset, ev, aux);
       if (same_step_reset && ok) {
         spawn<KIND>(p, e, j, ev.episode, s, aux);
         store_ac<WIND>(b, a, s);
@@ -1156,22 +1417,29 @@ __global__ __launch_bounds__(64) void step_kernel(KParams p) {
       if (same_step_reset) stage(L, lane, s);
     }
     __syncthreads();
+    const bool on2 = ok && j < ev.nac;
     sortkey = __builtin_inf();
-    if (same_step_reset && ok && j > 0 && KIND != BSG_ENV_DESCENT) lane_obs<KIND>(L, base, lane, o, &sortkey);
-    if constexpr (KIND == BSG_ENV_MERGE) {
+    if (kLaneObs && same_step_reset && on2 && j > 0) lane_obs<KIND>(L, base, lane, o, &sortkey);
+    if constexpr (kRanked) {
       if (same_step_reset) L.d[lane] = sortkey;
     }
     __syncthreads();
-    if (same_step_reset && ok) {
+    if (same_step_reset && on2) {
       float* obs = b.obs + (size_t)e * O;
       float* lrn = b.learner ? b.learner + (size_t)e * (O + 3) : nullptr;
       if (j == 0) {
         double wdist, drift, rwd;
         own_obs<KIND>(p, L, lane, ev, sc, &wdist, &drift, &rwd);
         write_own_obs<KIND>(obs, nullptr, lrn, K, N, sc, p.wpos, ws);
+        if constexpr (KIND == BSG_ENV_STATIC_OBSTACLE) {
+          static_obs_write(b.env_geom + (size_t)e * SO_GEOM, L.lat[lane], L.lon[lane],
+                           L.hdg[lane], obs, nullptr, lrn);
+          ev.aux[0] = wdist;
+          ev.aux[1] = drift;
+        }
       } else {
         int r = 0x7fffffff;
-        if constexpr (KIND == BSG_ENV_MERGE) r = rank_in_group(L, base, lane, j, N);
+        if constexpr (kRanked) r = rank_in_group(L, base, lane, j, N);
         write_lane_obs<KIND>(obs, nullptr, lrn, K, N, j, r, o, p.wpos, ws);
       }
     }
@@ -1192,13 +1460,19 @@ static hipError_t launch_kind_w(const KParams& p, hipStream_t st) {
   while (gs < p.N) gs <<= 1;
   const int epb = 64 / gs;
   const int grid = (p.E + epb - 1) / epb;
-  switch (gs) {
 #define BSG_CASE(G) \
-    case G: hipLaunchKernelGGL((step_kernel<KIND, G, WIND>), dim3(grid), dim3(64), p.lds_pad, st, p); break;
-    BSG_CASE(1) BSG_CASE(2) BSG_CASE(4) BSG_CASE(8) BSG_CASE(16) BSG_CASE(32) BSG_CASE(64)
-#undef BSG_CASE
-    default: return hipErrorInvalidValue;
+  case G: hipLaunchKernelGGL((step_kernel<KIND, G, WIND>), dim3(grid), dim3(64), p.lds_pad, st, p); break;
+  if constexpr (KIND == BSG_ENV_DESCENT || KIND == BSG_ENV_STATIC_OBSTACLE) {
+    switch (gs) { BSG_CASE(1) default: return hipErrorInvalidValue; }        // one aircraft
+  } else if constexpr (KIND == BSG_ENV_SECTOR_CR) {
+    switch (gs) { BSG_CASE(8) BSG_CASE(16) BSG_CASE(32) BSG_CASE(64) default: return hipErrorInvalidValue; }
+  } else {
+    switch (gs) {
+      BSG_CASE(2) BSG_CASE(4) BSG_CASE(8) BSG_CASE(16) BSG_CASE(32) BSG_CASE(64)
+      default: return hipErrorInvalidValue;
+    }
   }
+#undef BSG_CASE
   return hipGetLastError();
 }
 
@@ -1213,6 +1487,8 @@ hipError_t launch_step(const KParams& p, hipStream_t st) {
     case BSG_ENV_VERTICAL_CR: return launch_kind<BSG_ENV_VERTICAL_CR>(p, st);
     case BSG_ENV_DESCENT: return launch_kind<BSG_ENV_DESCENT>(p, st);
     case BSG_ENV_HORIZONTAL_CR: return launch_kind<BSG_ENV_HORIZONTAL_CR>(p, st);
+    case BSG_ENV_STATIC_OBSTACLE: return launch_kind<BSG_ENV_STATIC_OBSTACLE>(p, st);
+    case BSG_ENV_SECTOR_CR: return launch_kind<BSG_ENV_SECTOR_CR>(p, st);
     default: return hipErrorInvalidValue;
   }
 }

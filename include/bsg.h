@@ -41,7 +41,7 @@ enum {
 };
 
 enum { BSG_ENV_MERGE = 0, BSG_ENV_VERTICAL_CR = 1, BSG_ENV_DESCENT = 2,
-       BSG_ENV_HORIZONTAL_CR = 3 };
+       BSG_ENV_HORIZONTAL_CR = 3, BSG_ENV_STATIC_OBSTACLE = 4, BSG_ENV_SECTOR_CR = 5 };
 
 /* Vector-env autoreset conventions:
  *   NEXT_STEP: Gymnasium >= 1.0 VectorEnv default -- the step AFTER a done step resets
@@ -67,6 +67,9 @@ typedef struct bsg_config {
   int32_t route_len;         /* Merge intruder route (ADDWPT FIX; DEST RWY, merge_env.py:155-156) */
   int32_t env_offset;        /* global id of env 0 of this batch (Philox counter); a shard of a
                                 multi-GPU job passes its first global env id */
+  int32_t kind_option;       /* SectorCR ac_density_mode: 0 "normal", 1 uniform
+                                (sector_cr_env.py:45,95-100); 0 for the other kinds */
+  int32_t reserved0;
   double route_lat[BSG_MAX_ROUTE];
   double route_lon[BSG_MAX_ROUTE];
   double route_next_qdr[BSG_MAX_ROUTE]; /* qdrdist bearing wp k -> k+1; -999 for the last */
@@ -95,6 +98,10 @@ typedef struct bsg_buffers {
   double *final_altitude;    /* vertical/descent info */
   double *env_wpt_lat;       /* HorizontalCR per-env waypoint (horizontal_cr_env.py:135-148) */
   double *env_wpt_lon;
+  double *env_geom;          /* [E, bsg_geom_width] StaticObstacle obstacles + waypoint,
+                                SectorCR sector polygon + aircraft count + waypoint */
+  double *env_aux;           /* [E, 4] StaticObstacle: waypoint distance (km) and drift (deg)
+                                of the last observation, drift samples, crashed flag */
   /* ---- outputs --------------------------------------------------------------------- */
   float *obs;                /* [E, obs_dim] sorted-key flatten (gymnasium spaces.Dict order) */
   float *final_obs;          /* [E, obs_dim] terminal obs (SAME_STEP only; else may be NULL) */
@@ -142,12 +149,13 @@ const char* bsg_last_error(void);
 
 /* Flat observation length for an env kind (sum of the Box sizes of the reference
  * observation_space: merge_env.py:59-74 -> 5+7K; vertical_cr_env.py:67-83 -> 4+7(N-1);
- * descent_env.py:53-60 -> 4; horizontal_cr_env.py:49-60 -> 3+5(N-1)). Negative on
+ * descent_env.py:53-60 -> 4; horizontal_cr_env.py:49-60 -> 3+5(N-1);
+ * static_obstacle_env.py:61-71 -> 3+4*10; sector_cr_env.py:53-66 -> 3+7K). Negative on
  * invalid input.  A wind field with augment_obs adds 2 (bsg_ctx_obs_dim). */
 int32_t bsg_obs_dim(int32_t env_kind, int32_t num_ac, int32_t num_ac_state);
 
-/* Action width (merge_env.py:76 -> 2; vertical_cr_env.py:85 / descent_env.py:62 /
- * horizontal_cr_env.py:62 -> 1). */
+/* Action width (merge_env.py:76, static_obstacle_env.py:73, sector_cr_env.py:68 -> 2;
+ * vertical_cr_env.py:85 / descent_env.py:62 / horizontal_cr_env.py:62 -> 1). */
 int32_t bsg_action_dim(int32_t env_kind);
 
 /* Doubles per env of host-supplied spawn parameters for bsg_reset / bsg_step:
@@ -157,8 +165,18 @@ int32_t bsg_action_dim(int32_t env_kind);
  *                        the np.random draws of vertical_cr_env.py:188-195,267-268
  *   Descent  [2]       : alt_init, target_alt (descent_env.py:170-171)
  *   Horizontal [3(N-1)+1]: (dpsi, cpa, tlosh) per intruder, then the waypoint distance
- *                        (km), the np.random draws of horizontal_cr_env.py:130-132,140 */
+ *                        (km), the np.random draws of horizontal_cr_env.py:130-132,140
+ *   StaticObstacle [202]: per obstacle (distance km, bearing deg, area NM^2, vertices,
+ *                        16 uniform circle draws), then waypoint (distance km, bearing deg)
+ *                        (static_obstacle_env.py:148-226)
+ *   SectorCR [68+3N]   : aircraft count, vertices, 32 vertex lat, 32 vertex lon, ownship
+ *                        waypoint lat/lon, then (lat, lon, hdg) per aircraft
+ *                        (sector_cr_env.py:84-208) */
 int32_t bsg_spawn_width(int32_t env_kind, int32_t num_ac);
+
+/* Doubles per env of bsg_buffers.env_geom (0 for kinds without per-env geometry):
+ * StaticObstacle 2 + 10*(6 + 2*16); SectorCR 4 + 2*32. */
+int32_t bsg_geom_width(int32_t env_kind, int32_t num_ac);
 
 /* Replaces: gym.make(id) -> Env.__init__ (merge_env.py:54-101): validates the config
  * and binds a device.  No device memory is allocated. */

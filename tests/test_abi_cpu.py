@@ -48,7 +48,8 @@ def test_shape_helpers_match_reference_spaces():
     assert lib.bsg_spawn_width(nat.ENV_MERGE, 32) == 64
     assert lib.bsg_spawn_width(nat.ENV_VERTICAL_CR, 6) == 22
     for kind, n, k in ((nat.ENV_MERGE, 32, 5), (nat.ENV_VERTICAL_CR, 32, 0), (nat.ENV_DESCENT, 1, 0),
-                       (nat.ENV_HORIZONTAL_CR, 6, 0), (nat.ENV_HORIZONTAL_CR, 32, 0)):
+                       (nat.ENV_HORIZONTAL_CR, 6, 0), (nat.ENV_HORIZONTAL_CR, 32, 0),
+                       (nat.ENV_STATIC_OBSTACLE, 1, 0), (nat.ENV_SECTOR_CR, 32, 4)):
         assert ObsLayout(kind, n, k).dim == lib.bsg_obs_dim(kind, n, k)
 
 

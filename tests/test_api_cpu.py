@@ -25,10 +25,11 @@ def test_register_envs_matches_reference_ids_and_limits():
     for k, v in expect.items():
         assert reg[k].max_episode_steps == v
         assert reg[k].entry_point.startswith("bluesky_gym.envs.")
-    for k in ("MergeEnv-v0", "VerticalCREnv-v0", "DescentEnv-v0", "HorizontalCREnv-v0"):
+    for k in ("MergeEnv-v0", "VerticalCREnv-v0", "DescentEnv-v0", "HorizontalCREnv-v0",
+              "StaticObstacleEnv-v0", "SectorCREnv-v0"):
         assert reg[k].vector_entry_point.startswith("bluesky_gym.vector:")
     with pytest.raises(NotImplementedError):
-        _gym.make("SectorCREnv-v0")
+        _gym.make("PlanWaypointEnv-v0")
 
 
 def test_obs_layout_keys_sorted_like_gymnasium():
@@ -40,6 +41,13 @@ def test_obs_layout_keys_sorted_like_gymnasium():
     assert list(d.keys) == list(ob.DESCENT_OBS_KEYS) and d.dim == 4
     h = ObsLayout(nat.ENV_HORIZONTAL_CR, 6, 0)
     assert list(h.keys) == list(ob.HORIZONTAL_OBS_KEYS) and h.dim == 28
+    from oracle import batched_areas as oba
+    so = ObsLayout(nat.ENV_STATIC_OBSTACLE, 1, 0)
+    assert list(so.keys) == list(oba.STATIC_OBS_KEYS) and so.dim == 43
+    sc = ObsLayout(nat.ENV_SECTOR_CR, 32, 4)
+    assert list(sc.keys) == list(oba.SECTOR_OBS_KEYS) and sc.dim == 31
+    w = ObsLayout(nat.ENV_MERGE, 20, 5, wind=True)
+    assert w.dim == 42 and w.slices["wind_u"] == slice(30, 31)
     space = m.observation_space(_gym.spaces)
     assert list(space.spaces) == sorted(space.spaces)
 
@@ -85,3 +93,19 @@ def test_device_spawn_draws_in_reference_ranges():
     assert tlosh.min() >= 100 and tlosh.max() < 1000
     assert sp[:, -1].min() >= 100 and sp[:, -1].max() < 150
     assert np.array_equal(sp, np.floor(sp))
+
+
+def test_static_host_spawn_consumes_np_random_like_reference():
+    from bluesky_gym import areas
+    g = dict(np.load(f"{GOLD}/static.npz"))
+    np.random.seed(int(g["seed"]))
+    for ep in range(len(g["length"])):
+        assert np.array_equal(areas.static_spawn(), g["spawn"][ep])
+
+
+def test_sector_host_spawn_consumes_np_random_like_reference():
+    from bluesky_gym import areas
+    g = dict(np.load(f"{GOLD}/sector_N32.npz"))
+    np.random.seed(int(g["seed"]))
+    for ep in range(len(g["length"])):
+        assert np.array_equal(areas.sector_spawn(int(g["num_ac"])), g["spawn"][ep])
