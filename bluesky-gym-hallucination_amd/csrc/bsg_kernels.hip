@@ -1135,7 +1135,12 @@ __global__ __launch_bounds__(64) void step_kernel(KParams p) {
       } else {
         load_ac<WIND>(b, a, s);
       }
+#if defined(BSG_EXP_SKIP_OWN) && BSG_EXP_SKIP_OWN
+      // experiment build only (tools/ablate.py): the ownship does not move
+      if (stepping && on && j != 0) {
+#else
       if (stepping && on) {
+#endif
         if (j == 0) {
           if constexpr (KIND == BSG_ENV_MERGE) {
             hdg_spd_action<WIND>(p, s, p.actions[(size_t)e * 2 + 0], p.actions[(size_t)e * 2 + 1],
@@ -1482,6 +1487,11 @@ static hipError_t launch_kind(const KParams& p, hipStream_t st) {
 }
 
 hipError_t launch_step(const KParams& p, hipStream_t st) {
+#if defined(BSG_ONLY_MERGE) && BSG_ONLY_MERGE
+  // experiment builds (tools/flag_sweep.sh): Merge only, for fast compiler-flag sweeps
+  if (p.cfg.env_kind == BSG_ENV_MERGE) return launch_kind<BSG_ENV_MERGE>(p, st);
+  return hipErrorInvalidValue;
+#endif
   switch (p.cfg.env_kind) {
     case BSG_ENV_MERGE: return launch_kind<BSG_ENV_MERGE>(p, st);
     case BSG_ENV_VERTICAL_CR: return launch_kind<BSG_ENV_VERTICAL_CR>(p, st);

@@ -17,6 +17,7 @@ def run(cfg, E, cd, steps=60, warm=10):
     ms, n = b.step_timing()
     return ms / n
 
+only = set(sys.argv[1:])
 res = {}
 for name, cfg, E, cd in [
     ("merge32_full", config.merge_config(num_ac=32), 4096, True),
@@ -30,6 +31,8 @@ for name, cfg, E, cd in [
     ("merge32_full_8192", config.merge_config(num_ac=32), 8192, True),
     ("merge32_full_16384", config.merge_config(num_ac=32), 16384, True),
 ]:
+    if only and name not in only:
+        continue
     res[name] = run(cfg, E, cd)
     print(name, f"{res[name]*1e3:.1f} us", flush=True)
-json.dump(res, open("gpurun_out/ablate.json", "w"), indent=1)
+json.dump(res, open(os.environ.get("ABLATE_OUT", "gpurun_out/ablate.json"), "w"), indent=1)
