@@ -1454,7 +1454,10 @@ __global__ __launch_bounds__(64) void step_kernel(KParams p) {
 #if defined(BSG_STAMPS) && BSG_STAMPS
   BSG_STAMP(5, stamp_clock());
   BSG_STAMP(6, __builtin_amdgcn_s_memrealtime());
-  BSG_STAMP(7, (unsigned long long)__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11)));
+  // XCC id (hwreg 20, bits 3:0) << 32 | HW_ID (hwreg 4: wave 3:0, simd 5:4, cu 11:8, sh 12,
+  // se 15:13)
+  BSG_STAMP(7, ((unsigned long long)__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11)) << 32) |
+                   (unsigned long long)__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11)));
 #endif
 }
 

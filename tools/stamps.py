@@ -29,11 +29,36 @@ for k in range(30):
     b.step(act[k % 8])
 torch.cuda.synchronize()
 recs = []
+feats = []
+FIX = (config.FIX_LAT, config.FIX_LON)
 for k in range(5):
     st.zero_()
+    pre = {f: b.state[f].cpu().numpy().copy() for f in ("lat", "lon", "hdg", "tas", "nav", "alt")}
+    flags = b.envs["flags"].cpu().numpy().copy()
     b.step(act[k % 8])
     torch.cuda.synchronize()
     recs.append(st.cpu().numpy().astype(np.uint64))
+    post = {f: b.state[f].cpu().numpy() for f in ("lat", "lon", "hdg", "tas", "nav")}
+    # per-lane features of this step, folded per wave (64/gs envs per wave)
+    wp = np.where(((pre["nav"] >> 8) & 255) == 0, FIX[0], config.RWY_LAT)
+    wpn = np.where(((pre["nav"] >> 8) & 255) == 0, FIX[1], config.RWY_LON)
+    dlat = np.radians(wp - pre["lat"]); dlon = np.radians(wpn - pre["lon"])
+    dkm = 6371.0 * np.sqrt(dlat ** 2 + (dlon * np.cos(np.radians(pre["lat"]))) ** 2)
+    lnav = (pre["nav"] & 1) == 1
+    near = lnav & (dkm < 40.0)
+    switched = ((post["nav"] >> 8) & 255) != ((pre["nav"] >> 8) & 255)
+    lnav_off = lnav & ((post["nav"] & 1) == 0)
+    dh = np.abs(((post["hdg"] - pre["hdg"] + 180) % 360) - 180)
+    turning = dh > 1.0
+    spd = np.abs(post["tas"] - pre["tas"]) > 1e-9
+    epw = 64 // gs
+    def per_wave(x):
+        x = np.asarray(x, np.float64).reshape(-1, N).sum(1)
+        pad = (-len(x)) % epw
+        return np.concatenate([x, np.zeros(pad)]).reshape(-1, epw).sum(1)
+    feats.append(np.stack([per_wave(near), per_wave(switched | lnav_off), per_wave(turning),
+                           per_wave(spd), per_wave(np.repeat(flags & 1, N).reshape(-1, N)),
+                           per_wave(lnav)], 1))
 r = np.concatenate(recs)
 rt0 = r[:, 0].astype(np.int64); rt1 = r[:, 6].astype(np.int64)
 c1 = r[:, 1].astype(np.int64); c2 = r[:, 2].astype(np.int64); c3 = r[:, 3].astype(np.int64)
@@ -52,5 +77,39 @@ print("CD phase1 cyc       ", pct(c4 - c3))
 print("CD phase2+out cyc   ", pct(c5 - c4))
 print("candidates/wave     ", pct(tot))
 print("total cycles        ", pct(c5 - c1))
-hw = r[:, 7].astype(np.int64)
-print("xcc ids seen", np.unique(hw)[:16])
+F = np.concatenate(feats)
+A = (c2 - c1).astype(np.float64)
+names = ["lanes near wp (<40km)", "lanes wp switch/off", "lanes turning >1deg", "lanes speed change",
+         "lanes resetting", "lanes LNAV"]
+print("phase-A cycles vs per-wave features (Pearson r, mean of feature, A p50 for feature==0 / >0):")
+for i, nm in enumerate(names):
+    x = F[:, i]
+    r_ = np.corrcoef(x, A)[0, 1] if x.std() > 0 else float("nan")
+    a0 = np.median(A[x == 0]) if (x == 0).any() else float("nan")
+    a1 = np.median(A[x > 0]) if (x > 0).any() else float("nan")
+    print(f"  {nm:24s} r={r_:+.2f} mean={x.mean():6.2f}  A|0={a0:9.0f}  A|>0={a1:9.0f}")
+hw = r[:, 7].astype(np.uint64)
+xcc = (hw >> np.uint64(32)).astype(np.int64)
+hid = (hw & np.uint64(0xFFFFFFFF)).astype(np.int64)
+simd = (hid >> 4) & 3
+cu = (hid >> 8) & 15
+sh = (hid >> 12) & 1
+se = (hid >> 13) & 7
+print("xcc ids seen", np.unique(xcc)[:16])
+life = (rt1 - rt0) * 10 / 1000
+tot_c = c5 - c1
+for run in range(5):
+    s = slice(run * grid, (run + 1) * grid)
+    key = (((xcc[s] * 8 + se[s]) * 2 + sh[s]) * 16 + cu[s]) * 4 + simd[s]
+    cuk = key // 4
+    uk, inv, cnt = np.unique(key, return_inverse=True, return_counts=True)
+    per_wave = cnt[inv]
+    ucu, cinv, ccnt = np.unique(cuk, return_inverse=True, return_counts=True)
+    print(f"run {run}: {len(uk)} SIMDs used, waves/SIMD histogram",
+          dict(zip(*np.unique(cnt, return_counts=True))), f"; {len(ucu)} CUs, waves/CU",
+          dict(zip(*np.unique(ccnt, return_counts=True))))
+    for w in sorted(set(per_wave.tolist())):
+        sel = per_wave == w
+        print(f"   waves sharing a SIMD={w}: n={sel.sum():5d}  life us p50 {np.median(life[s][sel]):6.1f} "
+              f"max {life[s][sel].max():6.1f}   cycles p50 {np.median(tot_c[s][sel]):8.0f} "
+              f"max {tot_c[s][sel].max():8.0f}")
