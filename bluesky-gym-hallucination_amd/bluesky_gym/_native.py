@@ -60,7 +60,7 @@ class BsgConfig(C.Structure):
 BUFFER_FIELDS = [
     ("lat", _dp), ("lon", _dp), ("alt", _dp), ("hdg", _dp), ("tas", _dp), ("cas", _dp),
     ("vs", _dp), ("ax", _dp), ("ap_trk", _dp), ("selspd", _dp), ("selalt", _dp),
-    ("selvs", _dp), ("nav", _i32p), ("gs", _dp), ("trk", _dp),
+    ("selvs", _dp), ("nav", _i32p), ("gs", _dp), ("trk", _dp), ("memo_cache", _dp),
     ("step_count", _i32p), ("flags", _i32p), ("episode", _u32p), ("wpt_reach", _i32p),
     ("faf_reached", _i32p), ("total_intrusions", _i32p), ("total_reward", _dp),
     ("drift_sum", _dp), ("target_alt", _dp), ("final_altitude", _dp),

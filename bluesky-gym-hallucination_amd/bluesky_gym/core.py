@@ -19,7 +19,8 @@ F64_ENV = ("total_reward", "drift_sum", "target_alt", "final_altitude")
 
 class DeviceBatch:
     def __init__(self, cfg: EnvKindConfig, num_envs: int, *, autoreset=nat.AUTORESET_NEXT_STEP,
-                 compute_cd=True, seed=0, device=None, learner=False, env_offset=0):
+                 compute_cd=True, seed=0, device=None, learner=False, env_offset=0,
+                 memo_cache=True):
         if not torch.cuda.is_available():
             raise nat.BsgError("bluesky_gym needs a HIP device (MI355X); none is visible")
         self.lib = nat.load_library()
@@ -31,6 +32,7 @@ class DeviceBatch:
                                    else torch.device(device).index or 0)
         self.autoreset = autoreset
         self.want_learner = bool(learner)
+        self.want_memo = bool(memo_cache)
         self.compute_cd = bool(compute_cd) and cfg.kind not in (nat.ENV_DESCENT,
                                                                  nat.ENV_STATIC_OBSTACLE)
         self.obs_dim = self.lib.bsg_obs_dim(cfg.kind, cfg.num_ac, cfg.num_ac_state)
@@ -55,6 +57,9 @@ class DeviceBatch:
         z = lambda shape, dt: torch.zeros(shape, dtype=dt, device=d)
         self.state = {k: z((E, N), torch.float64) for k in F64_STATE}
         self.state["nav"] = z((E, N), torch.int32)
+        # cross-step memo of the speed schedule (csrc: memo_load/memo_store); NaN = no entry
+        self.memo_cache = torch.full((7, E, N), float("nan"), dtype=torch.float64, device=d) \
+            if self.want_memo else None
         self.envs = {k: z((E,), torch.int32) for k in I32_ENV}
         self.envs["episode"] = z((E,), torch.int32)     # uint32 on the device side
         self.envs.update({k: z((E,), torch.float64) for k in F64_ENV})
@@ -123,6 +128,7 @@ class DeviceBatch:
         b = nat.BsgBuffers()
         src = dict(self.state)
         src.update(self.envs)
+        src.update(memo_cache=self.memo_cache)
         src.update(obs=self.obs, final_obs=self.final_obs, reward=self.reward,
                    terminated=self.terminated, truncated=self.truncated, topk=self.topk,
                    intr_mask=self.intr_mask, conf_mask=self.conf_mask, los_mask=self.los_mask,

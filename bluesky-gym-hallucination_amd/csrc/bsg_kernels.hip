@@ -197,9 +197,20 @@ struct Memo {
   double coslat, sinlat;           // cos/sin(lat * D2R) of the current latitude
   uint64_t tr_bits;                // key of turnrate = deg(g0*tan(bank)/max(tas, eps))
   double turnrate;
+  double last_alt;                 // altitude at the start of the latest substep
+  uint64_t cas_tas_bits, cas_alt_bits;  // key of the stored cas = vtas2cas(tas, alt)
 };
 
 constexpr uint64_t kNoKey = 0x7ff8dead0000beefull;   // a NaN payload no input produces
+
+// Cross-step memo (bsg_buffers.memo_cache, SoA [MC_FIELDS][E*N]): the pure functions of an
+// aircraft's (selspd, alt, selalt) and the key of its stored cas survive the launch, so an
+// aircraft in steady flight evaluates no pow/exp at all -- not even in the first substep.
+// Keys are bit patterns stored as doubles (NaN payloads pass through memory unchanged).
+constexpr int MC_FIELDS = 7;
+enum { MC_SPD_SEL = 0, MC_SPD_ALT, MC_AP_TAS, MC_LIM_H, MC_ALLOW_TAS, MC_CAS_TAS, MC_CAS_ALT };
+
+__device__ __forceinline__ double key_as_double(uint64_t k) { return __longlong_as_double((long long)k); }
 
 __device__ __forceinline__ void memo_init(Memo& m, const AC& s) {
   m.alt_bits = kNoKey; m.spd_bits = kNoKey; m.spdalt_bits = kNoKey;
@@ -207,7 +218,53 @@ __device__ __forceinline__ void memo_init(Memo& m, const AC& s) {
   m.at = Atmos{0, 0, 0}; m.ap_tas = 0; m.allow_tas = 0;
   m.wp_k = -1; m.wp_lat = 0; m.wp_lon = 0; m.wp_nq = 0; m.wp_cos = 0; m.wp_sin = 0;
   m.tr_bits = kNoKey; m.turnrate = 0;
+  m.last_alt = s.alt;
+  m.cas_tas_bits = kNoKey; m.cas_alt_bits = kNoKey;
   sincos(s.lat * kD2R, &m.sinlat, &m.coslat);
+}
+
+__device__ __forceinline__ void memo_load(Memo& m, const double* mc, size_t a, size_t stride) {
+  m.spd_bits = bits(mc[MC_SPD_SEL * stride + a]);
+  m.spdalt_bits = bits(mc[MC_SPD_ALT * stride + a]);
+  m.ap_tas = mc[MC_AP_TAS * stride + a];
+  m.lim_tas_bits = bits(m.ap_tas);
+  m.lim_h_bits = bits(mc[MC_LIM_H * stride + a]);
+  m.allow_tas = mc[MC_ALLOW_TAS * stride + a];
+  m.cas_tas_bits = bits(mc[MC_CAS_TAS * stride + a]);
+  m.cas_alt_bits = bits(mc[MC_CAS_ALT * stride + a]);
+}
+
+// write back only the entries that changed (steady aircraft write nothing)
+__device__ __forceinline__ void memo_store(const Memo& m, double* mc, size_t a, size_t stride) {
+  const double v[MC_FIELDS] = {key_as_double(m.spd_bits), key_as_double(m.spdalt_bits), m.ap_tas,
+                               key_as_double(m.lim_h_bits), m.allow_tas,
+                               key_as_double(m.cas_tas_bits), key_as_double(m.cas_alt_bits)};
+#pragma unroll
+  for (int f = 0; f < MC_FIELDS; ++f) {
+    double* q = mc + f * stride + a;
+    if (bits(*q) != bits(v[f])) *q = v[f];
+  }
+}
+
+__device__ __forceinline__ void memo_invalidate(double* mc, size_t a, size_t stride) {
+#pragma unroll
+  for (int f = 0; f < MC_FIELDS; ++f) mc[f * stride + a] = key_as_double(kNoKey);
+}
+
+// the atmosphere at the current altitude, evaluated only when a memo entry needs it
+__device__ __forceinline__ const Atmos& memo_at(Memo& m, double alt, uint64_t ab) {
+  if (ab != m.alt_bits) { m.at = vatmos(alt); m.alt_bits = ab; }
+  return m.at;
+}
+
+// update_airspeed's cas = vtas2cas(tas, alt) of the LAST substep (its alt is the one
+// before that substep's update_pos); skipped when (tas, alt) equal the stored cas's key
+__device__ __forceinline__ void memo_final_cas(Memo& m, AC& s) {
+  const uint64_t tb = bits(s.tas), lb = bits(m.last_alt);
+  if (tb == m.cas_tas_bits && lb == m.cas_alt_bits) return;
+  s.cas = tas2cas_at(s.tas, memo_at(m, m.last_alt, lb));
+  m.cas_tas_bits = tb;
+  m.cas_alt_bits = lb;
 }
 
 __device__ __forceinline__ void memo_wp(Memo& m, const RouteRegs& rt, int k) {
@@ -274,9 +331,9 @@ __device__ __forceinline__ void substep(AC& s, Memo& m, double dt, const RouteRe
   const double ap_vs = fabs(s.selvs) > 0.1 ? s.selvs : APVSDEF;
   const double ap_alt = s.selalt;
   const uint64_t ab = bits(s.alt);
-  if (ab != m.alt_bits) { m.at = vatmos(s.alt); m.alt_bits = ab; }
+  m.last_alt = s.alt;
   if (bits(s.selspd) != m.spd_bits || ab != m.spdalt_bits) {
-    m.ap_tas = casormach2tas_at(s.selspd, m.at);
+    m.ap_tas = casormach2tas_at(s.selspd, memo_at(m, s.alt, ab));
     m.spd_bits = bits(s.selspd);
     m.spdalt_bits = ab;
   }
@@ -297,7 +354,7 @@ __device__ __forceinline__ void substep(AC& s, Memo& m, double dt, const RouteRe
   const double allow_h = ap_alt > HMAX ? HMAX : ap_alt;
   const uint64_t hb = bits(allow_h);
   if (bits(m.ap_tas) != m.lim_tas_bits || hb != m.lim_h_bits) {
-    const Atmos ah = (hb == ab) ? m.at : vatmos(allow_h);
+    const Atmos ah = (hb == ab) ? memo_at(m, s.alt, ab) : vatmos(allow_h);
     const double intent_cas = tas2cas_at(m.ap_tas, ah);
     double allow_cas = intent_cas < VMIN_CAS ? VMIN_CAS : intent_cas;
     allow_cas = intent_cas > VMAX_CAS ? VMAX_CAS : allow_cas;
@@ -1075,6 +1132,67 @@ __device__ __forceinline__ void hdg_spd_action(const KParams& p, AC& s, double a
   s.selspd = speed_new >= 1.0 ? speed_new * KTS : speed_new;
 }
 
+// One RL step of aircraft (e, j) whose state is in s: the ownship's action decode (j == 0),
+// ACTION_FREQUENCY substeps with the cross-step memo, the deferred cas.  StaticObstacle also
+// evaluates its per-substep reward here (sub_reward / sub_done).
+template <int KIND, bool WIND>
+__device__ __forceinline__ void propagate(const KParams& p, int e, int j, size_t a, AC& s,
+                                          EnvScalars& ev, double& sub_reward, bool& sub_done) {
+  const Buffers& b = p.b;
+  const int N = p.N;
+  if (j == 0) {
+    if constexpr (KIND == BSG_ENV_MERGE) {
+      hdg_spd_action<WIND>(p, s, p.actions[(size_t)e * 2 + 0], p.actions[(size_t)e * 2 + 1],
+                           15.0, 20.0);
+    } else if constexpr (KIND == BSG_ENV_STATIC_OBSTACLE) {
+      hdg_spd_action<WIND>(p, s, p.actions[(size_t)e * 2 + 0], p.actions[(size_t)e * 2 + 1],
+                           45.0, 20.0 / 3.0);
+    } else if constexpr (KIND == BSG_ENV_SECTOR_CR) {
+      hdg_spd_action<WIND>(p, s, p.actions[(size_t)e * 2 + 0], p.actions[(size_t)e * 2 + 1],
+                           22.5, 20.0 / 3.0);
+    } else if constexpr (KIND == BSG_ENV_HORIZONTAL_CR) {
+      // horizontal_cr_env.py:272-275: HDG KL001 {hdg + a*45} (no wrap)
+      s.ap_trk = hdg_command_track<WIND>(p.wind, s, s.hdg + p.actions[e] * 45);
+      s.nav &= ~1;
+    } else {
+      // vertical_cr_env.py:242-256 / descent_env.py:146-160
+      const double act = p.actions[e] * 12.5;
+      if (act >= 0) { s.selalt = 1000000; s.selvs = act; }
+      else if (act < 0) { s.selalt = 0; s.selvs = act; }
+    }
+  }
+  const int S = p.cfg.action_frequency;
+  if (S > 0) {
+    Memo m;
+    memo_init(m, s);
+    if (b.memo_cache) memo_load(m, b.memo_cache, a, (size_t)p.E * N);
+    RouteRegs rt;
+    rt.load(p.route);
+    const double dt = p.cfg.simdt;
+    if constexpr (KIND == BSG_ENV_STATIC_OBSTACLE) {
+      // static_obstacle_env.py:132-150: _get_reward after every substep, with the
+      // waypoint distance and drift of the previous observation; stop when done
+      const double* geo = b.env_geom + (size_t)e * SO_GEOM;
+      for (int it = 0; it < S; ++it) {
+        substep<WIND>(s, m, dt, rt, p.wind);
+        int reach = 0;
+        if (ev.aux[0] < 5 && ev.wpt_reach != 1) { ev.wpt_reach = 1; reach = 1; }
+        const double dd = fabs(ev.aux[1] * kD2R);
+        ev.drift_sum += dd;
+        ev.aux[2] += 1.0;
+        const int nin = static_inside_count(geo, s.lat, s.lon);
+        if (nin > 0) ev.aux[3] = 1.0;
+        sub_reward = ((double)reach + dd * -0.01) + (double)(nin * -5);
+        if (ev.wpt_reach == 1 || nin > 0) { sub_done = true; break; }
+      }
+    } else {
+      for (int it = 0; it < S; ++it) substep<WIND>(s, m, dt, rt, p.wind);
+    }
+    memo_final_cas(m, s);
+    if (b.memo_cache) memo_store(m, b.memo_cache, a, (size_t)p.E * N);
+  }
+}
+
 template <int KIND, int GS, bool WIND>
 __global__ __launch_bounds__(64) void step_kernel(KParams p) {
 #if defined(BSG_STAMPS) && BSG_STAMPS
@@ -1137,63 +1255,12 @@ __global__ __launch_bounds__(64) void step_kernel(KParams p) {
       }
 #if defined(BSG_EXP_SKIP_OWN) && BSG_EXP_SKIP_OWN
       // experiment build only (tools/ablate.py): the ownship does not move
-      if (stepping && on && j != 0) {
+      if (stepping && on && j != 0) propagate<KIND, WIND>(p, e, j, a, s, ev, sub_reward, sub_done);
 #else
-      if (stepping && on) {
+      if (stepping && on) propagate<KIND, WIND>(p, e, j, a, s, ev, sub_reward, sub_done);
 #endif
-        if (j == 0) {
-          if constexpr (KIND == BSG_ENV_MERGE) {
-            hdg_spd_action<WIND>(p, s, p.actions[(size_t)e * 2 + 0], p.actions[(size_t)e * 2 + 1],
-                                 15.0, 20.0);
-          } else if constexpr (KIND == BSG_ENV_STATIC_OBSTACLE) {
-            hdg_spd_action<WIND>(p, s, p.actions[(size_t)e * 2 + 0], p.actions[(size_t)e * 2 + 1],
-                                 45.0, 20.0 / 3.0);
-          } else if constexpr (KIND == BSG_ENV_SECTOR_CR) {
-            hdg_spd_action<WIND>(p, s, p.actions[(size_t)e * 2 + 0], p.actions[(size_t)e * 2 + 1],
-                                 22.5, 20.0 / 3.0);
-          } else if constexpr (KIND == BSG_ENV_HORIZONTAL_CR) {
-            // horizontal_cr_env.py:272-275: HDG KL001 {hdg + a*45} (no wrap)
-            s.ap_trk = hdg_command_track<WIND>(p.wind, s, s.hdg + p.actions[e] * 45);
-            s.nav &= ~1;
-          } else {
-            // vertical_cr_env.py:242-256 / descent_env.py:146-160
-            const double act = p.actions[e] * 12.5;
-            if (act >= 0) { s.selalt = 1000000; s.selvs = act; }
-            else if (act < 0) { s.selalt = 0; s.selvs = act; }
-          }
-        }
-        const int S = p.cfg.action_frequency;
-        if (S > 0) {
-          Memo m;
-          memo_init(m, s);
-          RouteRegs rt;
-          rt.load(p.route);
-          const double dt = p.cfg.simdt;
-          if constexpr (KIND == BSG_ENV_STATIC_OBSTACLE) {
-            // static_obstacle_env.py:132-150: _get_reward after every substep, with the
-            // waypoint distance and drift of the previous observation; stop when done
-            const double* geo = b.env_geom + (size_t)e * SO_GEOM;
-            for (int it = 0; it < S; ++it) {
-              substep<WIND>(s, m, dt, rt, p.wind);
-              int reach = 0;
-              if (ev.aux[0] < 5 && ev.wpt_reach != 1) { ev.wpt_reach = 1; reach = 1; }
-              const double dd = fabs(ev.aux[1] * kD2R);
-              ev.drift_sum += dd;
-              ev.aux[2] += 1.0;
-              const int nin = static_inside_count(geo, s.lat, s.lon);
-              if (nin > 0) ev.aux[3] = 1.0;
-              sub_reward = ((double)reach + dd * -0.01) + (double)(nin * -5);
-              if (ev.wpt_reach == 1 || nin > 0) { sub_done = true; break; }
-            }
-          } else {
-            for (int it = 0; it < S; ++it) substep<WIND>(s, m, dt, rt, p.wind);
-          }
-          // update_airspeed's cas = vtas2cas(tas, alt) of the LAST substep (its alt is the
-          // one before that substep's update_pos, i.e. m.at's key)
-          s.cas = tas2cas_at(s.tas, m.at);
-        }
-      }
       if (active) store_ac<WIND>(b, a, s);
+      if (resetting && b.memo_cache) memo_invalidate(b.memo_cache, a, (size_t)p.E * N);
     }
     if (resetting && j == 0) reset_scalars<KIND>(ev, aux);
     stage(L, lane, s);
@@ -1417,6 +1484,7 @@ __global__ __launch_bounds__(64) void step_kernel(KParams p) {
       if (same_step_reset && ok) {
         spawn<KIND>(p, e, j, ev.episode, s, aux);
         store_ac<WIND>(b, a, s);
+        if (b.memo_cache) memo_invalidate(b.memo_cache, a, (size_t)p.E * N);
       }
       if (same_step_reset && j == 0) reset_scalars<KIND>(ev, aux);
       if (same_step_reset) stage(L, lane, s);

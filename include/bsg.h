@@ -85,6 +85,10 @@ typedef struct bsg_buffers {
   double *gs, *trk;          /* ground speed / track (bs.traf.gs, .trk); required only while
                                 a wind field is set (bsg_set_wind) -- without wind gs = tas
                                 and trk = hdg, and these may be NULL */
+  double *memo_cache;        /* optional [7][E*N] scratch owned by the caller, initialised to
+                                NaN: cross-step memo of the pure per-aircraft speed-schedule
+                                functions (exact: entries are keyed by input bit patterns);
+                                NULL disables it */
   /* ---- per-env state [E] ----------------------------------------------------------- */
   int32_t *step_count;       /* TimeLimit elapsed steps */
   int32_t *flags;            /* bit0: reset pending (NEXT_STEP autoreset) */

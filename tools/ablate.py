@@ -5,7 +5,8 @@ import torch
 from bluesky_gym import core, config
 
 def run(cfg, E, cd, steps=60, warm=10):
-    b = core.DeviceBatch(cfg, E, compute_cd=cd, seed=1)
+    b = core.DeviceBatch(cfg, E, compute_cd=cd, seed=1,
+                         memo_cache=os.environ.get("BSG_NO_MEMO", "0") != "1")
     b.reset()
     act = torch.rand((8, E, b.act_dim), dtype=torch.float64, device="cuda") * 2 - 1
     for k in range(warm):
@@ -28,6 +29,7 @@ for name, cfg, E, cd in [
     ("merge16_full_1024", config.merge_config(num_ac=16), 1024, True),
     ("vert32_full_2048", config.vertical_config(num_intruders=31), 2048, True),
     ("descent_4096", config.descent_config(), 4096, False),
+    ("horiz32_full_4096", config.horizontal_config(num_intruders=31), 4096, True),
     ("merge32_full_8192", config.merge_config(num_ac=32), 8192, True),
     ("merge32_full_16384", config.merge_config(num_ac=32), 16384, True),
 ]:
