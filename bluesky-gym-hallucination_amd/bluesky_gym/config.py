@@ -126,3 +126,8 @@ def sector_config(num_ac=32, action_frequency=5, simdt=1.0, max_episode_steps=20
 
 def descent_config(action_frequency=30, simdt=1.0, max_episode_steps=300):
     return EnvKindConfig(nat.ENV_DESCENT, 1, 0, action_frequency, simdt, max_episode_steps)
+
+
+def plan_waypoint_config(action_frequency=10, simdt=1.0, max_episode_steps=300):
+    """plan_waypoint_env.py:21 ACTION_FREQUENCY, :72 'DT 1', bluesky_gym/__init__.py:15."""
+    return EnvKindConfig(nat.ENV_PLAN_WAYPOINT, 1, 0, action_frequency, simdt, max_episode_steps)

@@ -33,8 +33,7 @@ class DeviceBatch:
         self.autoreset = autoreset
         self.want_learner = bool(learner)
         self.want_memo = bool(memo_cache)
-        self.compute_cd = bool(compute_cd) and cfg.kind not in (nat.ENV_DESCENT,
-                                                                 nat.ENV_STATIC_OBSTACLE)
+        self.compute_cd = bool(compute_cd) and cfg.num_ac > 1   # single-aircraft kinds: no CD
         self.obs_dim = self.lib.bsg_obs_dim(cfg.kind, cfg.num_ac, cfg.num_ac_state)
         if self.obs_dim < 0:
             raise nat.BsgError(f"invalid env config {cfg}")

@@ -5,4 +5,4 @@ from .vertical_cr_env import VerticalCREnv  # noqa: F401
 from .horizontal_cr_env import HorizontalCREnv  # noqa: F401
 from .sector_cr_env import SectorCREnv  # noqa: F401
 from .static_obstacle_env import StaticObstacleEnv  # noqa: F401
-from ._out_of_scope import PlanWaypointEnv  # noqa: F401
+from .plan_waypoint_env import PlanWaypointEnv  # noqa: F401

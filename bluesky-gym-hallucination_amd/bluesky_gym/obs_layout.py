@@ -2,7 +2,8 @@
 flat (sorted-key) offsets the HIP kernel writes.
 
 merge_env.py:59-74, vertical_cr_env.py:67-83, descent_env.py:53-60,
-horizontal_cr_env.py:49-60.  Gymnasium's
+horizontal_cr_env.py:49-60, static_obstacle_env.py:61-71, sector_cr_env.py:53-66,
+plan_waypoint_env.py:50-56.  Gymnasium's
 spaces.Dict sorts its keys, and SB3's MultiInputPolicy flattens in that order, so the
 flat fp32 row of libbsg is laid out in sorted-key order.
 """
@@ -44,6 +45,11 @@ def sector_sizes(k=4):
             "sin(track)": k, "vx_r": k, "vy_r": k, "x_r": k, "y_r": k}
 
 
+def plan_sizes(nw=5):
+    return {"cos_difference": nw, "sin_difference": nw, "waypoint_distance": nw,
+            "waypoint_reached": nw}
+
+
 def descent_sizes():
     return {"altitude": 1, "runway_distance": 1, "target_altitude": 1, "vz": 1}
 
@@ -51,7 +57,8 @@ def descent_sizes():
 # reference Box bounds (low, high) per key
 _BOUNDS = {"cos(drift)": (-1, 1), "sin(drift)": (-1, 1), "faf_reached": (0, 1)}
 _KIND_BOUNDS = {nat.ENV_SECTOR_CR: {"airspeed": (-1, 1)},
-                nat.ENV_STATIC_OBSTACLE: {"restricted_area_radius": (0, 1)}}
+                nat.ENV_STATIC_OBSTACLE: {"restricted_area_radius": (0, 1)},
+                nat.ENV_PLAN_WAYPOINT: {"waypoint_reached": (0, 1)}}
 
 
 WIND_KEYS = ("wind_u", "wind_v")     # bluesky_gym/wrappers/wind.py:21-22
@@ -77,6 +84,8 @@ REF_ORDER = {
                               "sin_difference_restricted_area_pos"),
     nat.ENV_SECTOR_CR: ("cos(drift)", "sin(drift)", "airspeed", "x_r", "y_r", "vx_r", "vy_r",
                         "cos(track)", "sin(track)", "distances"),
+    nat.ENV_PLAN_WAYPOINT: ("waypoint_distance", "cos_difference", "sin_difference",
+                            "waypoint_reached"),
 }
 
 
@@ -92,6 +101,8 @@ class ObsLayout:
             sizes = static_sizes()
         elif kind == nat.ENV_SECTOR_CR:
             sizes = sector_sizes(num_ac_state)
+        elif kind == nat.ENV_PLAN_WAYPOINT:
+            sizes = plan_sizes()
         else:
             sizes = descent_sizes()
         if wind:

@@ -82,6 +82,17 @@ def horizontal_spawn(num_intruders, rs=None):
     return np.array(out, np.float64)
 
 
+def plan_spawn(rs=None):
+    """np.random draws of plan_waypoint_env.py:205-206, per waypoint (distance km, bearing
+    deg) -> [dis0..4, hdg0..4] (the PlanWaypoint spawn row, bsg.h bsg_spawn_width)."""
+    rs = np.random if rs is None else rs
+    d, h = [], []
+    for _ in range(5):
+        d.append(float(rs.randint(0, 75)))
+        h.append(float(rs.randint(0, 359)))
+    return np.array(d + h, np.float64)
+
+
 def descent_spawn(rs=None):
     rs = np.random if rs is None else rs
     alt_init = rs.randint(ALT_MIN, ALT_MAX)

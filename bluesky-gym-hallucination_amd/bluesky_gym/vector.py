@@ -1,6 +1,6 @@
 """Gymnasium VectorEnv front-ends of the device batch (the ``vector_entry_point`` of
 MergeEnv-v0 / VerticalCREnv-v0 / DescentEnv-v0 / HorizontalCREnv-v0 / StaticObstacleEnv-v0 /
-SectorCREnv-v0, registered by ``register_envs``).
+SectorCREnv-v0 / PlanWaypointEnv-v0, registered by ``register_envs``).
 
 ``gym.make_vec("MergeEnv-v0", num_envs=4096, vectorization_mode="vector_entry_point",
 num_ac=32)`` returns a :class:`MergeVectorEnv` whose E envs live on one HIP device and
@@ -27,6 +27,7 @@ _INFO_KEYS = {
     nat.ENV_HORIZONTAL_CR: ("total_reward", "total_intrusions", "average_drift"),
     nat.ENV_STATIC_OBSTACLE: ("total_reward", "waypoint_reached", "crashed", "average_drift"),
     nat.ENV_SECTOR_CR: ("total_reward", "total_intrusions", "average_drift"),
+    nat.ENV_PLAN_WAYPOINT: ("total_reward", "waypoints_completed"),
 }
 
 
@@ -96,6 +97,8 @@ class BlueSkyVectorEnv(_gym.VectorEnv):
             elif k.kind == nat.ENV_SECTOR_CR:
                 rows.append(areas.sector_spawn(k.num_ac, rs,
                                                "normal" if k.kind_option == 0 else "uniform"))
+            elif k.kind == nat.ENV_PLAN_WAYPOINT:
+                rows.append(spawnmod.plan_spawn(rs))
             else:
                 rows.append(spawnmod.descent_spawn(rs))
         return torch.from_numpy(np.stack(rows))
@@ -163,6 +166,10 @@ class BlueSkyVectorEnv(_gym.VectorEnv):
                 avg = b.envs["drift_sum"].cpu().numpy() / cnt
             out = {"total_reward": tr, "total_intrusions": b.envs["total_intrusions"].cpu().numpy(),
                    "average_drift": np.where(cnt > 0, avg, np.nan)}
+        elif kind == nat.ENV_PLAN_WAYPOINT:
+            wr = b.envs["wpt_reach"].cpu().numpy()
+            done_cnt = sum((wr >> k) & 1 for k in range(5))
+            out = {"total_reward": tr, "waypoints_completed": done_cnt.astype(np.int32)}
         else:
             out = {"total_reward": tr, "final_altitude": b.envs["final_altitude"].cpu().numpy()}
         if b.compute_cd:
@@ -218,4 +225,15 @@ class DescentVectorEnv(BlueSkyVectorEnv):
     def __init__(self, num_envs=1, action_frequency=30, simdt=1.0, max_episode_steps=300, **kw):
         kw.pop("compute_cd", None)
         super().__init__(cfgmod.descent_config(action_frequency, simdt, max_episode_steps or 0),
+                         num_envs, compute_cd=False, **kw)
+
+
+class PlanWaypointVectorEnv(BlueSkyVectorEnv):
+    """PlanWaypointEnv-v0 (plan_waypoint_env.py): five waypoints per episode around the
+    ownship; like the reference, a reset after a truncation keeps the aircraft where it is
+    (bsg.h BSG_FLAG_AC_PRESENT)."""
+
+    def __init__(self, num_envs=1, action_frequency=10, simdt=1.0, max_episode_steps=300, **kw):
+        kw.pop("compute_cd", None)
+        super().__init__(cfgmod.plan_waypoint_config(action_frequency, simdt, max_episode_steps or 0),
                          num_envs, compute_cd=False, **kw)

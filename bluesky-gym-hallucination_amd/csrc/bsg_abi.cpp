@@ -69,6 +69,7 @@ int wind_obs_pos(const bsg_config& cfg) {
     case BSG_ENV_HORIZONTAL_CR: return 3 * NI + 3; // ... waypoint_distance | x_/y_...
     case BSG_ENV_STATIC_OBSTACLE: return 3 + 4 * bsg::SO_NOBST;  // all keys sort before "wind"
     case BSG_ENV_SECTOR_CR: return 3 + 5 * K;      // ... vx_r, vy_r | x_r, y_r
+    case BSG_ENV_PLAN_WAYPOINT: return 4 * bsg::PW_NWPT;  // ... waypoint_reached | (end)
     default: return 0;
   }
 }
@@ -130,6 +131,7 @@ int32_t bsg_obs_dim(int32_t kind, int32_t num_ac, int32_t k) {
     case BSG_ENV_STATIC_OBSTACLE: return num_ac == 1 ? 3 + 4 * bsg::SO_NOBST : BSG_E_INVALID_ARG;
     case BSG_ENV_SECTOR_CR:        // at least NUM_AC_STATE + 1 aircraft (sector_cr_env.py:97)
       return (num_ac >= 5 && k >= 1 && k <= 4) ? 3 + 7 * k : BSG_E_INVALID_ARG;
+    case BSG_ENV_PLAN_WAYPOINT: return num_ac == 1 ? 4 * bsg::PW_NWPT : BSG_E_INVALID_ARG;
     default: return BSG_E_INVALID_ARG;
   }
 }
@@ -141,7 +143,8 @@ int32_t bsg_action_dim(int32_t kind) {
     case BSG_ENV_SECTOR_CR: return 2;
     case BSG_ENV_VERTICAL_CR:
     case BSG_ENV_DESCENT:
-    case BSG_ENV_HORIZONTAL_CR: return 1;
+    case BSG_ENV_HORIZONTAL_CR:
+    case BSG_ENV_PLAN_WAYPOINT: return 1;
     default: return BSG_E_INVALID_ARG;
   }
 }
@@ -154,6 +157,7 @@ int32_t bsg_spawn_width(int32_t kind, int32_t num_ac) {
     case BSG_ENV_HORIZONTAL_CR: return 3 * (num_ac - 1) + 1;
     case BSG_ENV_STATIC_OBSTACLE: return bsg::SO_SPAWN_W;
     case BSG_ENV_SECTOR_CR: return 4 + 2 * bsg::SC_VMAX + 3 * num_ac;
+    case BSG_ENV_PLAN_WAYPOINT: return 2 * bsg::PW_NWPT;
     default: return BSG_E_INVALID_ARG;
   }
 }
@@ -163,6 +167,7 @@ int32_t bsg_geom_width(int32_t kind, int32_t num_ac) {
   switch (kind) {
     case BSG_ENV_STATIC_OBSTACLE: return bsg::SO_GEOM;
     case BSG_ENV_SECTOR_CR: return bsg::SC_GEOM;
+    case BSG_ENV_PLAN_WAYPOINT: return bsg::PW_GEOM;
     default: return 0;
   }
 }
@@ -232,9 +237,8 @@ int32_t bsg_bind(bsg_ctx* c, const bsg_buffers* b) {
     if (!required[i]) return fail(BSG_E_INVALID_ARG, "bsg_bind: required buffer #%s%lld is NULL", "", (long long)i);
   if (c->cfg.env_kind == BSG_ENV_HORIZONTAL_CR && (!b->env_wpt_lat || !b->env_wpt_lon))
     return fail(BSG_E_INVALID_ARG, "bsg_bind: HorizontalCR needs env_wpt_lat/env_wpt_lon%s%lld");
-  if ((c->cfg.env_kind == BSG_ENV_STATIC_OBSTACLE || c->cfg.env_kind == BSG_ENV_SECTOR_CR) &&
-      !b->env_geom)
-    return fail(BSG_E_INVALID_ARG, "bsg_bind: StaticObstacle/SectorCR need env_geom%s%lld");
+  if (bsg_geom_width(c->cfg.env_kind, c->cfg.num_ac) > 0 && !b->env_geom)
+    return fail(BSG_E_INVALID_ARG, "bsg_bind: StaticObstacle/SectorCR/PlanWaypoint need env_geom%s%lld");
   if (c->cfg.env_kind == BSG_ENV_STATIC_OBSTACLE && !b->env_aux)
     return fail(BSG_E_INVALID_ARG, "bsg_bind: StaticObstacle needs env_aux%s%lld");
   if (c->cfg.env_kind == BSG_ENV_MERGE && !b->topk)
@@ -243,8 +247,7 @@ int32_t bsg_bind(bsg_ctx* c, const bsg_buffers* b) {
     return fail(BSG_E_INVALID_ARG, "bsg_bind: SAME_STEP autoreset needs final_obs%s%lld");
   if (c->wind.np > 0 && (!b->gs || !b->trk))
     return fail(BSG_E_INVALID_ARG, "bsg_bind: a wind field needs gs/trk%s%lld");
-  if (c->cfg.compute_cd && c->cfg.env_kind != BSG_ENV_DESCENT &&
-      c->cfg.env_kind != BSG_ENV_STATIC_OBSTACLE &&
+  if (c->cfg.compute_cd && c->cfg.num_ac > 1 &&
       (!b->conf_mask || !b->los_mask || !b->tcpamax || !b->min_sep))
     return fail(BSG_E_INVALID_ARG, "bsg_bind: compute_cd needs conf_mask/los_mask/tcpamax/min_sep%s%lld");
   c->bufs = *b;

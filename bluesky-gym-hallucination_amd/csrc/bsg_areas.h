@@ -24,7 +24,10 @@ constexpr int SO_GEOM = 2 + SO_NOBST * SO_W;
 constexpr int SO_SPAWN_W = SO_NOBST * (4 + SO_VMAX) + 2;
 constexpr int SC_VMAX = 32;
 constexpr int SC_GEOM = 4 + 2 * SC_VMAX;
+constexpr int PW_NWPT = 5;                 // plan_waypoint_env.py:15 NUM_WAYPOINTS
+constexpr int PW_GEOM = 2 * PW_NWPT;        // waypoint lat[5], lon[5]
 constexpr uint32_t TAG_STAT = 0x53544154u;  // 'STAT'
+constexpr uint32_t TAG_PLAN = 0x504C414Eu;  // 'PLAN'
 constexpr uint32_t TAG_SECT = 0x53454354u;  // 'SECT'
 constexpr double TWO_PI = 2.0 * 3.141592653589793;
 constexpr double SC_CLAT = 51.990426702297746;   // sector_cr_env.py:16 CENTER

@@ -705,11 +705,39 @@ __device__ __forceinline__ void spawn_static(const KParams& p, int e, uint32_t e
   aux[1] = geo[1];
 }
 
+// plan_waypoint_env.py:156-171 (reset) + :200-213 (_generate_waypoint): KL001 at 52N 4E,
+// alt 0, 150 kt unless it still exists (keep: cre refused), then five waypoints at
+// (randint(0, 75) km, randint(0, 359) deg) from its position into env_geom [lat[5], lon[5]]
+__device__ __forceinline__ void spawn_plan(const KParams& p, int e, uint32_t episode, AC& s,
+                                           bool keep) {
+  if (!keep) cre(s, 52.0, 4.0, 0.0, 0.0, 150.0);
+  double* geo = p.b.env_geom + (size_t)e * PW_GEOM;
+  const double* row = p.spawn ? p.spawn + (size_t)e * p.spawn_width : nullptr;
+  for (int k = 0; k < PW_NWPT; ++k) {
+    double dis, hdg;
+    if (row) {
+      dis = row[k];
+      hdg = row[PW_NWPT + k];
+    } else {
+      U4 r = philox4x32_10((uint32_t)(e + p.cfg.env_offset), episode, (uint32_t)k, TAG_PLAN, p.seed);
+      dis = (double)randint_u32(r.x, 0, 75);
+      hdg = (double)randint_u32(r.y, 0, 359);
+    }
+    get_point_at_distance(s.lat, s.lon, dis, hdg, &geo[k], &geo[PW_NWPT + k]);
+  }
+}
+
+// Descent and PlanWaypoint keep a truncated episode's aircraft through reset (bsg.h
+// BSG_FLAG_AC_PRESENT): their reset() never clears the traffic
+template <int KIND>
+constexpr bool kKeepsAircraft = KIND == BSG_ENV_DESCENT || KIND == BSG_ENV_PLAN_WAYPOINT;
+
 // aux[0]: target altitude (Vertical/Descent); aux[0..1]: waypoint (HorizontalCR);
-// aux[0..2]: lat, lon, hdg of this aircraft (SectorCR, from sector_reset_plan)
+// aux[0..2]: lat, lon, hdg of this aircraft (SectorCR, from sector_reset_plan).
+// keep: the aircraft (already loaded into s) survives the reset (kKeepsAircraft kinds)
 template <int KIND>
 __device__ __forceinline__ void spawn(const KParams& p, int e, int j, uint32_t episode, AC& s,
-                                      double* target) {
+                                      double* target, bool keep) {
   if constexpr (KIND == BSG_ENV_MERGE) {
     spawn_merge(p, e, j, episode, s);
   } else if constexpr (KIND == BSG_ENV_VERTICAL_CR) {
@@ -721,10 +749,13 @@ __device__ __forceinline__ void spawn(const KParams& p, int e, int j, uint32_t e
   } else if constexpr (KIND == BSG_ENV_SECTOR_CR) {
     if (target[3] != 0.0) cre(s, target[0], target[1], target[2], 350.0, 150.0);
     else s = AC{};                                 // slot beyond this episode's count
+  } else if constexpr (KIND == BSG_ENV_PLAN_WAYPOINT) {
+    spawn_plan(p, e, episode, s, keep);
   } else {
+    // descent_env.py:169-174: both altitudes are drawn even when cre is refused
     double alt_init;
     draw_alts(p, e, episode, TAG_DESC, &alt_init, target);
-    cre(s, 52.0, 4.0, 0.0, alt_init, 150.0);
+    if (!keep) cre(s, 52.0, 4.0, 0.0, alt_init, 150.0);
   }
 }
 
@@ -767,13 +798,13 @@ __device__ __forceinline__ void store_env(const Buffers& b, int e, const EnvScal
 
 template <int KIND>
 __device__ __forceinline__ void reset_scalars(EnvScalars& v, const double aux[2]) {
-  v.step_count = 0; v.flags = 0; v.wpt_reach = 0; v.faf_reached = 0; v.total_intr = 0;
+  v.step_count = 0; v.flags = kKeepsAircraft<KIND> ? BSG_FLAG_AC_PRESENT : 0; v.wpt_reach = 0; v.faf_reached = 0; v.total_intr = 0;
   v.total_reward = 0.0; v.drift_sum = 0.0; v.final_alt = 0.0;
   v.aux[2] = 0.0; v.aux[3] = 0.0;
   if constexpr (KIND == BSG_ENV_HORIZONTAL_CR || KIND == BSG_ENV_STATIC_OBSTACLE) {
     v.wpt_lat = aux[0]; v.wpt_lon = aux[1];
-  } else if constexpr (KIND == BSG_ENV_SECTOR_CR) {
-    // waypoint and aircraft count were set by sector_reset_plan
+  } else if constexpr (KIND == BSG_ENV_SECTOR_CR || KIND == BSG_ENV_PLAN_WAYPOINT) {
+    // waypoint(s) and aircraft count were written by sector_reset_plan / spawn_plan
   } else {
     v.target_alt = aux[0];
   }
@@ -942,6 +973,8 @@ __device__ __forceinline__ void own_obs(const KParams& p, const LT& L, int lane,
     double sd, cd;
     sincos(*drift * kD2R, &sd, &cd);
     sc[0] = *wdist / 170; sc[1] = cd; sc[2] = sd; sc[3] = 0.0; sc[4] = 0.0;
+  } else if constexpr (KIND == BSG_ENV_PLAN_WAYPOINT) {
+    // plan_obs (five waypoints)
   } else if constexpr (KIND == BSG_ENV_HORIZONTAL_CR) {
     // horizontal_cr_env.py:191-203
     double wqdr, wd;
@@ -990,6 +1023,8 @@ __device__ __forceinline__ void write_own_obs(float* obs, float* fobs, float* lr
     put(SO_NOBST, sc[1]);                   // destination_waypoint_cos_drift
     put(SO_NOBST + 1, sc[0]);               // destination_waypoint_distance
     put(SO_NOBST + 2, sc[2]);               // destination_waypoint_sin_drift
+  } else if constexpr (KIND == BSG_ENV_PLAN_WAYPOINT) {
+    // the waypoint terms are written by plan_obs_write
   } else if constexpr (KIND == BSG_ENV_HORIZONTAL_CR) {
     const int NI = N - 1;
     put(NI, sc[0]);                         // cos_drift
@@ -1021,6 +1056,38 @@ __device__ __forceinline__ void static_obs_write(const double* geo, double lat, 
     put(2 * SO_NOBST + 3 + o, g[2] / 50);               // restricted_area_radius
     put(3 * SO_NOBST + 3 + o, sb);                      // sin_difference_restricted_area_pos
   }
+}
+
+// plan_waypoint_env.py:86-124 (_get_obs) with the reach flags before _get_reward: per
+// waypoint k the distance (km, into dkm for the reward) and drift, masked by
+// f = (reach - 1) * -1 (0 once reached; 0 * negative gives -0.0 as in NumPy)
+__device__ __forceinline__ void plan_obs(const double* geo, double lat, double lon, double hdg,
+                                         int reach, double dkm[PW_NWPT], double po[3 * PW_NWPT]) {
+#pragma unroll
+  for (int k = 0; k < PW_NWPT; ++k) {
+    double qdr, d;
+    kwikqdrdist(lat, lon, geo[k], geo[PW_NWPT + k], &qdr, &d);
+    dkm[k] = d * 1.852;
+    const double drift = bound180(hdg - qdr);
+    double sd, cd;
+    sincos(drift * kD2R, &sd, &cd);
+    const double f = ((reach >> k) & 1) ? 0.0 : 1.0;
+    po[k] = f * cd;                                  // cos_difference
+    po[PW_NWPT + k] = f * sd;                        // sin_difference
+    po[2 * PW_NWPT + k] = f * dkm[k] / 75;           // waypoint_distance
+  }
+}
+
+__device__ __forceinline__ void plan_obs_write(const double po[3 * PW_NWPT], int reach, float* obs,
+                                               float* fobs, float* lrn) {
+  auto put = [&](int off, double v) {
+    const float f = (float)v;
+    obs[off] = f;
+    if (fobs) fobs[off] = f;
+    if (lrn) lrn[off] = f;
+  };
+  for (int k = 0; k < 3 * PW_NWPT; ++k) put(k, po[k]);
+  for (int k = 0; k < PW_NWPT; ++k) put(3 * PW_NWPT + k, (double)((reach >> k) & 1));   // waypoint_reached
 }
 
 template <class LT>
@@ -1150,8 +1217,9 @@ __device__ __forceinline__ void propagate(const KParams& p, int e, int j, size_t
     } else if constexpr (KIND == BSG_ENV_SECTOR_CR) {
       hdg_spd_action<WIND>(p, s, p.actions[(size_t)e * 2 + 0], p.actions[(size_t)e * 2 + 1],
                            22.5, 20.0 / 3.0);
-    } else if constexpr (KIND == BSG_ENV_HORIZONTAL_CR) {
-      // horizontal_cr_env.py:272-275: HDG KL001 {hdg + a*45} (no wrap)
+    } else if constexpr (KIND == BSG_ENV_HORIZONTAL_CR || KIND == BSG_ENV_PLAN_WAYPOINT) {
+      // horizontal_cr_env.py:272-275 / plan_waypoint_env.py:148-154: HDG KL001
+      // {hdg + a*45} (no wrap)
       s.ap_trk = hdg_command_track<WIND>(p.wind, s, s.hdg + p.actions[e] * 45);
       s.nav &= ~1;
     } else {
@@ -1248,11 +1316,9 @@ __global__ __launch_bounds__(64) void step_kernel(KParams p) {
     if constexpr (KIND == BSG_ENV_SECTOR_CR) sector_reset_plan<GS>(p, e, j, g, resetting, ev, aux);
     const bool on = ok && j < ev.nac;   // SectorCR: aircraft slot in use this episode
     if (ok) {
-      if (resetting) {
-        spawn<KIND>(p, e, j, ev.episode, s, aux);
-      } else {
-        load_ac<WIND>(b, a, s);
-      }
+      const bool keep = kKeepsAircraft<KIND> && (ev.flags & BSG_FLAG_AC_PRESENT);
+      if (!resetting || keep) load_ac<WIND>(b, a, s);
+      if (resetting) spawn<KIND>(p, e, j, ev.episode, s, aux, keep);
 #if defined(BSG_EXP_SKIP_OWN) && BSG_EXP_SKIP_OWN
       // experiment build only (tools/ablate.py): the ownship does not move
       if (stepping && on && j != 0) propagate<KIND, WIND>(p, e, j, a, s, ev, sub_reward, sub_done);
@@ -1271,7 +1337,9 @@ __global__ __launch_bounds__(64) void step_kernel(KParams p) {
 #endif
 
   // ---------------- B: observation, reward, CD -----------------------------------------
-  constexpr bool kLaneObs = KIND != BSG_ENV_DESCENT && KIND != BSG_ENV_STATIC_OBSTACLE;
+  constexpr bool kLaneObs = KIND != BSG_ENV_DESCENT && KIND != BSG_ENV_STATIC_OBSTACLE &&
+                            KIND != BSG_ENV_PLAN_WAYPOINT;
+  constexpr bool kPlan = KIND == BSG_ENV_PLAN_WAYPOINT;
   constexpr bool kRanked = KIND == BSG_ENV_MERGE || KIND == BSG_ENV_SECTOR_CR;
   const bool on = ok && j < ev.nac;
   double o[7] = {0, 0, 0, 0, 0, 0, 0};
@@ -1353,11 +1421,17 @@ __global__ __launch_bounds__(64) void step_kernel(KParams p) {
 
   // lane 0: scalar obs, reward, termination (per env)
   double sc[7] = {0, 0, 0, 0, 0, 0, 0};
+  double po[kPlan ? 3 * PW_NWPT : 1];     // PlanWaypoint waypoint obs terms
+  int reach_obs = ev.wpt_reach;           // PlanWaypoint: reach flags the obs shows
   float reward = 0.0f;
   bool term = false, trunc = false, done = false;
   if (ok && j == 0) {
     double wdist = 0, drift = 0, rwd = 0;
     own_obs<KIND>(p, L, lane, ev, sc, &wdist, &drift, &rwd);
+    double dkm[kPlan ? PW_NWPT : 1];
+    if constexpr (kPlan)
+      plan_obs(b.env_geom + (size_t)e * PW_GEOM, L.lat[lane], L.lon[lane], L.hdg[lane],
+               ev.wpt_reach, dkm, po);
     bool trunc_env = false;
     if (stepping) {
       double r;
@@ -1382,6 +1456,15 @@ __global__ __launch_bounds__(64) void step_kernel(KParams p) {
         const double dd = fabs(drift * kD2R);
         r = ((double)reach + dd * -0.1) + (double)(nintr * -1);
         ev.drift_sum += dd;
+      } else if constexpr (kPlan) {
+        // _get_reward :135-146 / _check_waypoint :215-227: +1 per newly reached waypoint
+        // (< 5 km); terminated once all five are reached
+        int nr = 0;
+        for (int k = 0; k < PW_NWPT; ++k) {
+          if (dkm[k] < 5 && !((ev.wpt_reach >> k) & 1)) { ev.wpt_reach |= 1 << k; ++nr; }
+        }
+        r = (double)nr;
+        d = ev.wpt_reach == (1 << PW_NWPT) - 1;
       } else if constexpr (KIND == BSG_ENV_HORIZONTAL_CR) {
         // _check_waypoint :237-248 ; _check_drift :250-253 ; _check_intrusion :255-265
         int reach = 0;
@@ -1407,6 +1490,7 @@ __global__ __launch_bounds__(64) void step_kernel(KParams p) {
       ev.total_reward += r;
       reward = (float)r;
       term = d != 0;
+      if (kKeepsAircraft<KIND> && term) ev.flags &= ~BSG_FLAG_AC_PRESENT;   // aircraft deleted
       ev.step_count += 1;
       trunc = (p.cfg.max_episode_steps > 0 && ev.step_count >= p.cfg.max_episode_steps) || trunc_env;
       done = term || trunc;
@@ -1430,6 +1514,7 @@ __global__ __launch_bounds__(64) void step_kernel(KParams p) {
       if constexpr (KIND == BSG_ENV_STATIC_OBSTACLE)
         static_obs_write(b.env_geom + (size_t)e * SO_GEOM, L.lat[lane], L.lon[lane], L.hdg[lane],
                          obs, fobs, lrn);
+      if constexpr (kPlan) plan_obs_write(po, reach_obs, obs, fobs, lrn);
       b.reward[e] = reward;
       b.terminated[e] = term ? 1 : 0;
       b.truncated[e] = trunc ? 1 : 0;
@@ -1449,6 +1534,10 @@ __global__ __launch_bounds__(64) void step_kernel(KParams p) {
           info[3] = ev.drift_sum / (double)ev.step_count;
         } else if constexpr (KIND == BSG_ENV_HORIZONTAL_CR || KIND == BSG_ENV_SECTOR_CR) {
           info[2] = ev.drift_sum / (double)ev.step_count;   // average_drift
+          info[3] = 0.0;
+        } else if constexpr (kPlan) {
+          info[1] = 0.0;
+          info[2] = (double)__popc(ev.wpt_reach);           // waypoints_completed
           info[3] = 0.0;
         } else if constexpr (KIND == BSG_ENV_STATIC_OBSTACLE) {
           info[1] = (double)ev.wpt_reach;                   // waypoint_reached
@@ -1482,7 +1571,9 @@ __global__ __launch_bounds__(64) void step_kernel(KParams p) {
       if constexpr (KIND == BSG_ENV_SECTOR_CR)
         sector_reset_plan<GS>(p, e, j, g, same_step_reset, ev, aux);
       if (same_step_reset && ok) {
-        spawn<KIND>(p, e, j, ev.episode, s, aux);
+        const bool keep = kKeepsAircraft<KIND> && (ev.flags & BSG_FLAG_AC_PRESENT);
+        if (keep) load_ac<WIND>(b, a, s);
+        spawn<KIND>(p, e, j, ev.episode, s, aux, keep);
         store_ac<WIND>(b, a, s);
         if (b.memo_cache) memo_invalidate(b.memo_cache, a, (size_t)p.E * N);
       }
@@ -1509,6 +1600,12 @@ __global__ __launch_bounds__(64) void step_kernel(KParams p) {
                            L.hdg[lane], obs, nullptr, lrn);
           ev.aux[0] = wdist;
           ev.aux[1] = drift;
+        }
+        if constexpr (kPlan) {
+          double dkm[PW_NWPT];
+          plan_obs(b.env_geom + (size_t)e * PW_GEOM, L.lat[lane], L.lon[lane], L.hdg[lane],
+                   ev.wpt_reach, dkm, po);
+          plan_obs_write(po, ev.wpt_reach, obs, nullptr, lrn);
         }
       } else {
         int r = 0x7fffffff;
@@ -1538,7 +1635,8 @@ static hipError_t launch_kind_w(const KParams& p, hipStream_t st) {
   const int grid = (p.E + epb - 1) / epb;
 #define BSG_CASE(G) \
   case G: hipLaunchKernelGGL((step_kernel<KIND, G, WIND>), dim3(grid), dim3(64), p.lds_pad, st, p); break;
-  if constexpr (KIND == BSG_ENV_DESCENT || KIND == BSG_ENV_STATIC_OBSTACLE) {
+  if constexpr (KIND == BSG_ENV_DESCENT || KIND == BSG_ENV_STATIC_OBSTACLE ||
+                KIND == BSG_ENV_PLAN_WAYPOINT) {
     switch (gs) { BSG_CASE(1) default: return hipErrorInvalidValue; }        // one aircraft
   } else if constexpr (KIND == BSG_ENV_SECTOR_CR) {
     switch (gs) { BSG_CASE(8) BSG_CASE(16) BSG_CASE(32) BSG_CASE(64) default: return hipErrorInvalidValue; }
@@ -1570,6 +1668,7 @@ hipError_t launch_step(const KParams& p, hipStream_t st) {
     case BSG_ENV_HORIZONTAL_CR: return launch_kind<BSG_ENV_HORIZONTAL_CR>(p, st);
     case BSG_ENV_STATIC_OBSTACLE: return launch_kind<BSG_ENV_STATIC_OBSTACLE>(p, st);
     case BSG_ENV_SECTOR_CR: return launch_kind<BSG_ENV_SECTOR_CR>(p, st);
+    case BSG_ENV_PLAN_WAYPOINT: return launch_kind<BSG_ENV_PLAN_WAYPOINT>(p, st);
     default: return hipErrorInvalidValue;
   }
 }

@@ -41,7 +41,16 @@ enum {
 };
 
 enum { BSG_ENV_MERGE = 0, BSG_ENV_VERTICAL_CR = 1, BSG_ENV_DESCENT = 2,
-       BSG_ENV_HORIZONTAL_CR = 3, BSG_ENV_STATIC_OBSTACLE = 4, BSG_ENV_SECTOR_CR = 5 };
+       BSG_ENV_HORIZONTAL_CR = 3, BSG_ENV_STATIC_OBSTACLE = 4, BSG_ENV_SECTOR_CR = 5,
+       BSG_ENV_PLAN_WAYPOINT = 6 };
+
+/* bsg_buffers.flags bits */
+enum { BSG_FLAG_RESET_PENDING = 1,   /* NEXT_STEP autoreset due on the next step */
+       BSG_FLAG_AC_PRESENT = 2 };    /* Descent / PlanWaypoint: KL001 exists.  Their reset()
+                                        does not clear the traffic, so a reset after a
+                                        truncation keeps the aircraft (cre refused,
+                                        descent_env.py:173, plan_waypoint_env.py:164); the
+                                        terminal step deletes it (:201-204, :189-193) */
 
 /* Vector-env autoreset conventions:
  *   NEXT_STEP: Gymnasium >= 1.0 VectorEnv default -- the step AFTER a done step resets
@@ -91,9 +100,9 @@ typedef struct bsg_buffers {
                                 NULL disables it */
   /* ---- per-env state [E] ----------------------------------------------------------- */
   int32_t *step_count;       /* TimeLimit elapsed steps */
-  int32_t *flags;            /* bit0: reset pending (NEXT_STEP autoreset) */
+  int32_t *flags;            /* BSG_FLAG_* (zero-initialised by the caller) */
   uint32_t *episode;         /* episode counter (Philox counter word) */
-  int32_t *wpt_reach;        /* merge_env.py:97 */
+  int32_t *wpt_reach;        /* merge_env.py:97; PlanWaypoint: bit k = waypoint k reached */
   int32_t *faf_reached;      /* merge_env.py:92 (info faf_reach) */
   int32_t *total_intrusions; /* info */
   double *total_reward;      /* info */
@@ -103,7 +112,8 @@ typedef struct bsg_buffers {
   double *env_wpt_lat;       /* HorizontalCR per-env waypoint (horizontal_cr_env.py:135-148) */
   double *env_wpt_lon;
   double *env_geom;          /* [E, bsg_geom_width] StaticObstacle obstacles + waypoint,
-                                SectorCR sector polygon + aircraft count + waypoint */
+                                SectorCR sector polygon + aircraft count + waypoint,
+                                PlanWaypoint 5 waypoint lat then 5 lon */
   double *env_aux;           /* [E, 4] StaticObstacle: waypoint distance (km) and drift (deg)
                                 of the last observation, drift samples, crashed flag */
   /* ---- outputs --------------------------------------------------------------------- */
@@ -154,12 +164,14 @@ const char* bsg_last_error(void);
 /* Flat observation length for an env kind (sum of the Box sizes of the reference
  * observation_space: merge_env.py:59-74 -> 5+7K; vertical_cr_env.py:67-83 -> 4+7(N-1);
  * descent_env.py:53-60 -> 4; horizontal_cr_env.py:49-60 -> 3+5(N-1);
- * static_obstacle_env.py:61-71 -> 3+4*10; sector_cr_env.py:53-66 -> 3+7K). Negative on
+ * static_obstacle_env.py:61-71 -> 3+4*10; sector_cr_env.py:53-66 -> 3+7K;
+ * plan_waypoint_env.py:50-56 -> 4*5). Negative on
  * invalid input.  A wind field with augment_obs adds 2 (bsg_ctx_obs_dim). */
 int32_t bsg_obs_dim(int32_t env_kind, int32_t num_ac, int32_t num_ac_state);
 
 /* Action width (merge_env.py:76, static_obstacle_env.py:73, sector_cr_env.py:68 -> 2;
- * vertical_cr_env.py:85 / descent_env.py:62 / horizontal_cr_env.py:62 -> 1). */
+ * vertical_cr_env.py:85 / descent_env.py:62 / horizontal_cr_env.py:62 /
+ * plan_waypoint_env.py:59 -> 1). */
 int32_t bsg_action_dim(int32_t env_kind);
 
 /* Doubles per env of host-supplied spawn parameters for bsg_reset / bsg_step:
@@ -175,11 +187,13 @@ int32_t bsg_action_dim(int32_t env_kind);
  *                        (static_obstacle_env.py:148-226)
  *   SectorCR [68+3N]   : aircraft count, vertices, 32 vertex lat, 32 vertex lon, ownship
  *                        waypoint lat/lon, then (lat, lon, hdg) per aircraft
- *                        (sector_cr_env.py:84-208) */
+ *                        (sector_cr_env.py:84-208)
+ *   PlanWaypoint [10]  : 5 waypoint distances (km) then 5 bearings (deg) from the ownship,
+ *                        the np.random draws of plan_waypoint_env.py:205-206 */
 int32_t bsg_spawn_width(int32_t env_kind, int32_t num_ac);
 
 /* Doubles per env of bsg_buffers.env_geom (0 for kinds without per-env geometry):
- * StaticObstacle 2 + 10*(6 + 2*16); SectorCR 4 + 2*32. */
+ * StaticObstacle 2 + 10*(6 + 2*16); SectorCR 4 + 2*32; PlanWaypoint 2*5. */
 int32_t bsg_geom_width(int32_t env_kind, int32_t num_ac);
 
 /* Replaces: gym.make(id) -> Env.__init__ (merge_env.py:54-101): validates the config

@@ -6,6 +6,8 @@ reference env classes compute per env:
 * ``MergeOracle``     -- bluesky_gym/envs/merge_env.py:103-293
 * ``VerticalOracle``  -- bluesky_gym/envs/vertical_cr_env.py:113-305
 * ``DescentOracle``   -- bluesky_gym/envs/descent_env.py:89-206
+* ``HorizontalOracle`` -- bluesky_gym/envs/horizontal_cr_env.py:82-275
+* ``PlanWaypointOracle`` -- bluesky_gym/envs/plan_waypoint_env.py:86-227
 
 plus Gymnasium's ``TimeLimit`` (bluesky_gym/__init__.py:9,27,45) and the two vector
 autoreset conventions (Gymnasium NEXT_STEP, SB3 SAME_STEP).  The simulator arithmetic
@@ -71,6 +73,7 @@ VERTICAL_OBS_KEYS = ("altitude", "altitude_difference", "cos_difference_pos",
                      "target_altitude", "vz", "x_difference_speed", "y_difference_speed",
                      "z_difference_speed")
 DESCENT_OBS_KEYS = ("altitude", "runway_distance", "target_altitude", "vz")
+PLAN_OBS_KEYS = ("cos_difference", "sin_difference", "waypoint_distance", "waypoint_reached")
 HORIZONTAL_OBS_KEYS = ("cos_difference_pos", "cos_drift", "intruder_distance",
                        "sin_difference_pos", "sin_drift", "waypoint_distance",
                        "x_difference_speed", "y_difference_speed")
@@ -109,6 +112,19 @@ def descent_obs_sizes():
     return {k: 1 for k in DESCENT_OBS_KEYS}
 
 
+# ---- plan_waypoint_env.py:11-23 --------------------------------------------------------------
+P_DISTANCE_MARGIN = 5
+P_WAYPOINT_DISTANCE_MIN, P_WAYPOINT_DISTANCE_MAX = 0, 75
+P_NUM_WAYPOINTS = 5
+P_REACH_REWARD = 1
+P_AC_SPD = 150
+P_D_HEADING = 45
+
+
+def plan_obs_sizes():
+    return {k: P_NUM_WAYPOINTS for k in PLAN_OBS_KEYS}
+
+
 def flatten_obs(obs: dict, keys) -> np.ndarray:
     return np.concatenate([np.asarray(obs[k], np.float64).reshape(obs[k].shape[0], -1)
                            for k in keys], axis=1)
@@ -117,6 +133,11 @@ def flatten_obs(obs: dict, keys) -> np.ndarray:
 # =======================================================================================
 class _Base:
     kind = None
+    # descent_env.py:162-182 / plan_waypoint_env.py:156-171: reset() does not clear the
+    # traffic, so after a truncation (the aircraft is only deleted on termination,
+    # descent_env.py:201-204, plan_waypoint_env.py:189-193) cre('KL001') is refused and the
+    # next episode continues with the old aircraft.  ``present`` tracks that aircraft.
+    keeps_aircraft = False
     route_lat = np.zeros(0)
     route_lon = np.zeros(0)
     route_next_qdr = np.zeros(0)
@@ -137,6 +158,7 @@ class _Base:
         self.total_reward = np.zeros(self.E, np.float64)
         self.total_intrusions = np.zeros(self.E, np.int32)
         self.env_ids = np.arange(self.E)     # global env ids (Philox counter word 0)
+        self.present = np.zeros(self.E, bool)  # keeps_aircraft kinds: KL001 exists
         self.wind = None                     # bsx.WindField (wrappers/wind.py) or None
         self.wind_augment = False
 
@@ -171,6 +193,7 @@ class _Base:
             spawn = np.zeros((self.E, self.spawn_width()), np.float64)
             spawn[ids] = self.device_spawn_params(self.env_ids[ids], self.episode[ids])
         self._reset_ids(ids, np.asarray(spawn, np.float64))
+        self.present[ids] = True
         self.episode[ids] += 1          # every reset consumes one Philox episode counter
         self.step_count[ids] = 0
         self.needs_reset[ids] = False
@@ -203,6 +226,8 @@ class _Base:
         self._commit(res, live)
         self.step_count[live] += 1
         term = res["terminated"] & live
+        if self.keeps_aircraft:
+            self.present[term] = False      # the terminal step deletes the aircraft
         trunc = (self.step_count >= self.max_steps) & live if self.max_steps > 0 \
             else np.zeros(self.E, bool)
         if "truncated_env" in res:          # SectorCR: ownship left the sector
@@ -414,9 +439,11 @@ class _VertBase(_Base):
         st.selvs[:, 0] = np.where(up | dn, a, st.selvs[:, 0])
 
     def _own_reset(self, ids, spawn):
-        alt_init = spawn[ids, 0]
         self.target_alt[ids] = spawn[ids, 1]
         self.final_altitude[ids] = 0.0
+        if self.keeps_aircraft:
+            ids = ids[~self.present[ids]]   # cre('KL001') refused: aircraft kept
+        alt_init = spawn[ids, 0]
         st = self.st
         for j in range(self.N):
             bsx.cre_state(st, (ids, np.full(len(ids), j)), 0.0, 0.0, 0.0, 0.0, 0.0)
@@ -582,6 +609,7 @@ def vertical_conflict_ints(altitude, target_alt, spd, y0, y1, y2, y3):
 class DescentOracle(_VertBase):
     """DescentEnv-v0 (descent_env.py).  N = 1."""
     kind = "descent"
+    keeps_aircraft = True
 
     def __init__(self, num_envs, action_frequency=30, simdt=1.0, max_episode_steps=300,
                  autoreset=AUTORESET_NEXT_STEP, seed=0):
@@ -834,3 +862,101 @@ def descent_spawn_from_np_random(rs):
     alt_init = rs.randint(ALT_MIN, ALT_MAX)
     target_alt = alt_init + rs.randint(-TARGET_ALT_DIF, TARGET_ALT_DIF)
     return np.array([float(alt_init), float(target_alt)])
+
+
+# =======================================================================================
+class PlanWaypointOracle(_Base):
+    """PlanWaypointEnv-v0 (plan_waypoint_env.py).  N = 1, five waypoints around the
+    ownship's position at reset (the kept aircraft's, after a truncation)."""
+    kind = "plan_waypoint"
+    keeps_aircraft = True
+
+    def __init__(self, num_envs, action_frequency=10, simdt=1.0, max_episode_steps=300,
+                 autoreset=AUTORESET_NEXT_STEP, seed=0):
+        super().__init__(num_envs, 1, action_frequency, simdt, max_episode_steps,
+                         autoreset, seed)
+        W = P_NUM_WAYPOINTS
+        self.obs_sizes = plan_obs_sizes()
+        self.obs_dim = 4 * W
+        self.wpt_lat = np.zeros((self.E, W))
+        self.wpt_lon = np.zeros((self.E, W))
+        self.wpt_reach = np.zeros((self.E, W), np.int64)
+
+    def spawn_width(self):
+        return 2 * P_NUM_WAYPOINTS
+
+    def device_spawn_params(self, env_ids, episodes):
+        k = np.arange(P_NUM_WAYPOINTS, dtype=np.uint32)[None, :]
+        x0, x1, _, _ = philox.philox4x32_10(np.asarray(env_ids, np.uint32)[:, None],
+                                            np.asarray(episodes, np.uint32)[:, None], k,
+                                            philox.TAG_PLAN, self.seed)
+        dis = philox.randint_u32(x0, P_WAYPOINT_DISTANCE_MIN, P_WAYPOINT_DISTANCE_MAX)
+        hdg = philox.randint_u32(x1, 0, 359)
+        return np.concatenate([dis, hdg], axis=1).astype(np.float64)
+
+    def _reset_ids(self, ids, spawn):
+        """plan_waypoint_env.py:156-171 (reset) + _generate_waypoint :200-213."""
+        st = self.st
+        new = ids[~self.present[ids]]
+        # cre('KL001', acspd=150): default 52N 4E, hdg 0, alt 0 (refused if KL001 exists)
+        bsx.cre_state(st, (new, np.zeros(len(new), int)), 52.0, 4.0, 0.0, 0.0, P_AC_SPD)
+        W = P_NUM_WAYPOINTS
+        lat, lon = bsx.get_point_at_distance(st.lat[ids, :1], st.lon[ids, :1],
+                                             spawn[ids, :W], spawn[ids, W:2 * W])
+        self.wpt_lat[ids] = lat
+        self.wpt_lon[ids] = lon
+        self.wpt_reach[ids] = 0
+
+    def _apply_action(self, actions):
+        """plan_waypoint_env.py:148-154: HDG KL001 {hdg + a*45} (no wrap)."""
+        st = self.st
+        st.ap_trk[:, 0] = bsx.selhdg_track(st, (slice(None), 0),
+                                           st.hdg[:, 0] + actions[:, 0] * P_D_HEADING, self.wind)
+        st.swlnav[:, 0] = False
+
+    def _obs_core(self):
+        """plan_waypoint_env.py:86-124 (_get_obs), with the reach flags before _get_reward."""
+        st = self.st
+        qdr, dis = bsx.kwikqdrdist(st.lat[:, :1], st.lon[:, :1], self.wpt_lat, self.wpt_lon)
+        dis_km = dis * NM2KM
+        drift = bsx.bound_angle_positive_negative_180(st.hdg[:, :1] - qdr)
+        f = (self.wpt_reach - 1) * -1          # int: 1 unreached, 0 reached
+        obs = {
+            "waypoint_distance": f * dis_km / P_WAYPOINT_DISTANCE_MAX,
+            "cos_difference": f * np.cos(np.deg2rad(drift)),
+            "sin_difference": f * np.sin(np.deg2rad(drift)),
+            "waypoint_reached": self.wpt_reach.astype(np.float64),
+        }
+        return obs, dis_km
+
+    def observe(self):
+        obs, _ = self._obs_core()
+        return {"obs": self._flat(obs, PLAN_OBS_KEYS), "obs_dict": obs}
+
+    def _observe_and_reward(self):
+        """_get_reward :135-146 + _check_waypoint :215-227."""
+        obs, dis_km = self._obs_core()
+        new = (dis_km < P_DISTANCE_MARGIN) & (self.wpt_reach != 1)
+        reward = (new.sum(axis=1) * P_REACH_REWARD).astype(np.float64)
+        new_wr = np.where(new, 1, self.wpt_reach)
+        done = (new_wr == 1).all(axis=1)
+        return dict(obs=self._flat(obs, PLAN_OBS_KEYS), obs_dict=obs, reward=reward,
+                    terminated=done, _new_wr=new_wr)
+
+    def _commit(self, res, live):
+        self.wpt_reach = np.where(live[:, None], res["_new_wr"], self.wpt_reach)
+        self.total_reward = np.where(live, self.total_reward + res["reward"], self.total_reward)
+
+    def info(self):
+        return {"total_reward": self.total_reward.copy(),
+                "waypoints_completed": self.wpt_reach.sum(axis=1)}
+
+
+def plan_spawn_from_np_random(rs):
+    """np.random draws of plan_waypoint_env.py:205-206 (distance, heading per waypoint)
+    -> [dis0..4, hdg0..4]."""
+    d, h = [], []
+    for _ in range(P_NUM_WAYPOINTS):
+        d.append(float(rs.randint(P_WAYPOINT_DISTANCE_MIN, P_WAYPOINT_DISTANCE_MAX)))
+        h.append(float(rs.randint(0, 359)))
+    return np.array(d + h, np.float64)

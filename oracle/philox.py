@@ -22,6 +22,7 @@ TAG_MERGE = 0x4D455247      # 'MERG'
 TAG_VERT = 0x56455254       # 'VERT'
 TAG_DESC = 0x44455343       # 'DESC'
 TAG_HORZ = 0x484F525A       # 'HORZ'
+TAG_PLAN = 0x504C414E       # 'PLAN'
 
 
 def philox4x32_10(c0, c1, c2, c3, seed):

@@ -357,6 +357,7 @@ def load_reference_envs(reference_root="/root/reference"):
         "horizontal": importlib.import_module("bluesky_gym.envs.horizontal_cr_env"),
         "static": importlib.import_module("bluesky_gym.envs.static_obstacle_env"),
         "sector": importlib.import_module("bluesky_gym.envs.sector_cr_env"),
+        "plan": importlib.import_module("bluesky_gym.envs.plan_waypoint_env"),
         "functions": importlib.import_module("bluesky_gym.envs.common.functions"),
         "wind": importlib.import_module("bluesky_gym.wrappers.wind"),
         "uncertainty": importlib.import_module("bluesky_gym.wrappers.uncertainty"),

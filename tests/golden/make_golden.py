@@ -219,7 +219,10 @@ def gen_horizontal(bs, mods, num_intruders, episodes, seed, max_steps=300, wind=
     return out
 
 
-def gen_descent(bs, mods, episodes, seed, max_steps=300, wind=None):
+def gen_descent(bs, mods, episodes, seed, max_steps=300, wind=None, keep_traffic=False):
+    """keep_traffic: the traffic is cleared only before the first episode, as a driver of
+    the reference env would see it -- after a truncation the next reset keeps KL001
+    (descent_env.py:173 cre refused; the aircraft is only deleted on termination)."""
     m = mods["descent"]
     np.random.seed(seed)
     rng_act = np.random.default_rng(seed)
@@ -227,7 +230,8 @@ def gen_descent(bs, mods, episodes, seed, max_steps=300, wind=None):
     rec = {k: [] for k in ("spawn", "obs0", "actions", "obs", "reward", "terminated",
                            "truncated", "state", "info", "length")}
     for ep in range(episodes):
-        bs.traf.reset()   # reference reset() does not clear traffic (descent_env.py:162-182)
+        if ep == 0 or not keep_traffic:
+            bs.traf.reset()   # reference reset() does not clear traffic (descent_env.py:162-182)
         rs = np.random.RandomState()
         rs.set_state(np.random.get_state())
         spawn = ob.descent_spawn_from_np_random(rs)
@@ -248,6 +252,67 @@ def gen_descent(bs, mods, episodes, seed, max_steps=300, wind=None):
         pad = lambda a, shape, dt: np.concatenate([np.asarray(a, dt), np.zeros((max_steps - L,) + shape, dt)])
         rec["spawn"].append(spawn)
         rec["obs0"].append(flat(obs0, keys))
+        rec["actions"].append(acts)
+        rec["obs"].append(pad(O, (len(O[0]),), np.float64))
+        rec["reward"].append(pad(R, (), np.float64))
+        rec["terminated"].append(pad(T, (), np.int8))
+        rec["truncated"].append(pad(TR, (), np.int8))
+        rec["state"].append(pad(ST, ST[0].shape, np.float64))
+        rec["info"].append(pad(INF, (2,), np.float64))
+        rec["length"].append(L)
+    out = {k: np.stack(v) if k != "length" else np.array(v) for k, v in rec.items()}
+    out["seed"] = np.array(seed)
+    return out
+
+
+def _plan_greedy(obs):
+    """Steer at the nearest unreached waypoint (drift from the obs' cos/sin terms)."""
+    d = np.where(np.asarray(obs["waypoint_reached"]) == 0, np.asarray(obs["waypoint_distance"]), np.inf)
+    k = int(np.argmin(d))
+    drift = np.degrees(np.arctan2(obs["sin_difference"][k], obs["cos_difference"][k]))
+    return np.array([np.clip(-drift / 45.0, -1.0, 1.0)])
+
+
+def gen_plan(bs, mods, episodes, seed, max_steps=300, wind=None, greedy=False):
+    """PlanWaypointEnv-v0 driven as one env instance over consecutive episodes (traffic
+    cleared only before the first): truncated episodes hand their aircraft to the next
+    (plan_waypoint_env.py:164 cre refused), terminated ones delete it (:189-193)."""
+    m = mods["plan"]
+    np.random.seed(seed)
+    rng_act = np.random.default_rng(seed)
+    env, keys = _wrap(mods, m.PlanWaypointEnv(), ob.PLAN_OBS_KEYS, wind)
+    rec = {k: [] for k in ("spawn", "obs0", "actions", "obs", "reward", "terminated",
+                           "truncated", "state", "info", "length", "wpt", "state0")}
+    bs.traf.reset()
+    for ep in range(episodes):
+        rs = np.random.RandomState()
+        rs.set_state(np.random.get_state())
+        spawn = ob.plan_spawn_from_np_random(rs)
+        obs0, _ = env.reset()
+        obs = obs0
+        base = env.unwrapped if hasattr(env, "unwrapped") else env
+        wpt = np.concatenate([np.asarray(base.wpt_lat, np.float64), np.asarray(base.wpt_lon, np.float64)])
+        st0 = snap(bs)
+        acts = rng_act.uniform(-1, 1, (max_steps, 1))
+        O, R, T, TR, ST, INF = [], [], [], [], [], []
+        for t in range(max_steps):
+            pre = snap(bs)
+            if greedy:
+                acts[t] = _plan_greedy(obs)
+            obs, rew, term, trunc, info = _step(env, acts[t])
+            trunc = (t + 1) >= max_steps
+            O.append(flat(obs, keys)); R.append(rew); T.append(int(term))
+            TR.append(trunc)
+            INF.append([info["total_reward"], info["waypoints_completed"]])
+            ST.append(snap(bs) if bs.traf.ntraf else pre)
+            if term or trunc:
+                break
+        L = len(O)
+        pad = lambda a, shape, dt: np.concatenate([np.asarray(a, dt), np.zeros((max_steps - L,) + shape, dt)])
+        rec["spawn"].append(spawn)
+        rec["obs0"].append(flat(obs0, keys))
+        rec["wpt"].append(wpt)
+        rec["state0"].append(st0)
         rec["actions"].append(acts)
         rec["obs"].append(pad(O, (len(O[0]),), np.float64))
         rec["reward"].append(pad(R, (), np.float64))
@@ -450,12 +515,19 @@ def main():
         ("wind_descent", lambda: {**gen_descent(bs, mods, 3, 11, wind=WIND_ONE),
                                   **wind_record(WIND_ONE)}),
         ("static", lambda: gen_static(bs, mods, 3, 14)),
+        ("descent_keep", lambda: gen_descent(bs, mods, 4, 16, max_steps=25, keep_traffic=True)),
+        ("plan", lambda: gen_plan(bs, mods, 4, 17, max_steps=60)),
+        ("plan_long", lambda: gen_plan(bs, mods, 2, 18)),
+        ("plan_greedy", lambda: gen_plan(bs, mods, 4, 19, max_steps=120, greedy=True)),
         ("sector_N32", lambda: gen_sector(bs, mods, 3, 15)),
         ("noisy_merge_N8", lambda: gen_noisy_merge(bs, mods, 8, 2, 13, 0.2)),
         ("wind_horizontal_N6", lambda: {**gen_horizontal(bs, mods, 5, 2, 12, wind=WIND_README),
                                         **wind_record(WIND_README)}),
     ]
+    only = set(sys.argv[1:])            # optional: regenerate just these names
     for name, job in jobs:
+        if only and name not in only:
+            continue
         out = job()
         np.savez_compressed(os.path.join(HERE, name + ".npz"), **out)
         print(name, "episodes", len(out["length"]), "lengths", out["length"].tolist())

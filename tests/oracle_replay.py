@@ -164,6 +164,45 @@ def replay_sector(g, autoreset=ob.AUTORESET_NONE):
     return {k: (np.stack(v, 1) if k != "obs0" else v) for k, v in out.items()}
 
 
+def replay_sequential(o, g, info_keys):
+    """One env driven over the golden's consecutive episodes (reset from each spawn row,
+    then the recorded steps) -- the goldens of the envs whose reset keeps a truncated
+    episode's aircraft (descent_keep, plan*: make_golden.py gen_plan / keep_traffic)."""
+    _apply_wind(o, g)
+    n_ep, T = g["actions"].shape[:2]
+    out = {k: np.zeros_like(g[k]) for k in ("obs0", "obs", "reward", "state", "info")}
+    out["terminated"] = np.zeros_like(g["terminated"])
+    out["truncated"] = np.zeros_like(g["truncated"])
+    wpt = []
+    for ep in range(n_ep):
+        out["obs0"][ep] = o.reset(spawn=g["spawn"][ep:ep + 1])["obs"][0]
+        if hasattr(o, "wpt_lat"):
+            wpt.append(np.concatenate([np.ravel(o.wpt_lat[0]), np.ravel(o.wpt_lon[0])]))
+        for t in range(int(g["length"][ep])):
+            r = o.step(g["actions"][ep, t][None])
+            out["obs"][ep, t] = r["obs"][0]
+            out["reward"][ep, t] = r["reward"][0]
+            out["terminated"][ep, t] = r["terminated"][0]
+            out["truncated"][ep, t] = r["truncated"][0]
+            out["state"][ep, t] = np.stack([o.st.lat, o.st.lon, o.st.alt, o.st.hdg, o.st.tas,
+                                            o.st.cas, o.st.vs], 1)[0]
+            inf = o.info()
+            out["info"][ep, t] = [inf[k][0] for k in info_keys]
+    if wpt:
+        out["wpt"] = np.stack(wpt)
+    return out
+
+
+def replay_plan(g):
+    o = ob.PlanWaypointOracle(1, autoreset=ob.AUTORESET_NONE, max_episode_steps=g["actions"].shape[1])
+    return replay_sequential(o, g, ("total_reward", "waypoints_completed"))
+
+
+def replay_descent_keep(g):
+    o = ob.DescentOracle(1, autoreset=ob.AUTORESET_NONE, max_episode_steps=g["actions"].shape[1])
+    return replay_sequential(o, g, ("total_reward", "final_altitude"))
+
+
 def step_mask(g):
     """[n_ep, T] bool: steps inside each recorded episode."""
     T = g["actions"].shape[1]

@@ -25,10 +25,10 @@ def test_register_envs_matches_reference_ids_and_limits():
     for k, v in expect.items():
         assert reg[k].max_episode_steps == v
         assert reg[k].entry_point.startswith("bluesky_gym.envs.")
-    for k in ("MergeEnv-v0", "VerticalCREnv-v0", "DescentEnv-v0", "HorizontalCREnv-v0",
-              "StaticObstacleEnv-v0", "SectorCREnv-v0"):
+    for k in expect:
         assert reg[k].vector_entry_point.startswith("bluesky_gym.vector:")
-    with pytest.raises(NotImplementedError):
+    # no HIP device here: every env id fails loudly instead of falling back to the CPU
+    with pytest.raises(nat.BsgError):
         _gym.make("PlanWaypointEnv-v0")
 
 
@@ -46,6 +46,9 @@ def test_obs_layout_keys_sorted_like_gymnasium():
     assert list(so.keys) == list(oba.STATIC_OBS_KEYS) and so.dim == 43
     sc = ObsLayout(nat.ENV_SECTOR_CR, 32, 4)
     assert list(sc.keys) == list(oba.SECTOR_OBS_KEYS) and sc.dim == 31
+    pw = ObsLayout(nat.ENV_PLAN_WAYPOINT, 1, 0)
+    assert list(pw.keys) == list(ob.PLAN_OBS_KEYS) and pw.dim == 20
+    assert pw.bounds["waypoint_reached"] == (0, 1)
     w = ObsLayout(nat.ENV_MERGE, 20, 5, wind=True)
     assert w.dim == 42 and w.slices["wind_u"] == slice(30, 31)
     space = m.observation_space(_gym.spaces)
@@ -109,3 +112,13 @@ def test_sector_host_spawn_consumes_np_random_like_reference():
     np.random.seed(int(g["seed"]))
     for ep in range(len(g["length"])):
         assert np.array_equal(areas.sector_spawn(int(g["num_ac"])), g["spawn"][ep])
+
+
+@pytest.mark.parametrize("name", ["plan", "plan_greedy"])
+def test_plan_host_spawn_consumes_np_random_like_reference(name):
+    """spawn.plan_spawn draws (distance, bearing) per waypoint from the legacy global
+    np.random like plan_waypoint_env.py:205-206: seeding it reproduces the golden rows."""
+    g = dict(np.load(f"{GOLD}/{name}.npz"))
+    np.random.seed(int(g["seed"]))
+    for ep in range(len(g["length"])):
+        assert np.array_equal(spawn.plan_spawn(), g["spawn"][ep])

@@ -100,6 +100,29 @@ def test_horizontal_oracle_matches_reference(name):
     assert np.array_equal(r["intr"][nt], g["intr"][nt])
 
 
+@pytest.mark.parametrize("name", ["plan", "plan_long", "plan_greedy", "descent_keep"])
+def test_kept_aircraft_oracle_matches_reference(name):
+    """One env over consecutive episodes: a truncated episode's aircraft carries into the
+    next reset (descent_env.py:173, plan_waypoint_env.py:164 cre refused), a terminated
+    one is deleted and re-created (descent_env.py:201-204, plan_waypoint_env.py:189-193)."""
+    g = load(name)
+    r = rp.replay_descent_keep(g) if name == "descent_keep" else rp.replay_plan(g)
+    m = rp.step_mask(g)
+    assert np.array_equal(r["obs0"], g["obs0"])
+    if "wpt" in g:
+        assert np.array_equal(r["wpt"], g["wpt"])
+    for k in ("obs", "reward", "info"):
+        assert np.array_equal(r[k][m], g[k][m]), k
+    assert np.array_equal(r["terminated"][m], g["terminated"][m])
+    assert np.array_equal(r["truncated"][m], g["truncated"][m])
+    nt = _nonterminal(g)
+    assert np.array_equal(r["state"][nt], g["state"][nt])
+    # the quirk is exercised: some episode starts from a kept (moved) aircraft
+    ends = g["length"] - 1
+    kept = [ep for ep in range(1, len(ends)) if g["truncated"][ep - 1, ends[ep - 1]]]
+    assert kept
+
+
 def _eq_obs(r, g, m):
     """Equal observations; the NaN wind keys of a terminal step (the reference wrapper
     raises there, tests/golden/make_golden.py:_step) are excluded."""
