@@ -23,6 +23,7 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path[:0] = [REPO, os.path.join(REPO, "bluesky-gym-hallucination_amd")]
 
 METRIC = "env steps/sec (whole node), MergeEnv-v0 4096 envs × 32 aircraft, 1/2/4/8 GPUs"
+TIMING_EVERY = 10              # HIP event pair around every 10th launch of the timed region
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md, chip table)
 
 
@@ -44,15 +45,16 @@ def layout_bytes_per_env_step(N, A=2, O=40, K=5, cd=True):
     return b
 
 
-def cpu_baseline(seconds: float):
-    """Time the CPU oracle (batched NumPy restatement, 1 core) on a bounded sample of
-    the same workload: 128 Merge envs x 32 aircraft, CD on, NEXT_STEP autoreset."""
+def _cpu_worker(args):
+    """One host core: the batched NumPy oracle on 128 Merge envs x 32 aircraft, CD on,
+    NEXT_STEP autoreset, stepped for `seconds`.  Returns (env-steps, elapsed s)."""
+    seconds, seed = args
     import numpy as np
     from oracle import batched as ob
     E = 128
-    o = ob.MergeOracle(E, num_ac=32, seed=11, compute_cd=True)
+    o = ob.MergeOracle(E, num_ac=32, seed=seed, compute_cd=True)
     o.reset()
-    rng = np.random.default_rng(0)
+    rng = np.random.default_rng(seed)
     o.step(rng.uniform(-1, 1, (E, 2)))
     n = 0
     t0 = time.perf_counter()
@@ -61,7 +63,29 @@ def cpu_baseline(seconds: float):
         n += 1
         el = time.perf_counter() - t0
         if el >= seconds and n >= 3:
-            break
+            return E * n, el
+
+
+def cpu_baseline(seconds: float):
+    """Time the CPU oracle on the host cores of this box on a bounded sample of the same
+    workload: one process per core (the reference's SubprocVecEnv layout,
+    scripts/multi_processing_example.py:51-53), each stepping the batched NumPy
+    restatement (oracle/batched.py, the fastest CPU form of the path) on 128 Merge envs x
+    32 aircraft with CD on for `seconds`.  Runs before anything touches the GPU (the
+    workers are forked).  value = sum of the per-core rates."""
+    import multiprocessing as mp
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count() or 1
+    # the GPU box's CPU share is 16 per GPU (os.cpu_count() there is the whole machine)
+    P = max(1, min(int(os.environ.get("BENCH_CPU_WORKERS", "16")), avail))
+    for v in ("OMP_NUM_THREADS", "OPENBLAS_NUM_THREADS", "MKL_NUM_THREADS"):
+        os.environ[v] = "1"
+    with mp.get_context("fork").Pool(P) as pool:
+        res = pool.map(_cpu_worker, [(seconds, 11 + w) for w in range(P)])
+    value = sum(n / el for n, el in res)
+    per = [n / el for n, el in res]
     model = platform.processor() or "unknown"
     try:
         with open("/proc/cpuinfo") as f:
@@ -71,10 +95,11 @@ def cpu_baseline(seconds: float):
                     break
     except OSError:
         pass
-    return {"value": E * n / el, "unit": "env_steps/s", "cores": 1, "kind": "port",
-            "sample": f"oracle/batched.py MergeOracle {E} envs x 32 aircraft, CD on, "
-                      f"{n} steps in {el:.1f} s, NumPy fp64 single thread on '{model}' "
-                      f"(host has {os.cpu_count()} logical CPUs)"}
+    return {"value": value, "unit": "env_steps/s", "cores": P, "kind": "port",
+            "sample": f"oracle/batched.py MergeOracle, {P} processes x 128 envs x 32 aircraft, "
+                      f"CD on, {seconds:.0f} s each ({min(per):.0f}-{max(per):.0f} env-steps/s "
+                      f"per core), NumPy fp64 one thread per process on '{model}' "
+                      f"({avail} CPUs available to this process, {os.cpu_count()} on the host)"}
 
 
 def load_profile(E):
@@ -105,13 +130,16 @@ def main():
     ap.add_argument("--skip-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    # CPU baseline first, on rank 0 at N=1 only, before anything initialises the GPU
+    cpu = None if (world > 1 or args.skip_cpu_baseline) else cpu_baseline(args.cpu_seconds)
+
     import torch
     import torch.distributed as dist
     from bluesky_gym.parallel import ShardedVectorEnv
     from bluesky_gym.vector import MergeVectorEnv
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # BENCH_BACKEND=gloo rehearses the multi-rank path on fewer GPUs than ranks (test only)
     backend = os.environ.get("BENCH_BACKEND", "nccl")
@@ -153,7 +181,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     batch.step_timing()                       # discard
-    batch.set_timing(True)
+    batch.set_timing(TIMING_EVERY)
     t0 = time.perf_counter()
     for k in range(args.steps):
         one(k)
@@ -218,13 +246,15 @@ def main():
                 "traffic": prof["hbm_bytes_per_launch"] if prof else None,
                 "kernel": "bsg::step_kernel<MERGE,32>",
                 "kernel_avg_ms": kern_avg_ms,
+                "kernel_timing": f"HIP event pair on the launch stream around every "
+                                 f"{TIMING_EVERY}th launch of the timed region ({launches} launches)",
                 "bytes_per_env_step": B,
                 "layout_bytes_per_env_step": layout_bytes_per_env_step(N, cd=not args.no_cd),
                 "valu": valu,
             },
         }
-        if world == 1 and not args.skip_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+        if cpu is not None:
+            out["cpu_baseline"] = cpu
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()

@@ -180,8 +180,9 @@ class DeviceBatch:
             raise nat.BsgError(f"spawn must be [{self.E}, {self.spawn_width}], got {tuple(sp.shape)}")
         return sp
 
-    def set_timing(self, enable: bool):
-        nat.check(self.lib.bsg_set_timing(self._ctx, int(enable)), "bsg_set_timing")
+    def set_timing(self, every: int | bool):
+        """HIP event pair around every `every`-th launch (True = 1 = every launch, 0 = off)."""
+        nat.check(self.lib.bsg_set_timing(self._ctx, int(every)), "bsg_set_timing")
 
     def step_timing(self):
         """(total kernel ms, launches) since the last call (HIP events on the launch stream)."""

@@ -23,8 +23,10 @@ struct bsg_ctx {
   int spawn_width = 0;
   bsg::Route route{};
   bsg::WindDev wind{};
-  // optional per-launch timing (bsg_set_timing)
-  bool timing = false;
+  // optional per-launch timing (bsg_set_timing): an event pair around every
+  // `timing`-th launch (0 = off)
+  int timing = 0;
+  long long launch_count = 0;
   unsigned long long* stamps = nullptr;
   unsigned lds_pad = 0;
   std::vector<hipEvent_t> ev_pool;
@@ -99,7 +101,8 @@ int launch(bsg_ctx* c, const bsg::KParams& p, void* stream) {
   if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   hipEvent_t t0 = nullptr, t1 = nullptr;
-  if (c->timing) {
+  const bool timed = c->timing > 0 && (c->launch_count++ % c->timing) == 0;
+  if (timed) {
     t0 = take_event(c);
     t1 = take_event(c);
     if (!t0 || !t1) return fail(BSG_E_HIP, "hipEventCreate failed%s%lld");
@@ -107,7 +110,7 @@ int launch(bsg_ctx* c, const bsg::KParams& p, void* stream) {
   }
   e = bsg::launch_step(p, st);
   if (e != hipSuccess) return hip_fail(e, "kernel launch");
-  if (c->timing) {
+  if (timed) {
     if ((e = hipEventRecord(t1, st)) != hipSuccess) return hip_fail(e, "hipEventRecord");
     c->pending.emplace_back(t0, t1);
   }
@@ -316,7 +319,9 @@ int32_t bsg_set_stamps(bsg_ctx* c, void* buf) {
 
 int32_t bsg_set_timing(bsg_ctx* c, int32_t enable) {
   if (!c) return fail(BSG_E_INVALID_ARG, "bsg_set_timing: null ctx%s%lld");
-  c->timing = enable != 0;
+  if (enable < 0) return fail(BSG_E_INVALID_ARG, "bsg_set_timing: negative interval%s%lld");
+  c->timing = enable;
+  c->launch_count = 0;
   return BSG_OK;
 }
 

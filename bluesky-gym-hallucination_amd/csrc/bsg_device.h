@@ -218,6 +218,22 @@ __device__ __forceinline__ void qdrdist_cached(double latd1, double lond1, doubl
                                                double sinlat1, double latd2, double lond2,
                                                double coslat2, double sinlat2, double far_m,
                                                double* qdr, double* distnm) {
+  double sdl, cdl;
+  sincos(lond2 * kD2R - lond1 * kD2R, &sdl, &cdl);
+  *qdr = atan2(sdl * coslat2, coslat1 * sinlat2 - sinlat1 * coslat2 * cdl) * kR2D;
+  // d = r*acos(x) is only compared against thresholds by the caller; when it is provably
+  // beyond `far_m` the WGS84 radius and the acos are skipped and +inf returned:
+  //  - the meridian gap alone: great-circle >= r*|dphi|, r >= b (1e-6 relative margin);
+  //  - the computed x itself: with t = far_m/b, x < 1 - t^2/2 <= cos(t) gives
+  //    acos(x) > t, so d >= b*t = far_m (the 1e-12 margin covers acos's ulp error;
+  //    the caller's thresholds sit >= 1 m inside far_m).  x is bit-identical to the
+  //    argument the full path would pass to acos.
+  const double x = coslat1 * coslat2 * cdl + sinlat1 * sinlat2;
+  const double t = far_m * (1.0 / 6356752.314245);
+  if (b_times_dphi_far(latd1, latd2, far_m) || x < (1.0 - 0.5 * t * t) - 1e-12) {
+    *distnm = __builtin_inf();
+    return;
+  }
   bool sw = (latd1 * latd2 >= 0.0);
   double r;
   if (sw) {
@@ -229,17 +245,7 @@ __device__ __forceinline__ void qdrdist_cached(double latd1, double lond1, doubl
     r = 0.5 * (fabs(latd1) * (r1 + a) + fabs(latd2) * (r2 + a)) /
         npmax(0.000001, fabs(latd1) + fabs(latd2));
   }
-  double sdl, cdl;
-  sincos(lond2 * kD2R - lond1 * kD2R, &sdl, &cdl);
-  *qdr = atan2(sdl * coslat2, coslat1 * sinlat2 - sinlat1 * coslat2 * cdl) * kR2D;
-  // d = r*acos(.) is only compared against thresholds by the caller; when the meridian
-  // gap alone puts it beyond `far_m` (great-circle >= r*|dphi|, r >= b, with a 1e-6
-  // relative margin) the acos is skipped and +inf returned.
-  if (b_times_dphi_far(latd1, latd2, far_m)) {
-    *distnm = __builtin_inf();
-    return;
-  }
-  double d = r * acos(coslat1 * coslat2 * cdl + sinlat1 * sinlat2);
+  double d = r * acos(x);
   *distnm = d / NM;
 }
 

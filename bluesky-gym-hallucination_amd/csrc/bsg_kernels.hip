@@ -223,26 +223,32 @@ __device__ __forceinline__ void memo_init(Memo& m, const AC& s) {
   sincos(s.lat * kD2R, &m.sinlat, &m.coslat);
 }
 
-__device__ __forceinline__ void memo_load(Memo& m, const double* mc, size_t a, size_t stride) {
-  m.spd_bits = bits(mc[MC_SPD_SEL * stride + a]);
-  m.spdalt_bits = bits(mc[MC_SPD_ALT * stride + a]);
-  m.ap_tas = mc[MC_AP_TAS * stride + a];
+// issued at kernel entry together with the state loads (one memory round trip)
+__device__ __forceinline__ void memo_fetch(double v[MC_FIELDS], const double* mc, size_t a, size_t stride) {
+#pragma unroll
+  for (int f = 0; f < MC_FIELDS; ++f) v[f] = mc[f * stride + a];
+}
+
+__device__ __forceinline__ void memo_load(Memo& m, const double v[MC_FIELDS]) {
+  m.spd_bits = bits(v[MC_SPD_SEL]);
+  m.spdalt_bits = bits(v[MC_SPD_ALT]);
+  m.ap_tas = v[MC_AP_TAS];
   m.lim_tas_bits = bits(m.ap_tas);
-  m.lim_h_bits = bits(mc[MC_LIM_H * stride + a]);
-  m.allow_tas = mc[MC_ALLOW_TAS * stride + a];
-  m.cas_tas_bits = bits(mc[MC_CAS_TAS * stride + a]);
-  m.cas_alt_bits = bits(mc[MC_CAS_ALT * stride + a]);
+  m.lim_h_bits = bits(v[MC_LIM_H]);
+  m.allow_tas = v[MC_ALLOW_TAS];
+  m.cas_tas_bits = bits(v[MC_CAS_TAS]);
+  m.cas_alt_bits = bits(v[MC_CAS_ALT]);
 }
 
 // write back only the entries that changed (steady aircraft write nothing)
-__device__ __forceinline__ void memo_store(const Memo& m, double* mc, size_t a, size_t stride) {
+__device__ __forceinline__ void memo_store(const Memo& m, const double old[MC_FIELDS], double* mc,
+                                           size_t a, size_t stride) {
   const double v[MC_FIELDS] = {key_as_double(m.spd_bits), key_as_double(m.spdalt_bits), m.ap_tas,
                                key_as_double(m.lim_h_bits), m.allow_tas,
                                key_as_double(m.cas_tas_bits), key_as_double(m.cas_alt_bits)};
 #pragma unroll
   for (int f = 0; f < MC_FIELDS; ++f) {
-    double* q = mc + f * stride + a;
-    if (bits(*q) != bits(v[f])) *q = v[f];
+    if (bits(old[f]) != bits(v[f])) mc[f * stride + a] = v[f];
   }
 }
 
@@ -1202,38 +1208,41 @@ __device__ __forceinline__ void hdg_spd_action(const KParams& p, AC& s, double a
 // One RL step of aircraft (e, j) whose state is in s: the ownship's action decode (j == 0),
 // ACTION_FREQUENCY substeps with the cross-step memo, the deferred cas.  StaticObstacle also
 // evaluates its per-substep reward here (sub_reward / sub_done).
+template <int KIND>
+constexpr int kActDim = (KIND == BSG_ENV_MERGE || KIND == BSG_ENV_STATIC_OBSTACLE ||
+                         KIND == BSG_ENV_SECTOR_CR) ? 2 : 1;
+
+// act: the env's action row, mc: its memo-cache entries (both fetched at kernel entry)
 template <int KIND, bool WIND>
 __device__ __forceinline__ void propagate(const KParams& p, int e, int j, size_t a, AC& s,
-                                          EnvScalars& ev, double& sub_reward, bool& sub_done) {
+                                          EnvScalars& ev, double& sub_reward, bool& sub_done,
+                                          const double act[2], const double mc[MC_FIELDS]) {
   const Buffers& b = p.b;
   const int N = p.N;
   if (j == 0) {
     if constexpr (KIND == BSG_ENV_MERGE) {
-      hdg_spd_action<WIND>(p, s, p.actions[(size_t)e * 2 + 0], p.actions[(size_t)e * 2 + 1],
-                           15.0, 20.0);
+      hdg_spd_action<WIND>(p, s, act[0], act[1], 15.0, 20.0);
     } else if constexpr (KIND == BSG_ENV_STATIC_OBSTACLE) {
-      hdg_spd_action<WIND>(p, s, p.actions[(size_t)e * 2 + 0], p.actions[(size_t)e * 2 + 1],
-                           45.0, 20.0 / 3.0);
+      hdg_spd_action<WIND>(p, s, act[0], act[1], 45.0, 20.0 / 3.0);
     } else if constexpr (KIND == BSG_ENV_SECTOR_CR) {
-      hdg_spd_action<WIND>(p, s, p.actions[(size_t)e * 2 + 0], p.actions[(size_t)e * 2 + 1],
-                           22.5, 20.0 / 3.0);
+      hdg_spd_action<WIND>(p, s, act[0], act[1], 22.5, 20.0 / 3.0);
     } else if constexpr (KIND == BSG_ENV_HORIZONTAL_CR || KIND == BSG_ENV_PLAN_WAYPOINT) {
       // horizontal_cr_env.py:272-275 / plan_waypoint_env.py:148-154: HDG KL001
       // {hdg + a*45} (no wrap)
-      s.ap_trk = hdg_command_track<WIND>(p.wind, s, s.hdg + p.actions[e] * 45);
+      s.ap_trk = hdg_command_track<WIND>(p.wind, s, s.hdg + act[0] * 45);
       s.nav &= ~1;
     } else {
       // vertical_cr_env.py:242-256 / descent_env.py:146-160
-      const double act = p.actions[e] * 12.5;
-      if (act >= 0) { s.selalt = 1000000; s.selvs = act; }
-      else if (act < 0) { s.selalt = 0; s.selvs = act; }
+      const double act0 = act[0] * 12.5;
+      if (act0 >= 0) { s.selalt = 1000000; s.selvs = act0; }
+      else if (act0 < 0) { s.selalt = 0; s.selvs = act0; }
     }
   }
   const int S = p.cfg.action_frequency;
   if (S > 0) {
     Memo m;
     memo_init(m, s);
-    if (b.memo_cache) memo_load(m, b.memo_cache, a, (size_t)p.E * N);
+    if (b.memo_cache) memo_load(m, mc);
     RouteRegs rt;
     rt.load(p.route);
     const double dt = p.cfg.simdt;
@@ -1254,10 +1263,28 @@ __device__ __forceinline__ void propagate(const KParams& p, int e, int j, size_t
         if (ev.wpt_reach == 1 || nin > 0) { sub_done = true; break; }
       }
     } else {
+#if defined(BSG_NO_PRIO_BALANCE) && BSG_NO_PRIO_BALANCE
       for (int it = 0; it < S; ++it) substep<WIND>(s, m, dt, rt, p.wind);
+#else
+      // Balance the two waves that share a SIMD (4096 x 32 Merge: 2048 waves on 1024
+      // SIMDs).  VALU issue goes by priority, then age, so the older wave (slot 0) used to
+      // finish ~19 us before its partner, which then ran alone at half the issue rate
+      // (tools/stamps.py SIMD-pair report, profiles/r01/diag/prio_balance.txt).  Odd slots
+      // take priority for the first 3/4 of the substeps, even slots for the rest; the
+      // partners now finish ~5 us apart (-7 % kernel time).  Scheduling only: no effect on
+      // results.
+      const int slot = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (3 << 11)) & 15;  // HW_ID wave id
+      const int sw = (3 * S + 3) / 4;
+      for (int it = 0; it < S; ++it) {
+        if ((slot & 1) ? (it < sw) : (it >= sw)) __builtin_amdgcn_s_setprio(1);
+        else __builtin_amdgcn_s_setprio(0);
+        substep<WIND>(s, m, dt, rt, p.wind);
+      }
+      __builtin_amdgcn_s_setprio(0);
+#endif
     }
     memo_final_cas(m, s);
-    if (b.memo_cache) memo_store(m, b.memo_cache, a, (size_t)p.E * N);
+    if (b.memo_cache) memo_store(m, mc, b.memo_cache, a, (size_t)p.E * N);
   }
 }
 
@@ -1282,8 +1309,23 @@ __global__ __launch_bounds__(64) void step_kernel(KParams p) {
   const int O = p.obs_dim;
   const int K = p.K;
 
+  // every global read of phase A is issued here, before any of it is needed, so the
+  // wave pays one memory round trip: env scalars, the aircraft (speculatively -- a
+  // respawned aircraft discards it), the action row and the memo-cache entries
   EnvScalars ev = {};
   if (env_ok) load_env(b, e, ev);
+  AC s_in = {};
+  if (ok) load_ac<WIND>(b, a, s_in);
+  double act[2] = {0.0, 0.0};
+  if (env_ok && p.mode == MODE_STEP) {
+#pragma unroll
+    for (int k = 0; k < kActDim<KIND>; ++k) act[k] = p.actions[(size_t)e * kActDim<KIND> + k];
+  }
+  double mc[MC_FIELDS];
+#pragma unroll
+  for (int f = 0; f < MC_FIELDS; ++f) mc[f] = key_as_double(kNoKey);
+  if (ok && b.memo_cache && p.mode == MODE_STEP && p.cfg.action_frequency > 0)
+    memo_fetch(mc, b.memo_cache, a, (size_t)p.E * N);
   ev.nac = N;
   if constexpr (KIND == BSG_ENV_SECTOR_CR) {
     if (env_ok) {
@@ -1311,19 +1353,18 @@ __global__ __launch_bounds__(64) void step_kernel(KParams p) {
   double sub_reward = 0.0;          // StaticObstacle: reward / done of the last substep
   bool sub_done = false;
   {
-    AC s = {};
     double aux[4] = {ev.target_alt, 0.0, 0.0, 0.0};
     if constexpr (KIND == BSG_ENV_SECTOR_CR) sector_reset_plan<GS>(p, e, j, g, resetting, ev, aux);
     const bool on = ok && j < ev.nac;   // SectorCR: aircraft slot in use this episode
+    const bool keep = kKeepsAircraft<KIND> && (ev.flags & BSG_FLAG_AC_PRESENT);
+    AC s = (!resetting || keep) ? s_in : AC{};
     if (ok) {
-      const bool keep = kKeepsAircraft<KIND> && (ev.flags & BSG_FLAG_AC_PRESENT);
-      if (!resetting || keep) load_ac<WIND>(b, a, s);
       if (resetting) spawn<KIND>(p, e, j, ev.episode, s, aux, keep);
 #if defined(BSG_EXP_SKIP_OWN) && BSG_EXP_SKIP_OWN
       // experiment build only (tools/ablate.py): the ownship does not move
-      if (stepping && on && j != 0) propagate<KIND, WIND>(p, e, j, a, s, ev, sub_reward, sub_done);
+      if (stepping && on && j != 0) propagate<KIND, WIND>(p, e, j, a, s, ev, sub_reward, sub_done, act, mc);
 #else
-      if (stepping && on) propagate<KIND, WIND>(p, e, j, a, s, ev, sub_reward, sub_done);
+      if (stepping && on) propagate<KIND, WIND>(p, e, j, a, s, ev, sub_reward, sub_done, act, mc);
 #endif
       if (active) store_ac<WIND>(b, a, s);
       if (resetting && b.memo_cache) memo_invalidate(b.memo_cache, a, (size_t)p.E * N);
@@ -1631,6 +1672,9 @@ template <int KIND, bool WIND>
 static hipError_t launch_kind_w(const KParams& p, hipStream_t st) {
   int gs = 1;
   while (gs < p.N) gs <<= 1;
+#if defined(BSG_EXP_GS64) && BSG_EXP_GS64
+  gs = 64;   // experiment: one env per wave (upper lanes idle)
+#endif
   const int epb = 64 / gs;
   const int grid = (p.E + epb - 1) / epb;
 #define BSG_CASE(G) \
@@ -1657,10 +1701,10 @@ static hipError_t launch_kind(const KParams& p, hipStream_t st) {
 
 hipError_t launch_step(const KParams& p, hipStream_t st) {
 #if defined(BSG_ONLY_MERGE) && BSG_ONLY_MERGE
-  // experiment builds (tools/flag_sweep.sh): Merge only, for fast compiler-flag sweeps
+  // experiment builds (tools/flag_sweep.sh, tools/variants.sh): Merge only, for fast sweeps
   if (p.cfg.env_kind == BSG_ENV_MERGE) return launch_kind<BSG_ENV_MERGE>(p, st);
   return hipErrorInvalidValue;
-#endif
+#else
   switch (p.cfg.env_kind) {
     case BSG_ENV_MERGE: return launch_kind<BSG_ENV_MERGE>(p, st);
     case BSG_ENV_VERTICAL_CR: return launch_kind<BSG_ENV_VERTICAL_CR>(p, st);
@@ -1671,6 +1715,7 @@ hipError_t launch_step(const KParams& p, hipStream_t st) {
     case BSG_ENV_PLAN_WAYPOINT: return launch_kind<BSG_ENV_PLAN_WAYPOINT>(p, st);
     default: return hipErrorInvalidValue;
   }
+#endif
 }
 
 }  // namespace bsg

@@ -224,9 +224,12 @@ int32_t bsg_set_wind(bsg_ctx* ctx, const bsg_wind* wind);
 /* Observation row length of this ctx (bsg_obs_dim + 2 with an augmenting wind field). */
 int32_t bsg_ctx_obs_dim(const bsg_ctx* ctx);
 
-/* Kernel-time instrumentation: record a HIP event pair around each step launch on the
- * launch stream; bsg_last_step_ms() returns the elapsed time of the most recent
- * completed pair (synchronises on that event only).  enable=0 turns it off. */
+/* Kernel-time instrumentation: record a HIP event pair on the launch stream around every
+ * `enable`-th step/reset launch (1 = every launch, k = launches 0, k, 2k, ... after the
+ * call; 0 = off).  An event pair adds ~8 us of stream serialisation to the launch it
+ * brackets, so throughput runs sample (bench.py: every 10th).  bsg_step_timing returns
+ * the summed elapsed ms and the number of timed launches since its last call
+ * (synchronises on those events). */
 int32_t bsg_set_timing(bsg_ctx* ctx, int32_t enable);
 int32_t bsg_step_timing(bsg_ctx* ctx, double* total_ms, int32_t* launches);
 

@@ -1,5 +1,6 @@
 """Time DeviceBatch.step under configuration ablations (kernel time via HIP events)."""
-import sys, os, json
+import sys, os, json, time
+WALL = [0.0]
 sys.path[:0] = [os.getcwd(), os.path.join(os.getcwd(), "bluesky-gym-hallucination_amd")]
 import torch
 from bluesky_gym import core, config
@@ -16,6 +17,12 @@ def run(cfg, E, cd, steps=60, warm=10):
         b.step(act[k % 8])
     torch.cuda.synchronize()
     ms, n = b.step_timing()
+    b.set_timing(False)
+    t0 = time.perf_counter()
+    for k in range(steps):
+        b.step(act[k % 8])
+    torch.cuda.synchronize()
+    WALL[0] = (time.perf_counter() - t0) / steps * 1e3
     return ms / n
 
 only = set(sys.argv[1:])
@@ -36,5 +43,5 @@ for name, cfg, E, cd in [
     if only and name not in only:
         continue
     res[name] = run(cfg, E, cd)
-    print(name, f"{res[name]*1e3:.1f} us", flush=True)
+    print(name, f"{res[name]*1e3:.1f} us  (wall/step untimed {WALL[0]*1e3:.1f} us)", flush=True)
 json.dump(res, open(os.environ.get("ABLATE_OUT", "gpurun_out/ablate.json"), "w"), indent=1)

@@ -113,3 +113,28 @@ for run in range(5):
         print(f"   waves sharing a SIMD={w}: n={sel.sum():5d}  life us p50 {np.median(life[s][sel]):6.1f} "
               f"max {life[s][sel].max():6.1f}   cycles p50 {np.median(tot_c[s][sel]):8.0f} "
               f"max {tot_c[s][sel].max():8.0f}")
+# per-SIMD pairs (run 0..4): the earlier- and later-finishing wave of each 2-wave SIMD and
+# their wave slot ids (HW_ID bits 3:0) -- tests the age-priority arbitration hypothesis
+slot = hid & 15
+first_l, second_l, first_s, second_s, start_gap = [], [], [], [], []
+for run in range(5):
+    s = np.arange(run * grid, (run + 1) * grid)
+    key = (((xcc[s] * 8 + se[s]) * 2 + sh[s]) * 16 + cu[s]) * 4 + simd[s]
+    order = np.argsort(key, kind="stable")
+    ks = key[order]
+    for i in range(len(ks) - 1):
+        if ks[i] == ks[i + 1] and (i == 0 or ks[i - 1] != ks[i]) and (i + 2 >= len(ks) or ks[i + 2] != ks[i]):
+            a, bb = s[order[i]], s[order[i + 1]]
+            if rt1[a] > rt1[bb]:
+                a, bb = bb, a
+            first_l.append(life[a]); second_l.append(life[bb])
+            first_s.append(slot[a]); second_s.append(slot[bb])
+            start_gap.append((rt0[bb] - rt0[a]) * 10 / 1000)
+first_l = np.array(first_l); second_l = np.array(second_l)
+print("2-wave SIMDs:", len(first_l))
+print("  first-finishing wave life ns ", pct(first_l * 1000))
+print("  second-finishing wave life ns", pct(second_l * 1000))
+print("  start(second) - start(first) ns", pct(np.array(start_gap) * 1000))
+print("  slot pairs (first,second) most common:",
+      sorted(zip(*np.unique(np.stack([first_s, second_s], 1), axis=0, return_counts=True)),
+             key=lambda t: -t[1])[:6])

@@ -1,0 +1,23 @@
+#!/bin/bash
+# Merge-only experiment builds of several kernel source trees for A/B timing.
+#   build (CPU container):  bash tools/variants.sh build NAME=SRC_CSRC_DIR ...
+#   time  (GPU box):        bash tools/variants.sh run NAME ...
+set -euo pipefail
+OUT=build/variants
+FLAGS="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -fno-fast-math -Wall -Wno-unused-function -mllvm -disable-machine-licm -DBSG_ONLY_MERGE=1 ${XFLAGS:-}"
+mode=$1; shift
+if [ "$mode" = build ]; then
+  mkdir -p $OUT
+  for kv in "$@"; do
+    k=${kv%%=*}; d=${kv#*=}; x=""
+    case "$d" in *:*) x=${d#*:}; d=${d%%:*};; esac
+    /opt/rocm/bin/hipcc $FLAGS $x -shared -o $OUT/libbsg_$k.so $d/bsg_kernels.hip -x hip $d/bsg_abi.cpp &
+  done
+  wait
+  ls -la $OUT
+else
+  for k in "$@"; do
+    echo "== $k"
+    BSG_LIBRARY=$PWD/$OUT/libbsg_$k.so ABLATE_OUT=gpurun_out/var_$k.json timeout -k 10 200 python tools/ablate.py ${ABL:-merge32_full merge32_nocd}
+  done
+fi
