@@ -481,10 +481,17 @@ __device__ __forceinline__ double cd_v(const LT& L, int i) {
 // holds a lane hostage to a near one.  Row masks / tcpamax / per-env min separation are
 // assembled with LDS atomics (u64 or / min / max; tcpa > 0 and dist >= 0 order like u64).
 
-// true unless the pair is provably outside the horizon.  Skip => computed
-// dist >= Re*|dlat|*(1-1e-14) > Re*|dlat|*0.999998 - 1 >= computed horizon.
-__device__ __forceinline__ bool cd_candidate(double dlat, double dv2f) {
-  const double a = 6371000.0 * fabs(dlat) * 0.999998 - 1.0;
+// true unless the pair is provably outside the horizon.  dlat is the pair's computed
+// latitude gap (rad), dlonc a lower bound of |dlon|*cavelat of cd_pair: the wrapped
+// longitude gap less 1e-9 deg (pymod's rounding is ~1e-13 deg) times 1 - x^2/2 <= cos(x)
+// at x = max(|lat_i|, |lat_k|) >= |mean latitude| (less 1e-9 relative).  So
+// a = Re*sqrt(dlat^2 + dlonc^2) is a lower bound of the computed dist; the fp32 square
+// root (<= 1.2e-7 relative with the conversion) sits far inside the 0.999998 factor.
+// Skip => computed dist >= a*0.999998 - 1 + 1 > computed horizon.
+__device__ __forceinline__ bool cd_candidate(double dlat, double dlonc, double dv2f) {
+  const double D2 = dlat * dlat + dlonc * dlonc;
+  const double sq = (double)__fsqrt_rn((float)D2);
+  const double a = 6371000.0 * sq * 0.999998 - 1.0;
   const double w = (a * 0.999999 - RPZ) * (1.0 / DTLOOKAHEAD);
   return !(w > 0.0 && w * w > dv2f * 1.000001);
 }
@@ -1410,19 +1417,41 @@ __global__ __launch_bounds__(64) void step_kernel(KParams p) {
     L.lm[lane] = 0ull;
     L.tmax[lane] = 0ull;                                   // bits of +0.0
     L.gmin[lane] = bits(__builtin_inf());
-    // phase 1: candidate pairs of row j (no transcendentals)
+    // phase 1: candidate pairs (no transcendentals).  The bound is symmetric in (i, k)
+    // bit for bit, so each unordered pair is tested once: lane j takes the ring offsets
+    // 1..nac/2 (16 per lane at N = 32, balanced) and ORs the mirrored bit into lane k's
+    // LDS word (L.lm, re-zeroed before phase 2).
+    __syncthreads();
     uint64_t cand = 0;
     if (on) {
-      const double lati = L.lat[lane], ui = cd_u(L, lane), vi = cd_v(L, lane);
-      for (int k = 0; k < ev.nac; ++k) {
+      const int nac = ev.nac;
+      const double lati = L.lat[lane], loni = L.lon[lane];
+      const double ui = cd_u(L, lane), vi = cd_v(L, lane);
+      const double ali = fabs(lati);
+      for (int sft = 1; 2 * sft <= nac; ++sft) {
+        if (2 * sft == nac && j >= sft) break;          // pair (j, j + nac/2) once
+        int k = j + sft;
+        if (k >= nac) k -= nac;
         const int lk = base + k;
-        const double dlat = (L.lat[lk] - lati) * kD2R;
+        const double latk = L.lat[lk];
+        const double dlat = (latk - lati) * kD2R;
+        double dl = fabs(L.lon[lk] - loni);
+        dl = dl > 180.0 ? 360.0 - dl : dl;
+        const double dlon = npmax(dl - 1e-9, 0.0) * kD2R;
+        const double x = npmax(ali, fabs(latk)) * kD2R;
+        const double c = npmax((1.0 - 0.5 * x * x) * (1.0 - 1e-9) - 1e-12, 0.0);
         const double du = cd_u(L, lk) - ui, dv = cd_v(L, lk) - vi;
         double dv2 = du * du + dv * dv;
         dv2 = fabs(dv2) < 1e-6 ? 1e-6 : dv2;
-        if (k != j && cd_candidate(dlat, dv2)) cand |= 1ull << k;
+        if (cd_candidate(dlat, dlon * c, dv2)) {
+          cand |= 1ull << k;
+          atomicOr(&L.lm[lk], 1ull << j);
+        }
       }
     }
+    __syncthreads();
+    cand |= L.lm[lane];
+    L.lm[lane] = 0ull;
     const int cnt = __popcll(cand);
     int incl = cnt;
 #pragma unroll

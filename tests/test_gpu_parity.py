@@ -277,3 +277,46 @@ def test_merge_full_size_subset_parity(bg):
     # near-threshold pair, so only require near-symmetry
     bm = bits(cm, N)
     assert (bm != bm.transpose(0, 2, 1)).sum() <= max(4, bm.sum() // 1000)
+
+
+@pytest.mark.parametrize("kind,E,N,T,stride", [
+    ("merge", 1024, 16, 60, 16),       # BASELINE.json configs[1]: MergeEnv-v0 1024 envs x 16 aircraft
+    ("vertical", 2048, 32, 30, 32),    # configs[2]: VerticalCREnv-v0 2048 envs x 32 aircraft
+])
+def test_baseline_config_subset_parity(bg, kind, E, N, T, stride):
+    """The BASELINE.json parity configs at full size on the GPU: a strided subset of 64
+    envs checked against the oracle every step (same global env ids -> same Philox
+    spawns), NEXT_STEP autoreset inside the run, plus whole-batch properties."""
+    core, config, nat = bg
+    if kind == "merge":
+        cfg, A = config.merge_config(num_ac=N), 2
+        mk = lambda n: ob.MergeOracle(n, num_ac=N, seed=77, compute_cd=True)  # noqa: E731
+    else:
+        cfg, A = config.vertical_config(num_intruders=N - 1), 1
+        mk = lambda n: ob.VerticalOracle(n, num_ac=N, seed=77, compute_cd=True)  # noqa: E731
+    b = core.DeviceBatch(cfg, E, compute_cd=True, seed=77)
+    ids = np.arange(0, E, stride)
+    o = mk(len(ids))
+    o.env_ids = ids
+    close(b.reset().cpu().numpy()[ids], o.reset()["obs"], "reset obs")
+    rng = np.random.default_rng(9)
+    for t in range(T):
+        a = rng.uniform(-1, 1, (E, A))
+        b.step(torch.from_numpy(a))
+        r = o.step(a[ids])
+        close(b.obs.cpu().numpy()[ids], r["obs"], f"obs t={t}")
+        close(b.reward.cpu().numpy()[ids].astype(np.float64), r["reward"], f"reward t={t}")
+        assert np.array_equal(b.terminated.cpu().numpy()[ids].astype(bool), r["terminated"]), t
+        assert np.array_equal(b.truncated.cpu().numpy()[ids].astype(bool), r["truncated"]), t
+        live = ~r["was_reset"]
+        gi = b.intr_mask.cpu().numpy()[ids].astype(np.uint64)
+        assert np.array_equal(gi[live], r["intr_mask"][live]), t
+        assert np.array_equal(b.conf_mask.cpu().numpy()[ids].astype(np.uint64), r["conf_mask"]), t
+        assert np.array_equal(b.los_mask.cpu().numpy()[ids].astype(np.uint64), r["los_mask"]), t
+        if kind == "merge":
+            assert np.array_equal(b.topk.cpu().numpy()[ids][live], r["topk"][live]), t
+    obs = b.obs.cpu().numpy()
+    assert np.isfinite(obs).all()
+    cm = b.conf_mask.cpu().numpy().astype(np.uint64)
+    diag = (cm >> np.arange(N, dtype=np.uint64)[None, :]) & np.uint64(1)
+    assert not diag.any()
