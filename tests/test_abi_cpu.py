@@ -89,3 +89,15 @@ def test_create_fails_cleanly_without_device_or_bad_config():
     cfg.abi_version = 99
     assert lib.bsg_create(C.byref(cfg), C.byref(ctx)) == -1
     assert lib.bsg_step(None, None, None, None) == -1               # null ctx -> error, no crash
+
+
+def test_empty_batch_and_bad_timing_interval_rejected():
+    """num_envs = 0 (an empty batch) is refused at bsg_create with a message, before any
+    device work; a negative timing interval is refused on a null ctx without a crash."""
+    lib = nat.load_library()
+    from bluesky_gym import config
+    ctx = C.c_void_p()
+    cfg = config.merge_config(num_ac=32).to_c(0, 1, 1, 0, 0)
+    assert lib.bsg_create(C.byref(cfg), C.byref(ctx)) == -1
+    assert b"num_envs" in lib.bsg_last_error()
+    assert lib.bsg_set_timing(None, -1) == -1

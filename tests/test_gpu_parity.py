@@ -320,3 +320,36 @@ def test_baseline_config_subset_parity(bg, kind, E, N, T, stride):
     cm = b.conf_mask.cpu().numpy().astype(np.uint64)
     diag = (cm >> np.arange(N, dtype=np.uint64)[None, :]) & np.uint64(1)
     assert not diag.any()
+
+
+@pytest.mark.parametrize("kind,E,N,K", [
+    ("merge", 1, 2, 1),       # one env, the smallest Merge (one intruder, top-1)
+    ("merge", 7, 20, 5),      # reference default N = 20 (12 idle lanes of 32), ragged last wave
+    ("merge", 5, 5, 4),       # N = 5 -> 8-lane groups, 8 envs per wave, one partial wave
+    ("merge", 3, 64, 5),      # maximum aircraft: one env per wave, every lane an aircraft
+    ("vertical", 9, 3, 0),    # two intruders, ragged
+    ("vertical", 2, 64, 0),   # maximum aircraft (63 intruders)
+])
+def test_edge_shapes_parity(bg, kind, E, N, K):
+    """Ragged batches (E not a multiple of envs per wave), group sizes that leave idle
+    lanes, and the minimum/maximum aircraft counts: every output vs the oracle over two
+    NEXT_STEP autoresets (short TimeLimit)."""
+    core, config, nat = bg
+    T, M = 45, 20
+    if kind == "merge":
+        cfg = config.merge_config(num_ac=N, num_ac_state=K, max_episode_steps=M)
+        o = ob.MergeOracle(E, num_ac=N, num_ac_state=K, seed=5, compute_cd=True,
+                           max_episode_steps=M)
+        A = 2
+    else:
+        cfg = config.vertical_config(num_intruders=N - 1, max_episode_steps=M)
+        o = ob.VerticalOracle(E, num_ac=N, seed=5, compute_cd=True, max_episode_steps=M)
+        A = 1
+    b = core.DeviceBatch(cfg, E, compute_cd=True, seed=5)
+    close(b.reset().cpu().numpy(), o.reset()["obs"], "reset obs")
+    rng = np.random.default_rng(13)
+    for t in range(T):
+        a = rng.uniform(-1, 1, (E, A))
+        b.step(torch.from_numpy(a))
+        r = o.step(a)
+        _compare_step(b, r, N, kind, t)
