@@ -91,6 +91,7 @@ EXPORTED_SYMBOLS = (
     "bsg_abi_version", "bsg_last_error", "bsg_obs_dim", "bsg_action_dim", "bsg_spawn_width",
     "bsg_create", "bsg_destroy", "bsg_bind", "bsg_reset", "bsg_step", "bsg_set_timing",
     "bsg_step_timing", "bsg_set_stamps", "bsg_set_wind", "bsg_ctx_obs_dim", "bsg_geom_width",
+    "bsg_set_learner",
 )
 
 _lib = None
@@ -130,6 +131,8 @@ def load_library(path: str | None = None):
     lib.bsg_destroy.argtypes = [C.c_void_p]
     lib.bsg_bind.restype = C.c_int32
     lib.bsg_bind.argtypes = [C.c_void_p, C.POINTER(BsgBuffers)]
+    lib.bsg_set_learner.restype = C.c_int32
+    lib.bsg_set_learner.argtypes = [C.c_void_p, C.c_void_p]
     lib.bsg_reset.restype = C.c_int32
     lib.bsg_reset.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
     lib.bsg_step.restype = C.c_int32

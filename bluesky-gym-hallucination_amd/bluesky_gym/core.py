@@ -140,6 +140,18 @@ class DeviceBatch:
         self._bufs = b
         nat.check(self.lib.bsg_bind(self._ctx, C.byref(b)), "bsg_bind")
 
+    def set_learner(self, rows: torch.Tensor | None):
+        """Point the kernel's learner-row output at `rows` ([E, obs_dim + 3] fp32 on this
+        device, or None) without re-binding the other buffers (bsg_set_learner)."""
+        if rows is not None:
+            if (rows.dtype != torch.float32 or rows.device != self.device or not rows.is_contiguous()
+                    or tuple(rows.shape) != (self.E, self.obs_dim + 3)):
+                raise nat.BsgError(f"learner rows must be contiguous fp32 [{self.E}, {self.obs_dim + 3}] "
+                                   f"on {self.device}")
+        nat.check(self.lib.bsg_set_learner(self._ctx, C.c_void_p(rows.data_ptr()) if rows is not None
+                                           else None), "bsg_set_learner")
+        self.learner = rows
+
     def _stream(self):
         return C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
 

@@ -2,9 +2,9 @@
 exchange during the step, and one all-gather per RL step of the learner rows
 [obs..., reward, terminated, truncated] (fp32) so every rank sees the whole node's batch.
 
-The gather of step t runs on a communication stream while step t+1's kernel runs on the
-compute stream (double-buffered learner rows), so at 4096 envs per GPU the collective
-hides behind the step.  Shards draw device spawns with global env ids (env_offset), so a
+The gather of step t runs on RCCL's own stream while step t+1's kernel runs on the
+compute stream (double-buffered learner rows, async Work handles), so at 4096 envs per
+GPU the collective hides behind the step.  Shards draw device spawns with global env ids (env_offset), so a
 sharded job is the same set of episodes as one big batch.
 """
 from __future__ import annotations
@@ -21,20 +21,40 @@ def shard_range(total: int, world: int, rank: int):
     return rank * n, n
 
 
-def all_gather_rows(out: torch.Tensor, local: torch.Tensor, group=None):
+def all_gather_rows(out: torch.Tensor, local: torch.Tensor, group=None, async_op=False):
     """out[world*n, d] <- concat over ranks of local[n, d] (RCCL all_gather_into_tensor;
-    list all_gather fallback for backends without it, e.g. some gloo builds)."""
+    list all_gather fallback for backends without it, e.g. some gloo builds).  With
+    async_op the collective's Work handle is returned (else None after completion)."""
     try:
-        dist.all_gather_into_tensor(out, local, group=group)
+        return dist.all_gather_into_tensor(out, local, group=group, async_op=async_op)
     except (RuntimeError, AttributeError, NotImplementedError):
         world = dist.get_world_size(group)
         parts = list(out.chunk(world, dim=0))
-        dist.all_gather(parts, local, group=group)
-    return out
+        return dist.all_gather(parts, local, group=group, async_op=async_op)
+
+
+class Ready:
+    """Completion of one step's gathered rows.  wait(): the current stream (RCCL) or the
+    host (gloo) waits until every rank's rows of that step are in the gathered buffer."""
+
+    def __init__(self, work=None):
+        self._work = work
+
+    def wait(self):
+        if self._work is not None:
+            self._work.wait()
 
 
 class ShardedVectorEnv:
-    """Local shard of a node-wide vector env + per-step learner-row all-gather."""
+    """Local shard of a node-wide vector env + per-step learner-row all-gather.
+
+    Per step the host does: one bsg_step launch, one pointer swap of the learner rows
+    (bsg_set_learner) and one asynchronous all_gather_into_tensor -- RCCL runs it on its
+    own stream after the step kernel, concurrently with the next step's kernel; the
+    kernel two steps later, which rewrites the same rows buffer, is ordered after it by
+    Work.wait() (a stream wait, the host does not block).  Keeping the host side to these
+    three calls matters: a full re-bind plus event bookkeeping per step cost ~70 us of host
+    time, as much as the kernel itself (tools/shard_overhead.py)."""
 
     def __init__(self, make_local, total_envs: int, *, overlap=True, group=None):
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
@@ -50,45 +70,39 @@ class ShardedVectorEnv:
                           for _ in range(2)]
         self._cur = 0
         self.overlap = overlap and self.world > 1
-        self._comm = torch.cuda.Stream(device=dev) if self.overlap else None
-        self._done_ev = [None, None]
+        self._work = [None, None]
 
     def reset(self, **kw):
         return self.local.reset(**kw)
 
     def step(self, local_actions):
-        """Steps the local shard; returns (gathered rows tensor, ready event).  The rows of
-        this step are complete on every rank once `ready` has completed."""
+        """Steps the local shard; returns (gathered rows [total_envs, obs+3], Ready).  The
+        rows of this step may be read after ready.wait(), until the step after next."""
         b = self.local.batch
         cur = self._cur
+        w = self._work[cur]
+        if w is not None:                 # the gather two steps ago still reads rows[cur]
+            w.wait()
+            self._work[cur] = None
         if b.learner is not self._rows[cur]:
-            b.learner = self._rows[cur]
-            b._bind()
+            b.set_learner(self._rows[cur])
         self.local.step_tensors(local_actions)
         if self.world == 1:
             self._gathered[cur][: self.n_local].copy_(self._rows[cur])
-            ev = torch.cuda.Event()
-            ev.record()
+            ready = Ready()
         elif self.overlap:
-            compute = torch.cuda.current_stream(b.device)
-            ev_k = torch.cuda.Event()
-            ev_k.record(compute)
-            with torch.cuda.stream(self._comm):
-                self._comm.wait_event(ev_k)
-                all_gather_rows(self._gathered[cur], self._rows[cur], self.group)
-                ev = torch.cuda.Event()
-                ev.record(self._comm)
-            # the kernel two steps ahead rewrites this buffer: make compute wait for the gather
-            self._done_ev[cur] = ev
-            nxt = 1 - cur
-            if self._done_ev[nxt] is not None:
-                compute.wait_event(self._done_ev[nxt])
+            work = all_gather_rows(self._gathered[cur], self._rows[cur], self.group, async_op=True)
+            self._work[cur] = work
+            ready = Ready(work)
         else:
             all_gather_rows(self._gathered[cur], self._rows[cur], self.group)
-            ev = torch.cuda.Event()
-            ev.record()
+            ready = Ready()
         self._cur = 1 - cur
-        return self._gathered[cur], ev
+        return self._gathered[cur], ready
 
     def close(self):
+        for w in self._work:
+            if w is not None:
+                w.wait()
+        self._work = [None, None]
         self.local.close()

@@ -258,6 +258,13 @@ int32_t bsg_bind(bsg_ctx* c, const bsg_buffers* b) {
   return BSG_OK;
 }
 
+int32_t bsg_set_learner(bsg_ctx* c, float* learner) {
+  if (!c) return fail(BSG_E_INVALID_ARG, "bsg_set_learner: null ctx%s%lld");
+  if (!c->bound) return fail(BSG_E_STATE, "bsg_set_learner: buffers not bound%s%lld");
+  c->bufs.learner = learner;
+  return BSG_OK;
+}
+
 int32_t bsg_reset(bsg_ctx* c, const uint8_t* env_mask, const double* spawn, void* stream) {
   if (!c) return fail(BSG_E_INVALID_ARG, "bsg_reset: null ctx%s%lld");
   if (!c->bound) return fail(BSG_E_STATE, "bsg_reset: buffers not bound%s%lld");

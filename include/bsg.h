@@ -204,6 +204,13 @@ int32_t bsg_destroy(bsg_ctx* ctx);
 /* Attach the caller-owned device buffers (non-owning). */
 int32_t bsg_bind(bsg_ctx* ctx, const bsg_buffers* bufs);
 
+/* Re-point only the optional learner-row buffer ([E, obs_dim + 3] fp32, NULL = none) of a
+ * bound ctx, from the next launch on: the multi-GPU path double-buffers the rows it
+ * all-gathers (bluesky_gym/parallel.py) and swaps them every step without re-binding.
+ * Replaces nothing in the reference (its learner hand-off is SubprocVecEnv's pipe,
+ * stable_baselines3 common/vec_env/subproc_vec_env.py). */
+int32_t bsg_set_learner(bsg_ctx* ctx, float* learner_rows);
+
 /* Replaces: Env.reset() (merge_env.py:103-130 + _gen_aircraft :148-158;
  * vertical_cr_env.py:258-281 + _generate_conflicts :183-200; descent_env.py:162-182).
  * env_mask: device u8 [E] (NULL = all envs).  spawn: device f64 [E, spawn_width]
