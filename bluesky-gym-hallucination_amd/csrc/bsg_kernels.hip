@@ -65,6 +65,20 @@ __device__ __forceinline__ void store_ac(const Buffers& b, size_t a, const AC& s
   if constexpr (WIND) { b.gs[a] = s.gs; b.trk[a] = s.trk; }
 }
 
+// store only the fields whose bits changed since load_ac (`old` holds what memory has):
+// a steady Merge intruder rewrites 4 of its 13 fields (lat, lon, hdg, ap_trk), which
+// halves the launch's HBM writes.  The buffer contents are identical either way.
+template <bool WIND>
+__device__ __forceinline__ void store_ac_changed(const Buffers& b, size_t a, const AC& s,
+                                                 const AC& old) {
+#define BSG_ST(f) if (bits(s.f) != bits(old.f)) b.f[a] = s.f
+  BSG_ST(lat); BSG_ST(lon); BSG_ST(alt); BSG_ST(hdg); BSG_ST(tas); BSG_ST(cas); BSG_ST(vs);
+  BSG_ST(ax); BSG_ST(ap_trk); BSG_ST(selspd); BSG_ST(selalt); BSG_ST(selvs);
+  if constexpr (WIND) { BSG_ST(gs); BSG_ST(trk); }
+#undef BSG_ST
+  if (s.nav != old.nav) b.nav[a] = s.nav;
+}
+
 // Traffic.cre (bluesky/traffic/traffic.py): creation state + autopilot holding it
 __device__ __forceinline__ void cre(AC& s, double lat, double lon, double hdg, double alt,
                                     double spd) {
@@ -1373,7 +1387,7 @@ __global__ __launch_bounds__(64) void step_kernel(KParams p) {
 #else
       if (stepping && on) propagate<KIND, WIND>(p, e, j, a, s, ev, sub_reward, sub_done, act, mc);
 #endif
-      if (active) store_ac<WIND>(b, a, s);
+      if (active) store_ac_changed<WIND>(b, a, s, s_in);
       if (resetting && b.memo_cache) memo_invalidate(b.memo_cache, a, (size_t)p.E * N);
     }
     if (resetting && j == 0) reset_scalars<KIND>(ev, aux);
