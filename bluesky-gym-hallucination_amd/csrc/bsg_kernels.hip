@@ -211,6 +211,8 @@ struct Memo {
   double coslat, sinlat;           // cos/sin(lat * D2R) of the current latitude
   uint64_t tr_bits;                // key of turnrate = deg(g0*tan(bank)/max(tas, eps))
   double turnrate;
+  uint64_t rad_bits;               // key of the LNAV turn radius tas^2/(g0*tan(bank))
+  double turnrad;
   double last_alt;                 // altitude at the start of the latest substep
   uint64_t cas_tas_bits, cas_alt_bits;  // key of the stored cas = vtas2cas(tas, alt)
 };
@@ -232,6 +234,7 @@ __device__ __forceinline__ void memo_init(Memo& m, const AC& s) {
   m.at = Atmos{0, 0, 0}; m.ap_tas = 0; m.allow_tas = 0;
   m.wp_k = -1; m.wp_lat = 0; m.wp_lon = 0; m.wp_nq = 0; m.wp_cos = 0; m.wp_sin = 0;
   m.tr_bits = kNoKey; m.turnrate = 0;
+  m.rad_bits = kNoKey; m.turnrad = 0;
   m.last_alt = s.alt;
   m.cas_tas_bits = kNoKey; m.cas_alt_bits = kNoKey;
   sincos(s.lat * kD2R, &m.sinlat, &m.coslat);
@@ -308,7 +311,11 @@ __device__ __forceinline__ void substep(AC& s, Memo& m, double dt, const RouteRe
     if (k != m.wp_k) memo_wp(m, rt, k);
     // the waypoint distance only feeds `dist < turndist` (turndist <= turnrad while the
     // leg change is <= 90 deg) and `dist/|gs| < 4 s`; beyond both it need not be exact
-    const double turnrad = s.tas * s.tas / (npmax(0.01, TAN_BANKDEF) * G0);
+    if (bits(s.tas) != m.rad_bits) {
+      m.turnrad = s.tas * s.tas / (npmax(0.01, TAN_BANKDEF) * G0);
+      m.rad_bits = bits(s.tas);
+    }
+    const double turnrad = m.turnrad;
     const double far_m = npmax(turnrad, 4.0 * fabs(gsv)) * 1.000001 + 1.0;
     double qdr, dnm;
     qdrdist_cached(s.lat, s.lon, m.coslat, m.sinlat, m.wp_lat, m.wp_lon, m.wp_cos, m.wp_sin,
@@ -427,7 +434,8 @@ __device__ __forceinline__ void substep(AC& s, Memo& m, double dt, const RouteRe
       s.trk = s.hdg;
     }
   }
-  s.alt = swaltsel ? rint((s.alt + s.vs * dt) * 1e6) / 1e6 : allow_h;
+  if (swaltsel) s.alt = rint((s.alt + s.vs * dt) * 1e6) / 1e6;   // a branch: level flight
+  else s.alt = allow_h;                                            // skips the division
   s.lat = s.lat + (dt * gsnorth / Rearth) * kR2D;
   sincos(s.lat * kD2R, &m.sinlat, &m.coslat);
   s.lon = s.lon + (dt * gseast / m.coslat / Rearth) * kR2D;
