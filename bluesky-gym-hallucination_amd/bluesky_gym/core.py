@@ -57,7 +57,7 @@ class DeviceBatch:
         self.state = {k: z((E, N), torch.float64) for k in F64_STATE}
         self.state["nav"] = z((E, N), torch.int32)
         # cross-step memo of the speed schedule (csrc: memo_load/memo_store); NaN = no entry
-        self.memo_cache = torch.full((7, E, N), float("nan"), dtype=torch.float64, device=d) \
+        self.memo_cache = torch.full((2, E, N), float("nan"), dtype=torch.float64, device=d) \
             if self.want_memo else None
         self.envs = {k: z((E,), torch.int32) for k in I32_ENV}
         self.envs["episode"] = z((E,), torch.int32)     # uint32 on the device side

@@ -219,14 +219,25 @@ struct Memo {
 
 constexpr uint64_t kNoKey = 0x7ff8dead0000beefull;   // a NaN payload no input produces
 
-// Cross-step memo (bsg_buffers.memo_cache, SoA [MC_FIELDS][E*N]): the pure functions of an
-// aircraft's (selspd, alt, selalt) and the key of its stored cas survive the launch, so an
-// aircraft in steady flight evaluates no pow/exp at all -- not even in the first substep.
-// Keys are bit patterns stored as doubles (NaN payloads pass through memory unchanged).
-constexpr int MC_FIELDS = 7;
-enum { MC_SPD_SEL = 0, MC_SPD_ALT, MC_AP_TAS, MC_LIM_H, MC_ALLOW_TAS, MC_CAS_TAS, MC_CAS_ALT };
+// Cross-step memo (bsg_buffers.memo_cache, SoA [MC_FIELDS][E*N]): the speed-schedule values
+// of an aircraft survive the launch, so one in steady flight evaluates no pow/exp at all --
+// not even in the first substep.  Their keys are not stored.  After the last substep they
+// are, bit for bit:
+//   ap_tas     <- (selspd, alt at the start of the last substep)
+//   allow_tas  <- (ap_tas, min(selalt, HMAX))   (the limits follow every ap_tas update)
+//   stored cas <- (tas, alt at the start of the last substep)
+// and selspd / selalt / tas / alt are then the values stored to the state buffers, so the
+// keys are the stored state's own (selspd, selalt, tas, alt) whenever the last substep
+// started at the final altitude ("level").  The sign of the stored allow_tas (> 0 by
+// construction) carries that flag; NaN = no entry.  The next launch recovers the keys from
+// the state it loads, before the action decode.  Only the kernel writes the state buffers;
+// a caller that writes them directly must re-fill memo_cache with NaN (include/bsg.h).
+constexpr int MC_FIELDS = 2;
+enum { MC_AP_TAS = 0, MC_ALLOW_TAS };
 
 __device__ __forceinline__ double key_as_double(uint64_t k) { return __longlong_as_double((long long)k); }
+
+__device__ __forceinline__ double allow_h_of(double selalt) { return selalt > HMAX ? HMAX : selalt; }
 
 __device__ __forceinline__ void memo_init(Memo& m, const AC& s) {
   m.alt_bits = kNoKey; m.spd_bits = kNoKey; m.spdalt_bits = kNoKey;
@@ -246,23 +257,33 @@ __device__ __forceinline__ void memo_fetch(double v[MC_FIELDS], const double* mc
   for (int f = 0; f < MC_FIELDS; ++f) v[f] = mc[f * stride + a];
 }
 
-__device__ __forceinline__ void memo_load(Memo& m, const double v[MC_FIELDS]) {
-  m.spd_bits = bits(v[MC_SPD_SEL]);
-  m.spdalt_bits = bits(v[MC_SPD_ALT]);
+// s0: the aircraft as loaded (before this launch's action decode)
+__device__ __forceinline__ void memo_load(Memo& m, const double v[MC_FIELDS], const AC& s0) {
+  const double al = v[MC_ALLOW_TAS];
   m.ap_tas = v[MC_AP_TAS];
-  m.lim_tas_bits = bits(m.ap_tas);
-  m.lim_h_bits = bits(v[MC_LIM_H]);
-  m.allow_tas = v[MC_ALLOW_TAS];
-  m.cas_tas_bits = bits(v[MC_CAS_TAS]);
-  m.cas_alt_bits = bits(v[MC_CAS_ALT]);
+  if (al == al) {
+    m.lim_tas_bits = bits(m.ap_tas);
+    m.lim_h_bits = bits(allow_h_of(s0.selalt));
+    m.allow_tas = fabs(al);
+    if (al > 0.0) {
+      m.spd_bits = bits(s0.selspd);
+      m.spdalt_bits = bits(s0.alt);
+      m.cas_tas_bits = bits(s0.tas);
+      m.cas_alt_bits = bits(s0.alt);
+    }
+  }
 }
 
-// write back only the entries that changed (steady aircraft write nothing)
-__device__ __forceinline__ void memo_store(const Memo& m, const double old[MC_FIELDS], double* mc,
-                                           size_t a, size_t stride) {
-  const double v[MC_FIELDS] = {key_as_double(m.spd_bits), key_as_double(m.spdalt_bits), m.ap_tas,
-                               key_as_double(m.lim_h_bits), m.allow_tas,
-                               key_as_double(m.cas_tas_bits), key_as_double(m.cas_alt_bits)};
+// s: the aircraft as stored; write back only the entries that changed (steady aircraft
+// write nothing)
+__device__ __forceinline__ void memo_store(const Memo& m, const AC& s, const double old[MC_FIELDS],
+                                           double* mc, size_t a, size_t stride) {
+  const bool lim_ok = m.lim_tas_bits == bits(m.ap_tas) &&
+                      m.lim_h_bits == bits(allow_h_of(s.selalt)) && m.allow_tas > 0.0;
+  const bool level = m.spd_bits == bits(s.selspd) && m.spdalt_bits == bits(s.alt) &&
+                     m.cas_tas_bits == bits(s.tas) && m.cas_alt_bits == bits(s.alt);
+  const double v[MC_FIELDS] = {m.ap_tas, !lim_ok ? key_as_double(kNoKey)
+                                                 : (level ? m.allow_tas : -m.allow_tas)};
 #pragma unroll
   for (int f = 0; f < MC_FIELDS; ++f) {
     if (bits(old[f]) != bits(v[f])) mc[f * stride + a] = v[f];
@@ -574,7 +595,7 @@ __device__ __forceinline__ CdOut cd_pair(const LT& L, int i, int k) {
 
 template <int GS>
 __device__ __forceinline__ uint64_t group_bits(uint64_t ballot, int g) {
-  const uint64_t gm = (GS == 64) ? ~0ull : ((1ull << GS) - 1ull);
+  const uint64_t gm = (GS >= 64) ? ~0ull : ((1ull << (GS & 63)) - 1ull);
   return (ballot >> (g * GS)) & gm;
 }
 
@@ -1248,6 +1269,7 @@ __device__ __forceinline__ void propagate(const KParams& p, int e, int j, size_t
                                           const double act[2], const double mc[MC_FIELDS]) {
   const Buffers& b = p.b;
   const int N = p.N;
+  const AC s0 = s;                  // as loaded: the cross-step memo's keys (memo_load)
   if (j == 0) {
     if constexpr (KIND == BSG_ENV_MERGE) {
       hdg_spd_action<WIND>(p, s, act[0], act[1], 15.0, 20.0);
@@ -1271,7 +1293,7 @@ __device__ __forceinline__ void propagate(const KParams& p, int e, int j, size_t
   if (S > 0) {
     Memo m;
     memo_init(m, s);
-    if (b.memo_cache) memo_load(m, mc);
+    if (b.memo_cache) memo_load(m, mc, s0);
     RouteRegs rt;
     rt.load(p.route);
     const double dt = p.cfg.simdt;
@@ -1313,7 +1335,7 @@ __device__ __forceinline__ void propagate(const KParams& p, int e, int j, size_t
 #endif
     }
     memo_final_cas(m, s);
-    if (b.memo_cache) memo_store(m, mc, b.memo_cache, a, (size_t)p.E * N);
+    if (b.memo_cache) memo_store(m, s, mc, b.memo_cache, a, (size_t)p.E * N);
   }
 }
 

@@ -353,3 +353,35 @@ def test_edge_shapes_parity(bg, kind, E, N, K):
         b.step(torch.from_numpy(a))
         r = o.step(a)
         _compare_step(b, r, N, kind, t)
+
+
+@pytest.mark.parametrize("kind", ["merge", "vertical", "descent", "horizontal", "plan"])
+def test_memo_cache_is_bit_exact(bg, kind):
+    """The cross-step memo (memo_cache) only skips re-evaluating pure functions of
+    unchanged inputs: a batch stepped with it and one stepped without it hold bit-identical
+    aircraft state and outputs after every step (climbing/descending aircraft exercise the
+    non-level branch, autoresets the invalidation)."""
+    core, config, nat = bg
+    cfg, E, A = {
+        "merge": (config.merge_config(num_ac=32, max_episode_steps=25), 256, 2),
+        "vertical": (config.vertical_config(num_intruders=7, max_episode_steps=40), 128, 1),
+        "descent": (config.descent_config(max_episode_steps=40), 256, 1),
+        "horizontal": (config.horizontal_config(num_intruders=7, max_episode_steps=30), 128, 1),
+        "plan": (config.plan_waypoint_config(max_episode_steps=30), 256, 1),
+    }[kind]
+    with_m = core.DeviceBatch(cfg, E, compute_cd=True, seed=21, memo_cache=True)
+    no_m = core.DeviceBatch(cfg, E, compute_cd=True, seed=21, memo_cache=False)
+    with_m.reset()
+    no_m.reset()
+    gen = torch.Generator(device="cuda")
+    gen.manual_seed(4)
+    for t in range(70):
+        a = torch.rand((E, A), dtype=torch.float64, device="cuda", generator=gen) * 2 - 1
+        o1, r1, te1, tr1 = with_m.step(a)
+        o2, r2, te2, tr2 = no_m.step(a)
+        assert torch.equal(o1, o2) and torch.equal(r1, r2), t
+        assert torch.equal(te1, te2) and torch.equal(tr1, tr2), t
+        for f, v in with_m.state.items():
+            assert torch.equal(v.view(torch.int64) if v.dtype == torch.float64 else v,
+                               no_m.state[f].view(torch.int64) if v.dtype == torch.float64
+                               else no_m.state[f]), (t, f)
