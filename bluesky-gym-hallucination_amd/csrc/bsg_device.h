@@ -214,26 +214,27 @@ __device__ __forceinline__ bool b_times_dphi_far(double latd1, double latd2, dou
   return bmin * (fabs(latd2 - latd1) * kD2R) * 0.999999 > far_m;
 }
 
-__device__ __forceinline__ void qdrdist_cached(double latd1, double lond1, double coslat1,
-                                               double sinlat1, double latd2, double lond2,
-                                               double coslat2, double sinlat2, double far_m,
-                                               double* qdr, double* distnm) {
+// First half of geo.qdrdist for the LNAV loop: the bearing (exact, as qdrdist) and the
+// acos argument x of its distance.  Returns true when the distance is provably beyond
+// `far_m` (then the caller needs no more of it):
+//  - the meridian gap alone: great-circle >= r*|dphi|, r >= b (1e-6 relative margin);
+//  - the computed x itself: with t = far_m/b, x < 1 - t^2/2 <= cos(t) gives acos(x) > t,
+//    so d >= b*t = far_m (the 1e-12 margin covers acos's ulp error; the caller's
+//    thresholds sit >= 1 m inside far_m).  x is bit-identical to the argument the full
+//    path passes to acos.
+__device__ __forceinline__ bool qdr_x(double latd1, double lond1, double coslat1, double sinlat1,
+                                      double latd2, double lond2, double coslat2, double sinlat2,
+                                      double far_m, double* qdr, double* x) {
   double sdl, cdl;
   sincos(lond2 * kD2R - lond1 * kD2R, &sdl, &cdl);
   *qdr = atan2(sdl * coslat2, coslat1 * sinlat2 - sinlat1 * coslat2 * cdl) * kR2D;
-  // d = r*acos(x) is only compared against thresholds by the caller; when it is provably
-  // beyond `far_m` the WGS84 radius and the acos are skipped and +inf returned:
-  //  - the meridian gap alone: great-circle >= r*|dphi|, r >= b (1e-6 relative margin);
-  //  - the computed x itself: with t = far_m/b, x < 1 - t^2/2 <= cos(t) gives
-  //    acos(x) > t, so d >= b*t = far_m (the 1e-12 margin covers acos's ulp error;
-  //    the caller's thresholds sit >= 1 m inside far_m).  x is bit-identical to the
-  //    argument the full path would pass to acos.
-  const double x = coslat1 * coslat2 * cdl + sinlat1 * sinlat2;
+  *x = coslat1 * coslat2 * cdl + sinlat1 * sinlat2;
   const double t = far_m * (1.0 / 6356752.314245);
-  if (b_times_dphi_far(latd1, latd2, far_m) || x < (1.0 - 0.5 * t * t) - 1e-12) {
-    *distnm = __builtin_inf();
-    return;
-  }
+  return b_times_dphi_far(latd1, latd2, far_m) || *x < (1.0 - 0.5 * t * t) - 1e-12;
+}
+
+// Second half: the distance (NM) exactly as geo.qdrdist computes it from the same x.
+__device__ __forceinline__ double qdrdist_exact_nm(double latd1, double latd2, double x) {
   bool sw = (latd1 * latd2 >= 0.0);
   double r;
   if (sw) {
@@ -246,7 +247,41 @@ __device__ __forceinline__ void qdrdist_cached(double latd1, double lond1, doubl
         npmax(0.000001, fabs(latd1) + fabs(latd2));
   }
   double d = r * acos(x);
-  *distnm = d / NM;
+  return d / NM;
+}
+
+// Bounds [lo, hi] (metres) on the distance the exact path would yield, (d / NM) * NM with
+// d = r*acos(x), from x alone -- no transcendental.  r = rwgs84(mid-latitude) lies in
+// [b, a] on the same-hemisphere branch.  acos(1 - u) = 2 asin(sqrt(u/2)) >= sqrt(2u) for
+// u in [0, 2] (asin(y) >= y), <= sqrt(2u)(1 + 1e-4) for u <= 1e-3 (asin(y)/y <= 1 +
+// 1.01 y^2/6 at y <= 0.0224) and <= sqrt(2u) pi/2 beyond (asin convex on [0, 1]).
+// u = 1 - x is exact (Sterbenz) where it matters; the 1e-12 relative slack covers the
+// rounding of sqrt, r, acos and the /NM*NM round trip (each ~1e-16).  Returns false (use
+// the exact path) off the same-hemisphere branch and for x >= 1 (where acos(x) is 0 or
+// NaN in the exact path).
+__device__ __forceinline__ bool qdrdist_bounds(double latd1, double latd2, double x, double* lo,
+                                               double* hi) {
+  if (!(latd1 * latd2 >= 0.0)) return false;
+  const double u = 1.0 - x;
+  if (!(u > 0.0)) return false;
+  const double sq = sqrt(2.0 * u);
+  *lo = (6356752.314245 * sq) * (1.0 - 1e-12);
+  *hi = (6378137.0 * sq) * ((u <= 1e-3 ? 1.0001 : 1.5707963267948966) * (1.0 + 1e-12));
+  return true;
+}
+
+// Bounds [lo, hi] on tan(h) as the device libm computes it, 0 <= h <= 1.5 rad, without a
+// transcendental: every Taylor coefficient of tan is positive, so the partial sum
+// h + h^3/3 + 2h^5/15 + 17h^7/315 is a lower bound; pi^2 h / (pi^2 - 4h^2) is an upper
+// bound on (0, pi/2) (Becker-Stark).  The 1e-12 relative slack covers tan's ulp error
+// and the rounding of both expressions (each ~1e-16).  false: h outside [0, 1.5].
+__device__ __forceinline__ bool tan_bounds(double h, double* lo, double* hi) {
+  if (!(h >= 0.0 && h <= 1.5)) return false;
+  const double h2 = h * h;
+  const double pi2 = 9.869604401089358;    // pi^2 rounded: the slack absorbs its error
+  *lo = (h + h * h2 * (1.0 / 3.0 + h2 * (2.0 / 15.0 + h2 * (17.0 / 315.0)))) * (1.0 - 1e-12);
+  *hi = (pi2 * h / (pi2 - 4.0 * h2)) * (1.0 + 1e-12);
+  return true;
 }
 
 // functions.py:24-42 get_point_at_distance (R = 6371 km)

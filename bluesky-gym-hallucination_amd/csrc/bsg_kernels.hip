@@ -338,30 +338,49 @@ __device__ __forceinline__ void substep(AC& s, Memo& m, double dt, const RouteRe
     }
     const double turnrad = m.turnrad;
     const double far_m = npmax(turnrad, 4.0 * fabs(gsv)) * 1.000001 + 1.0;
-    double qdr, dnm;
-    qdrdist_cached(s.lat, s.lon, m.coslat, m.sinlat, m.wp_lat, m.wp_lon, m.wp_cos, m.wp_sin,
-                   far_m, &qdr, &dnm);
+    double qdr, x;
+    const bool far = qdr_x(s.lat, s.lon, m.coslat, m.sinlat, m.wp_lat, m.wp_lon, m.wp_cos,
+                           m.wp_sin, far_m, &qdr, &x);
     const double next_qdr = m.wp_nq < -900.0 ? qdr : m.wp_nq;
     const double half = 0.5 * fabs(degto180(pymod(qdr, 360.0) - pymod(next_qdr, 360.0)));
-    if (half > 45.0 && dnm == __builtin_inf())   // turndist may exceed turnrad: exact d
-      qdrdist_cached(s.lat, s.lon, m.coslat, m.sinlat, m.wp_lat, m.wp_lon, m.wp_cos, m.wp_sin,
-                     __builtin_inf(), &qdr, &dnm);
     bool reached = false;
-    if (dnm != __builtin_inf()) {
-      const double dist = dnm * NM;
-      bool reached_turn;
-      if (half <= 45.0 && dist > turnrad * 1.000001) {
-        reached_turn = false;                // tan(half) <= 1 -> turndist <= turnrad < dist
-      } else {
-        const double turndist = fabs(turnrad * tan(half * kD2R));
-        reached_turn = dist < turndist;
-      }
+    // far and half <= 45: dist > far_m > turnrad >= turndist and dist > 4|gs|: not reached
+    if (!far || half > 45.0) {
+      // ActiveWaypoint.reached needs only `dist < turndist` and `dist/g < 4`; decide each
+      // from bounds on the distance the exact path would compute (qdrdist_bounds) and
+      // evaluate the WGS84 radius and acos only when a bound straddles a threshold
       const double g = npmax(0.0001, fabs(gsv));
-      // dist/g < 4, decided without the division outside a 1e-6 band around 4*g
-      const bool close2wp = dist < 4.0 * g * 0.999999 ? true
-                          : (dist > 4.0 * g * 1.000001 ? false : dist / g < 4.0);
-      const bool tooclose = close2wp && (fabs(degto180(pymod(trkv, 360.0) - pymod(qdr, 360.0))) > 90.0);
-      reached = reached_turn || tooclose;
+      double lo = 0.0, hi = 0.0;
+      int rtn = -1, cw = -1;                 // reached_turn / close2wp: -1 = undecided
+      if (qdrdist_bounds(s.lat, m.wp_lat, x, &lo, &hi)) {
+        if (half <= 45.0 && lo > turnrad * 1.000001) {
+          rtn = 0;                           // tan(half) <= 1 -> turndist <= turnrad < dist
+        } else {
+          // turndist = |turnrad * tan(half)| bounded without the tan (tan_bounds); the
+          // exact tan only when the bounds overlap the distance's
+          double tl, th;
+          if (tan_bounds(half * kD2R, &tl, &th))
+            rtn = hi < turnrad * tl * (1.0 - 1e-15) ? 1 : (lo >= turnrad * th * (1.0 + 1e-15) ? 0 : -1);
+          if (rtn < 0) {
+            const double turndist = fabs(turnrad * tan(half * kD2R));
+            rtn = hi < turndist ? 1 : (lo >= turndist ? 0 : -1);
+          }
+        }
+        cw = hi < 4.0 * g * 0.999999 ? 1 : (lo > 4.0 * g * 1.000001 ? 0 : -1);
+      }
+      if (rtn < 0 || cw < 0) {
+        const double dist = qdrdist_exact_nm(s.lat, m.wp_lat, x) * NM;
+        if (half <= 45.0 && dist > turnrad * 1.000001) {
+          rtn = 0;
+        } else {
+          const double turndist = fabs(turnrad * tan(half * kD2R));
+          rtn = dist < turndist;
+        }
+        // dist/g < 4, decided without the division outside a 1e-6 band around 4*g
+        cw = dist < 4.0 * g * 0.999999 ? 1 : (dist > 4.0 * g * 1.000001 ? 0 : dist / g < 4.0);
+      }
+      const bool tooclose = cw && (fabs(degto180(pymod(trkv, 360.0) - pymod(qdr, 360.0))) > 90.0);
+      reached = rtn || tooclose;
     }
     if (reached) {
       if (k >= rt.len - 1) {
@@ -370,8 +389,8 @@ __device__ __forceinline__ void substep(AC& s, Memo& m, double dt, const RouteRe
         ++k;
         s.nav = (k << 8) | 1;
         memo_wp(m, rt, k);
-        qdrdist_cached(s.lat, s.lon, m.coslat, m.sinlat, m.wp_lat, m.wp_lon, m.wp_cos,
-                       m.wp_sin, __builtin_inf(), &qdr, &dnm);
+        qdr_x(s.lat, s.lon, m.coslat, m.sinlat, m.wp_lat, m.wp_lon, m.wp_cos, m.wp_sin,
+              0.0, &qdr, &x);              // only the bearing to the new waypoint is used
       }
     }
     if (s.nav & 1) s.ap_trk = qdr;
@@ -545,6 +564,48 @@ struct CdOut {
   bool inside;
 };
 
+// StateBased conflict decision of an inside pair from interval bounds, without the
+// bearing's atan2 + sincos.  The exact path's dx = dist*sin(qdr), dy = dist*cos(qdr) with
+// qdr = atan2(y, dlat) (y = dlon*cavelat, then the degree round trip through pymod) lie
+// within dist*7e-15 of dist*y/dangle and dist*dlat/dangle (atan2/sincos ulps, ~1e-15 rad of
+// degree rounding, dangle's rounding); 2e-13 is used.  That error is carried through tcpa,
+// dcpa2 and the horizontal entry/exit times as intervals (plus 1e-14 relative and small
+// absolute terms for the rounding of the bound arithmetic, 1e-9 s on times), then through
+// min/max with the exact vertical window.  When every conjunct of
+// `swhor && tin <= tout && tout > 0 && tin < 300` is settled by its interval, r->confl is the
+// exact path's decision and r->tcpa is within ~1e-12 s of its tcpa (an fp32 output); else
+// false and the caller runs the exact arithmetic.
+__device__ __forceinline__ bool cd_conflict_bounded(double dist, double dlat, double y,
+                                                    double dangle, double du, double dv,
+                                                    double dv2, double vrel, double tinver,
+                                                    double toutver, CdOut* r) {
+  if (!(dangle > 0.0)) return false;
+  const double inv = 1.0 / dangle;
+  const double dx = dist * (y * inv), dy = dist * (dlat * inv);
+  const double num = du * dx + dv * dy;
+  const double e_num = (fabs(du) + fabs(dv)) * (dist * 2e-13) + (fabs(du * dx) + fabs(dv * dy)) * 1e-14;
+  const double tcpa = -num / dv2;
+  const double e_t = e_num / dv2 + fabs(tcpa) * 1e-14 + 1e-300;
+  const double R2 = RPZ * RPZ;
+  const double dcpa2 = fabs(dist * dist - tcpa * tcpa * dv2);
+  const double e_d = dv2 * (2.0 * fabs(tcpa) * e_t + e_t * e_t) +
+                     (dist * dist + tcpa * tcpa * dv2 + R2) * 1e-14;
+  r->tcpa = tcpa;
+  if (dcpa2 - e_d >= R2) { r->confl = false; return true; }      // swhor false for sure
+  if (!(dcpa2 + e_d < R2)) return false;                          // swhor undecided
+  const double dtlo = sqrt(npmax(0.0, (R2 - dcpa2) - e_d)) / vrel * (1.0 - 1e-14);
+  const double dthi = sqrt((R2 - dcpa2) + e_d) / vrel * (1.0 + 1e-14);
+  const double sl = 1e-9;
+  const double slr = 1e-13 * (fabs(tcpa) + dthi);
+  const double tinh_lo = tcpa - e_t - dthi - sl - slr, tinh_hi = tcpa + e_t - dtlo + sl + slr;
+  const double touth_lo = tcpa - e_t + dtlo - sl - slr, touth_hi = tcpa + e_t + dthi + sl + slr;
+  const double tin_lo = npmax(tinver, tinh_lo), tin_hi = npmax(tinver, tinh_hi);
+  const double tout_lo = npmin(toutver, touth_lo), tout_hi = npmin(toutver, touth_hi);
+  if (tin_lo > tout_hi || tout_hi <= 0.0 || tin_lo >= DTLOOKAHEAD) { r->confl = false; return true; }
+  if (tin_hi <= tout_lo && tout_lo > 0.0 && tin_hi < DTLOOKAHEAD) { r->confl = true; return true; }
+  return false;
+}
+
 // exact StateBased terms of pair (i, k) (i != k), oracle operation order
 template <class LT>
 __device__ __forceinline__ CdOut cd_pair(const LT& L, int i, int k) {
@@ -565,6 +626,18 @@ __device__ __forceinline__ CdOut cd_pair(const LT& L, int i, int k) {
   if (dist > horizon) return r;
   r.inside = true;
   r.dist = dist;
+  const double dalt = L.alt[k] - L.alt[i] + 0.0;
+  double dvs = L.vs[k] - L.vs[i];
+  dvs = fabs(dvs) < 1e-6 ? 1e-6 : dvs;
+  const double tcrosshi = (dalt + HPZ) / -dvs;
+  const double tcrosslo = (dalt - HPZ) / -dvs;
+  const double tinver = npmin(tcrosshi, tcrosslo);
+  const double toutver = npmax(tcrosshi, tcrosslo);
+  r.lossep = (dist < RPZ) && (fabs(dalt) < HPZ);
+  if (cd_conflict_bounded(dist, dlat, dlon * cavelat, dangle, du, dv, dv2, vrel, tinver,
+                          toutver, &r))
+    return r;
+  // undecided by the bounds: the exact StateBased arithmetic
   const double qdr = pymod(atan2(dlon * cavelat, dlat) * kR2D, 360.0);
   double sq, cq;
   sincos(qdr * kD2R, &sq, &cq);
@@ -578,17 +651,9 @@ __device__ __forceinline__ CdOut cd_pair(const LT& L, int i, int k) {
   const double dtinhor = dxinhor / vrel;
   const double tinhor = swhor ? tcpa - dtinhor : 1e8;
   const double touthor = swhor ? tcpa + dtinhor : -1e8;
-  const double dalt = L.alt[k] - L.alt[i] + 0.0;
-  double dvs = L.vs[k] - L.vs[i];
-  dvs = fabs(dvs) < 1e-6 ? 1e-6 : dvs;
-  const double tcrosshi = (dalt + HPZ) / -dvs;
-  const double tcrosslo = (dalt - HPZ) / -dvs;
-  const double tinver = npmin(tcrosshi, tcrosslo);
-  const double toutver = npmax(tcrosshi, tcrosslo);
   const double tin = npmax(tinver, tinhor);
   const double tout = npmin(toutver, touthor);
   r.confl = swhor && (tin <= tout) && (tout > 0.0) && (tin < DTLOOKAHEAD);
-  r.lossep = (dist < RPZ) && (fabs(dalt) < HPZ);
   r.tcpa = tcpa;
   return r;
 }
