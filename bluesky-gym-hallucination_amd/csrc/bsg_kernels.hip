@@ -1390,7 +1390,11 @@ __device__ __forceinline__ void propagate(const KParams& p, int e, int j, size_t
       // partners now finish ~5 us apart (-7 % kernel time).  Scheduling only: no effect on
       // results.
       const int slot = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (3 << 11)) & 15;  // HW_ID wave id
-      const int sw = (3 * S + 3) / 4;
+#ifndef BSG_PRIO_SW_NUM
+#define BSG_PRIO_SW_NUM 3                  // switch after 3/4 of the substeps (swept:
+#define BSG_PRIO_SW_DEN 4                  // 1/2, 2/3, 9/10 measured slower, diag file)
+#endif
+      const int sw = (BSG_PRIO_SW_NUM * S + BSG_PRIO_SW_DEN - 1) / BSG_PRIO_SW_DEN;
       for (int it = 0; it < S; ++it) {
         if ((slot & 1) ? (it < sw) : (it >= sw)) __builtin_amdgcn_s_setprio(1);
         else __builtin_amdgcn_s_setprio(0);
