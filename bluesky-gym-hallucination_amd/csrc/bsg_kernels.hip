@@ -1541,8 +1541,12 @@ __global__ __launch_bounds__(64) void step_kernel(KParams p) {
       const double lati = L.lat[lane], loni = L.lon[lane];
       const double ui = cd_u(L, lane), vi = cd_v(L, lane);
       const double ali = fabs(lati);
-      for (int sft = 1; 2 * sft <= nac; ++sft) {
-        if (2 * sft == nac && j >= sft) break;          // pair (j, j + nac/2) once
+      // loads and tests only (unrolled so the LDS reads of several offsets are in
+      // flight together); the mirrored bits go out afterwards
+      const int nsft = (nac & 1) ? nac / 2 : (j < nac / 2 ? nac / 2 : nac / 2 - 1);
+      uint64_t mine = 0;                 // bit sft-1: pair (j, j + sft) is a candidate
+#pragma unroll 4
+      for (int sft = 1; sft <= nsft; ++sft) {
         int k = j + sft;
         if (k >= nac) k -= nac;
         const int lk = base + k;
@@ -1556,10 +1560,13 @@ __global__ __launch_bounds__(64) void step_kernel(KParams p) {
         const double du = cd_u(L, lk) - ui, dv = cd_v(L, lk) - vi;
         double dv2 = du * du + dv * dv;
         dv2 = fabs(dv2) < 1e-6 ? 1e-6 : dv2;
-        if (cd_candidate(dlat, dlon * c, dv2)) {
-          cand |= 1ull << k;
-          atomicOr(&L.lm[lk], 1ull << j);
-        }
+        if (cd_candidate(dlat, dlon * c, dv2)) mine |= 1ull << (sft - 1);
+      }
+      for (uint64_t mm = mine; mm; mm &= mm - 1) {
+        int k = j + 1 + __builtin_ctzll(mm);
+        if (k >= nac) k -= nac;
+        cand |= 1ull << k;
+        atomicOr(&L.lm[base + k], 1ull << j);
       }
     }
     __syncthreads();
