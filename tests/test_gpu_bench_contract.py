@@ -1,0 +1,33 @@
+"""bench.py keeps the driver contract: one JSON line with BASELINE.json's metric, the
+roofline object and the CPU baseline (short run, GPU box)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_bench_json_line():
+    out = subprocess.run([sys.executable, "bench.py", "--steps", "5", "--warmup", "2",
+                          "--cpu-seconds", "1"], cwd=REPO, capture_output=True, text=True,
+                         timeout=110)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    r = json.loads(lines[0])
+    with open(os.path.join(REPO, "BASELINE.json")) as f:
+        assert r["metric"] == json.load(f)["metric"]
+    assert r["value"] > 0 and r["unit"] == "env_steps/s" and r["n_gpus"] == 1
+    assert r["steps"] == 5 and r["warmup"] == 2 and r["higher_is_better"] is True
+    assert r["scaling"] == "weak" and r["vs_baseline"] is None and r["dtype"] == "f64"
+    rf = r["roofline"]
+    assert rf["bound"] == "hbm" and rf["unit"] == "GB/s" and rf["peak"] == 8000.0
+    assert rf["achieved"] > 0 and abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-12
+    cb = r["cpu_baseline"]
+    assert cb["value"] > 0 and cb["cores"] >= 1 and cb["kind"] in ("port", "reference")
+    assert "workload" in r["config"]
