@@ -494,6 +494,9 @@ struct Lds : LdsWind<WIND> {
   // u = tas*sin(hdg), v = tas*cos(hdg): the Merge obs velocities, and StateBased's
   // gs*sin(trk) / gs*cos(trk) when there is no wind
   double lat[64], lon[64], alt[64], hdg[64], tas[64], vs[64], u[64], v[64], d[64];
+  // fp32 copies for the StateBased candidate filter (cd_candidate_f): latitude in rad,
+  // longitude in deg, StateBased velocity components
+  float flat[64], flon[64], fu[64], fv[64];
   int done[64];
   // StateBased assembly (LDS atomics)
   unsigned long long cm[64], lm[64], tmax[64], gmin[64];
@@ -513,6 +516,15 @@ __device__ __forceinline__ void stage(LT& L, int lane, const AC& s) {
     sincos(s.trk * kD2R, &sk, &ck);
     L.cu[lane] = s.gs * sk;
     L.cv[lane] = s.gs * ck;
+  }
+  L.flat[lane] = (float)(s.lat * kD2R);
+  L.flon[lane] = (float)s.lon;
+  if constexpr (LT::kWind) {
+    L.fu[lane] = (float)L.cu[lane];
+    L.fv[lane] = (float)L.cv[lane];
+  } else {
+    L.fu[lane] = (float)L.u[lane];
+    L.fv[lane] = (float)L.v[lane];
   }
 }
 
@@ -543,19 +555,25 @@ __device__ __forceinline__ double cd_v(const LT& L, int i) {
 // holds a lane hostage to a near one.  Row masks / tcpamax / per-env min separation are
 // assembled with LDS atomics (u64 or / min / max; tcpa > 0 and dist >= 0 order like u64).
 
-// true unless the pair is provably outside the horizon.  dlat is the pair's computed
-// latitude gap (rad), dlonc a lower bound of |dlon|*cavelat of cd_pair: the wrapped
-// longitude gap less 1e-9 deg (pymod's rounding is ~1e-13 deg) times 1 - x^2/2 <= cos(x)
-// at x = max(|lat_i|, |lat_k|) >= |mean latitude| (less 1e-9 relative).  So
-// a = Re*sqrt(dlat^2 + dlonc^2) is a lower bound of the computed dist; the fp32 square
-// root (<= 1.2e-7 relative with the conversion) sits far inside the 0.999998 factor.
-// Skip => computed dist >= a*0.999998 - 1 + 1 > computed horizon.
-__device__ __forceinline__ bool cd_candidate(double dlat, double dlonc, double dv2f) {
-  const double D2 = dlat * dlat + dlonc * dlonc;
-  const double sq = (double)__fsqrt_rn((float)D2);
-  const double a = 6371000.0 * sq * 0.999998 - 1.0;
-  const double w = (a * 0.999999 - RPZ) * (1.0 / DTLOOKAHEAD);
-  return !(w > 0.0 && w * w > dv2f * 1.000001);
+// true unless the pair is provably outside the horizon, decided in fp32 from the LDS
+// copies (flat = lat*kD2R, flon = lon in deg, fu/fv = StateBased velocity, each rounded to
+// fp32: <= 1e-7 rad, 1.1e-5 deg, 2.4e-5 m/s).  dlat = |flat_k - flat_i|, dl = the wrapped
+// |flon_k - flon_i|, x = max(|flat_i|, |flat_k|), dv2 = du^2 + dv^2 of the fp32 components.
+// Lower bounds of cd_pair's computed |dlat|, |dlon| (less 3e-7 rad / 1e-4 deg) and cavelat
+// (1 - x^2/2 <= cos x at x + 2e-7 >= |mean latitude|) give a lower bound a of its
+// computed dist (1e-5 relative and 20 m to spare for fp32 rounding); vrel <= sqrt(dv2)(1 +
+// 1e-5) + 2e-3 covers the fp32 velocities and the 1e-6 clamp, so skip => computed dist >
+// computed horizon RPZ + DTLOOKAHEAD*vrel (+1e-9 relative + 1 m).  Every step of it is
+// symmetric in (i, k), so the decision is the same for both orders of a pair.
+__device__ __forceinline__ bool cd_candidate_f(float dlat, float dl, float x, float dv2) {
+  const float dlat_lb = fmaxf(dlat * (1.0f - 1e-6f) - 3e-7f, 0.0f);
+  const float dlon_lb = fmaxf(dl - 1e-4f, 0.0f) * 0.017453292f;
+  const float xu = x + 2e-7f;
+  const float c = fmaxf(1.0f - 0.5f * xu * xu - 1e-6f, 0.0f);
+  const float y = dlon_lb * c;
+  const float a = 6371000.0f * __fsqrt_rn(dlat_lb * dlat_lb + y * y) * (1.0f - 1e-5f) - 20.0f;
+  const float hor = (9260.0f + 300.0f * (__fsqrt_rn(dv2) * (1.0f + 1e-5f) + 2e-3f)) * (1.0f + 1e-6f) + 2.0f;
+  return !(a > hor);
 }
 
 struct CdOut {
@@ -1538,9 +1556,9 @@ __global__ __launch_bounds__(64) void step_kernel(KParams p) {
     uint64_t cand = 0;
     if (on) {
       const int nac = ev.nac;
-      const double lati = L.lat[lane], loni = L.lon[lane];
-      const double ui = cd_u(L, lane), vi = cd_v(L, lane);
-      const double ali = fabs(lati);
+      const float flati = L.flat[lane], floni = L.flon[lane];
+      const float fui = L.fu[lane], fvi = L.fv[lane];
+      const float fali = fabsf(flati);
       // loads and tests only (unrolled so the LDS reads of several offsets are in
       // flight together); the mirrored bits go out afterwards
       const int nsft = (nac & 1) ? nac / 2 : (j < nac / 2 ? nac / 2 : nac / 2 - 1);
@@ -1550,17 +1568,16 @@ __global__ __launch_bounds__(64) void step_kernel(KParams p) {
         int k = j + sft;
         if (k >= nac) k -= nac;
         const int lk = base + k;
-        const double latk = L.lat[lk];
-        const double dlat = (latk - lati) * kD2R;
-        double dl = fabs(L.lon[lk] - loni);
-        dl = dl > 180.0 ? 360.0 - dl : dl;
-        const double dlon = npmax(dl - 1e-9, 0.0) * kD2R;
-        const double x = npmax(ali, fabs(latk)) * kD2R;
-        const double c = npmax((1.0 - 0.5 * x * x) * (1.0 - 1e-9) - 1e-12, 0.0);
-        const double du = cd_u(L, lk) - ui, dv = cd_v(L, lk) - vi;
-        double dv2 = du * du + dv * dv;
-        dv2 = fabs(dv2) < 1e-6 ? 1e-6 : dv2;
-        if (cd_candidate(dlat, dlon * c, dv2)) mine |= 1ull << (sft - 1);
+        const float dlat = fabsf(L.flat[lk] - flati);
+        float dl = fabsf(L.flon[lk] - floni);
+        dl = dl > 180.0f ? 360.0f - dl : dl;
+        const float x = fmaxf(fali, fabsf(L.flat[lk]));
+        const float du = L.fu[lk] - fui, dv = L.fv[lk] - fvi;
+#if defined(BSG_EXP_CD_NOP1) && BSG_EXP_CD_NOP1
+        if (du > -1e30f) mine |= 1ull << (sft - 1);      // experiment: every pair a candidate
+#else
+        if (cd_candidate_f(dlat, dl, x, du * du + dv * dv)) mine |= 1ull << (sft - 1);
+#endif
       }
       for (uint64_t mm = mine; mm; mm &= mm - 1) {
         int k = j + 1 + __builtin_ctzll(mm);
@@ -1590,7 +1607,11 @@ __global__ __launch_bounds__(64) void step_kernel(KParams p) {
     BSG_STAMP(4, stamp_clock() | ((unsigned long long)total << 48));
 #endif
     // phase 2: dense exact StateBased over the surviving pairs
+#if defined(BSG_EXP_CD_NOP2) && BSG_EXP_CD_NOP2
+    for (int t = lane; t < 0; t += 64) {            // experiment: phase 2 skipped
+#else
     for (int t = lane; t < total; t += 64) {
+#endif
       const int pr = cd_list[t];
       const int li = pr >> 6, lk = pr & 63;
       const CdOut r = cd_pair(L, li, lk);
