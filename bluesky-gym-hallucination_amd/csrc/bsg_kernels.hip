@@ -954,11 +954,17 @@ __device__ __forceinline__ void reset_scalars(EnvScalars& v, const double aux[2]
 // Per-lane observation terms of aircraft j (j >= 1) relative to the ownship (LDS).
 // o[0..6] per kind (see the writers below); returns the intrusion predicate.
 // ---------------------------------------------------------------------------------------
+// Merge: the ownship lane (own != nullptr) runs the same kwikqdrdist instructions towards
+// its active waypoint (own_obs's terms, merge_env.py:178-191) while the intruder lanes run
+// them towards their aircraft, instead of lane 0 evaluating them alone afterwards.
+struct OwnPre { double wlat, wlon, wdist, drift, sd, cd; };
+
 template <int KIND, class LT>
 __device__ __forceinline__ bool lane_obs(const LT& L, int base, int lane, double o[7],
-                                         double* sortkey) {
+                                         double* sortkey, OwnPre* own = nullptr) {
   const double lat0 = L.lat[base], lon0 = L.lon[base], hdg0 = L.hdg[base];
-  const double latj = L.lat[lane], lonj = L.lon[lane];
+  const bool is_own = own != nullptr && lane == base;
+  const double latj = is_own ? own->wlat : L.lat[lane], lonj = is_own ? own->wlon : L.lon[lane];
   // shared kwik terms: lata + latb == latb + lata bitwise, so cavelat is common to the
   // kwikdist_matrix (merge_env.py:195) and kwikqdrdist (:203) forms
   const double dlat = (latj - lat0) * kD2R;
@@ -968,9 +974,16 @@ __device__ __forceinline__ bool lane_obs(const LT& L, int base, int lane, double
   const double qdr = pymod(atan2(dlon * cavelat, dlat) * kR2D, 360.0);
   if constexpr (KIND == BSG_ENV_MERGE) {
     // merge_env.py:195-218
-    const double dmat = 6371000.0 * sqrt(dlat * dlat + (dlon * dlon) * (cavelat * cavelat)) / NM;
+    // ownship: drift = bound180(hdg - qdr to the waypoint) and its cos/sin (own_obs)
+    const double ang = is_own ? bound180(hdg0 - qdr) : qdr;
     double sb, cb;
-    sincos(qdr * kD2R, &sb, &cb);
+    sincos(ang * kD2R, &sb, &cb);
+    if (is_own) {
+      own->wdist = dist; own->drift = ang; own->sd = sb; own->cd = cb;
+      *sortkey = __builtin_inf();
+      return false;
+    }
+    const double dmat = 6371000.0 * sqrt(dlat * dlat + (dlon * dlon) * (cavelat * cavelat)) / NM;
     const double x_r = (dist * 1.852 * 1000) * cb;
     const double y_r = (dist * 1.852 * 1000) * sb;
     // vx = cos(hdg)*tas == v = tas*cos(hdg) bitwise (LDS staging)
@@ -1233,6 +1246,7 @@ template <class LT>
 __device__ __forceinline__ int rank_in_group(const LT& L, int base, int lane, int j, int N) {
   const double dj = L.d[lane];
   int r = 0;
+#pragma unroll 8
   for (int k = 1; k < N; ++k) {
     const double dk = L.d[base + k];
     r += (dk < dj) || (dk == dj && k < j);
@@ -1524,7 +1538,15 @@ __global__ __launch_bounds__(64) void step_kernel(KParams p) {
   double o[7] = {0, 0, 0, 0, 0, 0, 0};
   double sortkey = __builtin_inf();
   bool intr = false;
-  if (kLaneObs && on && j > 0) intr = lane_obs<KIND>(L, base, lane, o, &sortkey);
+  OwnPre own{};                     // Merge: the ownship's waypoint terms (lane j == 0)
+  if constexpr (KIND == BSG_ENV_MERGE) {
+    const int w = ev.wpt_reach == 0 ? 0 : 1;
+    own.wlat = p.cfg.wpt_lat[w];
+    own.wlon = p.cfg.wpt_lon[w];
+    if (on) intr = lane_obs<KIND>(L, base, lane, o, &sortkey, &own);
+  } else {
+    if (kLaneObs && on && j > 0) intr = lane_obs<KIND>(L, base, lane, o, &sortkey);
+  }
   if constexpr (kRanked) {
     L.d[lane] = sortkey;
   }
@@ -1638,7 +1660,15 @@ __global__ __launch_bounds__(64) void step_kernel(KParams p) {
   bool term = false, trunc = false, done = false;
   if (ok && j == 0) {
     double wdist = 0, drift = 0, rwd = 0;
-    own_obs<KIND>(p, L, lane, ev, sc, &wdist, &drift, &rwd);
+    if constexpr (KIND == BSG_ENV_MERGE && !WIND) {
+      // own_obs (merge_env.py:178-191) from the terms lane_obs computed on this lane
+      wdist = own.wdist;
+      drift = own.drift;
+      sc[0] = L.tas[lane]; sc[1] = own.cd; sc[2] = (double)ev.wpt_reach; sc[3] = own.sd;
+      sc[4] = wdist / 250;
+    } else {
+      own_obs<KIND>(p, L, lane, ev, sc, &wdist, &drift, &rwd);
+    }
     double dkm[kPlan ? PW_NWPT : 1];
     if constexpr (kPlan)
       plan_obs(b.env_geom + (size_t)e * PW_GEOM, L.lat[lane], L.lon[lane], L.hdg[lane],
