@@ -385,3 +385,36 @@ def test_memo_cache_is_bit_exact(bg, kind):
             assert torch.equal(v.view(torch.int64) if v.dtype == torch.float64 else v,
                                no_m.state[f].view(torch.int64) if v.dtype == torch.float64
                                else no_m.state[f]), (t, f)
+
+
+def test_merge_full_size_soak_300_steps(bg):
+    """The bench workload for 300 RL steps (six TimeLimit episodes per env, thousands of
+    autoresets): a strided 32-env subset stays on the oracle every 10th step (outputs and
+    masks), and the whole batch keeps finite state, valid top-K and in-range counters."""
+    core, config, nat = bg
+    E, N, T = 4096, 32, 300
+    b = core.DeviceBatch(config.merge_config(num_ac=N), E, compute_cd=True, seed=2024)
+    ids = np.arange(0, E, 128)
+    o = ob.MergeOracle(len(ids), num_ac=N, seed=2024, compute_cd=True)
+    o.env_ids = ids
+    b.reset()
+    o.reset()
+    rng = np.random.default_rng(77)
+    for t in range(T):
+        a = rng.uniform(-1, 1, (E, 2))
+        b.step(torch.from_numpy(a))
+        r = o.step(a[ids])
+        if t % 10 == 9:
+            close(b.obs.cpu().numpy()[ids], r["obs"], f"obs t={t}")
+            assert np.array_equal(b.terminated.cpu().numpy()[ids].astype(bool), r["terminated"]), t
+            assert np.array_equal(b.truncated.cpu().numpy()[ids].astype(bool), r["truncated"]), t
+            assert np.array_equal(b.conf_mask.cpu().numpy()[ids].astype(np.uint64), r["conf_mask"]), t
+            assert np.array_equal(b.los_mask.cpu().numpy()[ids].astype(np.uint64), r["los_mask"]), t
+    for f, v in b.state.items():
+        if v.dtype == torch.float64:
+            assert torch.isfinite(v).all(), f
+    sc = b.envs["step_count"].cpu().numpy()
+    assert sc.min() >= 0 and sc.max() <= 50
+    tk = b.topk.cpu().numpy()
+    assert ((tk >= 1) & (tk < N)).all()
+    assert np.isfinite(b.obs.cpu().numpy()).all()
