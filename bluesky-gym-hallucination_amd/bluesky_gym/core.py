@@ -57,7 +57,8 @@ class DeviceBatch:
         self.state = {k: z((E, N), torch.float64) for k in F64_STATE}
         self.state["nav"] = z((E, N), torch.int32)
         # cross-step memo of the speed schedule (csrc: memo_load/memo_store); NaN = no entry
-        self.memo_cache = torch.full((2, E, N), float("nan"), dtype=torch.float64, device=d) \
+        # [2][E*N] per-aircraft entries, then [E][4] ownship atmosphere (csrc: memo_*, oat)
+        self.memo_cache = torch.full((2 * E * N + 4 * E,), float("nan"), dtype=torch.float64, device=d) \
             if self.want_memo else None
         self.envs = {k: z((E,), torch.int32) for k in I32_ENV}
         self.envs["episode"] = z((E,), torch.int32)     # uint32 on the device side

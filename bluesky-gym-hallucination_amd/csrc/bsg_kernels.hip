@@ -1363,7 +1363,8 @@ constexpr int kActDim = (KIND == BSG_ENV_MERGE || KIND == BSG_ENV_STATIC_OBSTACL
 template <int KIND, bool WIND>
 __device__ __forceinline__ void propagate(const KParams& p, int e, int j, size_t a, AC& s,
                                           EnvScalars& ev, double& sub_reward, bool& sub_done,
-                                          const double act[2], const double mc[MC_FIELDS]) {
+                                          const double act[2], const double mc[MC_FIELDS],
+                                          const double oat[4]) {
   const Buffers& b = p.b;
   const int N = p.N;
   const AC s0 = s;                  // as loaded: the cross-step memo's keys (memo_load)
@@ -1391,6 +1392,7 @@ __device__ __forceinline__ void propagate(const KParams& p, int e, int j, size_t
     Memo m;
     memo_init(m, s);
     if (b.memo_cache) memo_load(m, mc, s0);
+    if (j == 0) { m.alt_bits = bits(oat[0]); m.at = Atmos{oat[1], oat[2], oat[3]}; }
     RouteRegs rt;
     rt.load(p.route);
     const double dt = p.cfg.simdt;
@@ -1437,6 +1439,10 @@ __device__ __forceinline__ void propagate(const KParams& p, int e, int j, size_t
     }
     memo_final_cas(m, s);
     if (b.memo_cache) memo_store(m, s, mc, b.memo_cache, a, (size_t)p.E * N);
+    if (j == 0 && b.memo_cache && m.alt_bits != bits(oat[0])) {
+      double* t = b.memo_cache + (size_t)MC_FIELDS * p.E * N + (size_t)e * 4;
+      t[0] = key_as_double(m.alt_bits); t[1] = m.at.p; t[2] = m.at.rho; t[3] = m.at.T;
+    }
   }
 }
 
@@ -1478,6 +1484,15 @@ __global__ __launch_bounds__(64) void step_kernel(KParams p) {
   for (int f = 0; f < MC_FIELDS; ++f) mc[f] = key_as_double(kNoKey);
   if (ok && b.memo_cache && p.mode == MODE_STEP && p.cfg.action_frequency > 0)
     memo_fetch(mc, b.memo_cache, a, (size_t)p.E * N);
+  // the ownship's atmosphere memo (key = altitude bits, then p, rho, T): vatmos is a pure
+  // function of the altitude, so an entry is valid whenever its key matches -- a level
+  // ownship skips the pow + exp its speed chain would open with every RL step
+  double oat[4] = {key_as_double(kNoKey), 0.0, 0.0, 0.0};
+  if (ok && j == 0 && b.memo_cache && p.mode == MODE_STEP && p.cfg.action_frequency > 0) {
+    const double* t = b.memo_cache + (size_t)MC_FIELDS * p.E * N + (size_t)e * 4;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) oat[k] = t[k];
+  }
   ev.nac = N;
   if constexpr (KIND == BSG_ENV_SECTOR_CR) {
     if (env_ok) {
@@ -1514,9 +1529,9 @@ __global__ __launch_bounds__(64) void step_kernel(KParams p) {
       if (resetting) spawn<KIND>(p, e, j, ev.episode, s, aux, keep);
 #if defined(BSG_EXP_SKIP_OWN) && BSG_EXP_SKIP_OWN
       // experiment build only (tools/ablate.py): the ownship does not move
-      if (stepping && on && j != 0) propagate<KIND, WIND>(p, e, j, a, s, ev, sub_reward, sub_done, act, mc);
+      if (stepping && on && j != 0) propagate<KIND, WIND>(p, e, j, a, s, ev, sub_reward, sub_done, act, mc, oat);
 #else
-      if (stepping && on) propagate<KIND, WIND>(p, e, j, a, s, ev, sub_reward, sub_done, act, mc);
+      if (stepping && on) propagate<KIND, WIND>(p, e, j, a, s, ev, sub_reward, sub_done, act, mc, oat);
 #endif
       if (active) store_ac_changed<WIND>(b, a, s, s_in);
       if (resetting && b.memo_cache) memo_invalidate(b.memo_cache, a, (size_t)p.E * N);

@@ -94,10 +94,11 @@ typedef struct bsg_buffers {
   double *gs, *trk;          /* ground speed / track (bs.traf.gs, .trk); required only while
                                 a wind field is set (bsg_set_wind) -- without wind gs = tas
                                 and trk = hdg, and these may be NULL */
-  double *memo_cache;        /* optional [2][E*N] scratch owned by the caller, initialised to
+  double *memo_cache;        /* optional [2*E*N + 4*E] scratch owned by the caller, initialised to
                                 NaN: cross-step memo of the pure per-aircraft speed-schedule
                                 functions (exact: the entries' keys are the aircraft's stored
-                                selspd/selalt/tas/alt bits, see bsg_kernels.hip).  Re-fill it
+                                selspd/selalt/tas/alt bits; the [E][4] tail is the ownship's
+                                atmosphere keyed by altitude, see bsg_kernels.hip).  Re-fill it
                                 with NaN after writing any aircraft-state buffer directly;
                                 NULL disables it */
   /* ---- per-env state [E] ----------------------------------------------------------- */
