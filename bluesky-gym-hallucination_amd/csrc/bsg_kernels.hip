@@ -496,7 +496,7 @@ struct Lds : LdsWind<WIND> {
   double lat[64], lon[64], alt[64], hdg[64], tas[64], vs[64], u[64], v[64], d[64];
   // fp32 copies for the StateBased candidate filter (cd_candidate_f): latitude in rad,
   // longitude in deg, StateBased velocity components
-  float flat[64], flon[64], fu[64], fv[64];
+  float4 fpk[64];                  // (lat rad, lon deg, u, v): one ds_read_b128 per pair
   int done[64];
   // StateBased assembly (LDS atomics)
   unsigned long long cm[64], lm[64], tmax[64], gmin[64];
@@ -517,14 +517,10 @@ __device__ __forceinline__ void stage(LT& L, int lane, const AC& s) {
     L.cu[lane] = s.gs * sk;
     L.cv[lane] = s.gs * ck;
   }
-  L.flat[lane] = (float)(s.lat * kD2R);
-  L.flon[lane] = (float)s.lon;
   if constexpr (LT::kWind) {
-    L.fu[lane] = (float)L.cu[lane];
-    L.fv[lane] = (float)L.cv[lane];
+    L.fpk[lane] = make_float4((float)(s.lat * kD2R), (float)s.lon, (float)L.cu[lane], (float)L.cv[lane]);
   } else {
-    L.fu[lane] = (float)L.u[lane];
-    L.fv[lane] = (float)L.v[lane];
+    L.fpk[lane] = make_float4((float)(s.lat * kD2R), (float)s.lon, (float)L.u[lane], (float)L.v[lane]);
   }
 }
 
@@ -1591,10 +1587,14 @@ __global__ __launch_bounds__(64) void step_kernel(KParams p) {
     // LDS word (L.lm, re-zeroed before phase 2).
     __syncthreads();
     uint64_t cand = 0;
+#if defined(BSG_EXP_CD_NOTEST) && BSG_EXP_CD_NOTEST
+    if (false) {                                     // experiment: no phase-1 tests at all
+#else
     if (on) {
+#endif
       const int nac = ev.nac;
-      const float flati = L.flat[lane], floni = L.flon[lane];
-      const float fui = L.fu[lane], fvi = L.fv[lane];
+      const float4 pi = L.fpk[lane];
+      const float flati = pi.x, floni = pi.y, fui = pi.z, fvi = pi.w;
       const float fali = fabsf(flati);
       // loads and tests only (unrolled so the LDS reads of several offsets are in
       // flight together); the mirrored bits go out afterwards
@@ -1604,12 +1604,12 @@ __global__ __launch_bounds__(64) void step_kernel(KParams p) {
       for (int sft = 1; sft <= nsft; ++sft) {
         int k = j + sft;
         if (k >= nac) k -= nac;
-        const int lk = base + k;
-        const float dlat = fabsf(L.flat[lk] - flati);
-        float dl = fabsf(L.flon[lk] - floni);
+        const float4 pk = L.fpk[base + k];
+        const float dlat = fabsf(pk.x - flati);
+        float dl = fabsf(pk.y - floni);
         dl = dl > 180.0f ? 360.0f - dl : dl;
-        const float x = fmaxf(fali, fabsf(L.flat[lk]));
-        const float du = L.fu[lk] - fui, dv = L.fv[lk] - fvi;
+        const float x = fmaxf(fali, fabsf(pk.x));
+        const float du = pk.z - fui, dv = pk.w - fvi;
 #if defined(BSG_EXP_CD_NOP1) && BSG_EXP_CD_NOP1
         if (du > -1e30f) mine |= 1ull << (sft - 1);      // experiment: every pair a candidate
 #else
