@@ -234,7 +234,8 @@ def main():
                             + (", RCCL all_gather of [E, obs+3] fp32 per step" if gather else ""),
                 "envs_per_gpu": E,
                 "num_ac": N,
-                "parallelism": f"env-shard x{world}" + (" + RCCL all_gather (overlapped)" if gather else ""),
+                "parallelism": f"env-shard x{world}" + ((" + RCCL all_gather (overlapped)" if backend == "nccl"
+                                                          else f" + {backend} all_gather") if gather else ""),
                 "backend": backend if world > 1 else None,
             },
             "roofline": {
