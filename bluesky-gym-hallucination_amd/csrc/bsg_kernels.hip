@@ -205,6 +205,7 @@ struct Memo {
   uint64_t spd_bits, spdalt_bits;  // key of ap_tas = casormach2tas(selspd, alt)
   double ap_tas;
   uint64_t lim_tas_bits, lim_h_bits;  // key of the PerfModel.limits speed clamp
+  bool lim_gd;                         //   (and its flight phase: GD or airborne)
   double allow_tas;
   int wp_k;                        // cached waypoint (coords, next-leg bearing, trig)
   double wp_lat, wp_lon, wp_nq, wp_cos, wp_sin;
@@ -239,9 +240,12 @@ __device__ __forceinline__ double key_as_double(uint64_t k) { return __longlong_
 
 __device__ __forceinline__ double allow_h_of(double selalt) { return selalt > HMAX ? HMAX : selalt; }
 
+// OpenAP flight phase GD (on the ground): its own speed envelope and axmax
+__device__ __forceinline__ bool ground_phase(double alt) { return alt / FT <= GD_ALT_FT; }
+
 __device__ __forceinline__ void memo_init(Memo& m, const AC& s) {
   m.alt_bits = kNoKey; m.spd_bits = kNoKey; m.spdalt_bits = kNoKey;
-  m.lim_tas_bits = kNoKey; m.lim_h_bits = kNoKey;
+  m.lim_tas_bits = kNoKey; m.lim_h_bits = kNoKey; m.lim_gd = false;
   m.at = Atmos{0, 0, 0}; m.ap_tas = 0; m.allow_tas = 0;
   m.wp_k = -1; m.wp_lat = 0; m.wp_lon = 0; m.wp_nq = 0; m.wp_cos = 0; m.wp_sin = 0;
   m.tr_bits = kNoKey; m.turnrate = 0;
@@ -264,6 +268,7 @@ __device__ __forceinline__ void memo_load(Memo& m, const double v[MC_FIELDS], co
   if (al == al) {
     m.lim_tas_bits = bits(m.ap_tas);
     m.lim_h_bits = bits(allow_h_of(s0.selalt));
+    m.lim_gd = ground_phase(s0.alt);
     m.allow_tas = fabs(al);
     if (al > 0.0) {
       m.spd_bits = bits(s0.selspd);
@@ -279,7 +284,8 @@ __device__ __forceinline__ void memo_load(Memo& m, const double v[MC_FIELDS], co
 __device__ __forceinline__ void memo_store(const Memo& m, const AC& s, const double old[MC_FIELDS],
                                            double* mc, size_t a, size_t stride) {
   const bool lim_ok = m.lim_tas_bits == bits(m.ap_tas) &&
-                      m.lim_h_bits == bits(allow_h_of(s.selalt)) && m.allow_tas > 0.0;
+                      m.lim_h_bits == bits(allow_h_of(s.selalt)) && m.allow_tas > 0.0 &&
+                      m.lim_gd == ground_phase(s.alt);
   const bool level = m.spd_bits == bits(s.selspd) && m.spdalt_bits == bits(s.alt) &&
                      m.cas_tas_bits == bits(s.tas) && m.cas_alt_bits == bits(s.alt);
   const double v[MC_FIELDS] = {m.ap_tas, !lim_ok ? key_as_double(kNoKey)
@@ -417,29 +423,33 @@ __device__ __forceinline__ void substep(AC& s, Memo& m, double dt, const RouteRe
   } else {
     hdg_cmd = pymod(s.ap_trk, 360.0);
   }
-  // PerfModel.limits (frozen A320 envelope)
+  // PerfModel.limits (frozen A320 envelope; phase GD has its own speed range and axmax)
+  const bool gd = ground_phase(s.alt);
+  const double axmax = gd ? AXMAX_GD : AXMAX;
   const double allow_h = ap_alt > HMAX ? HMAX : ap_alt;
   const uint64_t hb = bits(allow_h);
-  if (bits(m.ap_tas) != m.lim_tas_bits || hb != m.lim_h_bits) {
+  if (bits(m.ap_tas) != m.lim_tas_bits || hb != m.lim_h_bits || gd != m.lim_gd) {
     const Atmos ah = (hb == ab) ? memo_at(m, s.alt, ab) : vatmos(allow_h);
     const double intent_cas = tas2cas_at(m.ap_tas, ah);
-    double allow_cas = intent_cas < VMIN_CAS ? VMIN_CAS : intent_cas;
-    allow_cas = intent_cas > VMAX_CAS ? VMAX_CAS : allow_cas;
+    const double vmin = gd ? 0.0 : VMIN_CAS, vmax = gd ? VMAX_GD : VMAX_CAS;
+    double allow_cas = intent_cas < vmin ? vmin : intent_cas;
+    allow_cas = intent_cas > vmax ? vmax : allow_cas;
     double allow_tas = cas2tas_at(allow_cas, ah);
     const double snd_h = sound_at(ah);
     if (allow_tas / snd_h > MMO) allow_tas = MMO * snd_h;
     m.allow_tas = allow_tas;
     m.lim_tas_bits = bits(m.ap_tas);
     m.lim_h_bits = hb;
+    m.lim_gd = gd;
   }
   const double allow_tas = m.allow_tas;
-  const double vs_max_with_acc = (1 - s.ax / AXMAX) * VSMAX;
+  const double vs_max_with_acc = (1 - s.ax / axmax) * VSMAX;
   double vs_cmd = (vs_cmd0 > 0 && vs_cmd0 > VSMAX) ? vs_max_with_acc : vs_cmd0;
   vs_cmd = (vs_cmd0 < 0 && vs_cmd0 < VSMIN) ? VSMIN : vs_cmd;
   // update_airspeed (traf.cas is evaluated after the last substep, see step_kernel)
   const double delta_spd = allow_tas - s.tas;
-  const bool need_ax = fabs(delta_spd) > fabs(dt * AXMAX);
-  s.ax = (double)need_ax * sgn(delta_spd) * AXMAX;
+  const bool need_ax = fabs(delta_spd) > fabs(dt * axmax);
+  s.ax = (double)need_ax * sgn(delta_spd) * axmax;
   s.tas = need_ax ? s.tas + s.ax * dt : allow_tas;
   if (bits(s.tas) != m.tr_bits) {
     m.turnrate = (G0 * TAN_BANKDEF / npmax(s.tas, EPS_SPD)) * kR2D;

@@ -53,18 +53,27 @@ rho0 = 1.225            # kg/m3
 T0 = 288.15             # K
 Tstrat = 216.65         # K
 
-# Frozen A320 envelope and autopilot defaults (docs/BLUESKY_SUBSET_SPEC.md §A.3)
+# Frozen A320 envelope and autopilot defaults (docs/BLUESKY_SUBSET_SPEC.md §A.3).  The
+# speed / vertical-speed limits and the ground-phase envelope are FITTED to the reference's
+# own SAC training logs (scripts/common/results/logs_backup/*_SAC.csv) by rolling out its
+# saved actors (tests/golden/sac_actors.npz; tests/test_sac_logs.py):
+#   VMAX_CAS: Descent + Vertical episode-length distributions (162.5..163.5 bracket)
+#   VSMAX:    Descent final-altitude distribution (the terminal dive runs at the limit)
+#   VMAX_GD:  Horizontal + PlanWaypoint episode lengths (aircraft created at alt 0)
 BANKDEF = math.radians(25.0)          # ap.bankdef
 TAN_BANKDEF = 0.4663076581549986      # tan(BANKDEF), frozen literal shared with the device code
 APVSDEF = 1500.0 * fpm                # ap.apvsdef  (m/s)
 EPS_SPD = 0.01                        # traf.eps
 AXMAX = 0.5                           # perf.axmax  (m/s2), airborne
 VMIN_CAS = 140.0 * kts                # perf.vmin   (m/s CAS)
-VMAX_CAS = 350.0 * kts                # perf.vmax   (m/s CAS)
+VMAX_CAS = 163.0                      # perf.vmax   (m/s CAS), fitted
 MMO = 0.82                            # perf.mmo
 HMAX = 39800.0 * ft                   # perf.hmax   (m)
-VSMAX = 4000.0 * fpm                  # perf.vsmax  (m/s)
-VSMIN = -4000.0 * fpm                 # perf.vsmin  (m/s)
+VSMAX = 12.1                          # perf.vsmax  (m/s), fitted
+VSMIN = -12.1                         # perf.vsmin  (m/s); unreachable: the intent is |ap.vs|
+GD_ALT_FT = 75.0                      # OpenAP phase GD: alt <= 75 ft
+VMAX_GD = 88.5                        # perf.vmax in phase GD (m/s CAS), fitted; vmin 0
+AXMAX_GD = 2.0                        # perf.axmax in phase GD (m/s2)
 
 # asas defaults (bluesky settings: asas_pzr, asas_pzh, asas_dtlookahead)
 RPZ = 5.0 * nm
@@ -287,15 +296,24 @@ def cre_state(st, idx, aclat, aclon, achdg, acalt, acspd):
     st.actwp[idx] = 0
 
 
-def perf_limits(intent_tas, intent_vs, intent_h, ax):
-    """OpenAP-style PerfModel.limits with the frozen A320 envelope."""
+def ground_phase(alt):
+    """OpenAP flight phase GD (bluesky performance/openap/phase.py): alt <= 75 ft."""
+    return alt / ft <= GD_ALT_FT
+
+
+def perf_limits(intent_tas, intent_vs, intent_h, ax, ground=False):
+    """OpenAP-style PerfModel.limits with the frozen A320 envelope; `ground` = phase GD
+    (its own speed envelope and axmax)."""
+    vmin = np.where(ground, 0.0, VMIN_CAS)
+    vmax = np.where(ground, VMAX_GD, VMAX_CAS)
+    axmax = np.where(ground, AXMAX_GD, AXMAX)
     allow_h = np.where(intent_h > HMAX, HMAX, intent_h)
     intent_cas = vtas2cas(intent_tas, allow_h)
-    allow_cas = np.where(intent_cas < VMIN_CAS, VMIN_CAS, intent_cas)
-    allow_cas = np.where(intent_cas > VMAX_CAS, VMAX_CAS, allow_cas)
+    allow_cas = np.where(intent_cas < vmin, vmin, intent_cas)
+    allow_cas = np.where(intent_cas > vmax, vmax, allow_cas)
     allow_tas = vcas2tas(allow_cas, allow_h)
     allow_tas = np.where(vtas2mach(allow_tas, allow_h) > MMO, vmach2tas(MMO, allow_h), allow_tas)
-    vs_max_with_acc = (1 - ax / AXMAX) * VSMAX
+    vs_max_with_acc = (1 - ax / axmax) * VSMAX
     allow_vs = np.where((intent_vs > 0) & (intent_vs > VSMAX), vs_max_with_acc, intent_vs)
     allow_vs = np.where((intent_vs < 0) & (intent_vs < VSMIN), VSMIN, allow_vs)
     return allow_tas, allow_vs, allow_h
@@ -481,11 +499,13 @@ def traffic_update(st, dt, route_lat, route_lon, route_next_qdr, wind=None):
     else:
         hdg_cmd = pymod(trk_cmd, 360.0)
     # ---- performance limits ------------------------------------------------------------
-    tas_cmd, vs_cmd, alt_cmd = perf_limits(ap_tas, vs_cmd, ap_alt, st.ax)
+    ground = ground_phase(st.alt)
+    tas_cmd, vs_cmd, alt_cmd = perf_limits(ap_tas, vs_cmd, ap_alt, st.ax, ground)
     # ---- update_airspeed ------------------------------------------------------------
+    axmax = np.where(ground, AXMAX_GD, AXMAX)
     delta_spd = tas_cmd - st.tas
-    need_ax = np.abs(delta_spd) > np.abs(dt * AXMAX)
-    st.ax = need_ax * np.sign(delta_spd) * AXMAX
+    need_ax = np.abs(delta_spd) > np.abs(dt * axmax)
+    st.ax = need_ax * np.sign(delta_spd) * axmax
     st.tas = np.where(need_ax, st.tas + st.ax * dt, tas_cmd)
     st.cas = vtas2cas(st.tas, st.alt)
     turnrate = np.degrees(g0 * TAN_BANKDEF / np.maximum(st.tas, EPS_SPD))

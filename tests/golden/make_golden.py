@@ -518,7 +518,7 @@ def main():
         ("descent_keep", lambda: gen_descent(bs, mods, 4, 16, max_steps=25, keep_traffic=True)),
         ("plan", lambda: gen_plan(bs, mods, 4, 17, max_steps=60)),
         ("plan_long", lambda: gen_plan(bs, mods, 2, 18)),
-        ("plan_greedy", lambda: gen_plan(bs, mods, 4, 19, max_steps=120, greedy=True)),
+        ("plan_greedy", lambda: gen_plan(bs, mods, 4, 19, max_steps=200, greedy=True)),
         ("sector_N32", lambda: gen_sector(bs, mods, 3, 15)),
         ("noisy_merge_N8", lambda: gen_noisy_merge(bs, mods, 8, 2, 13, 0.2)),
         ("wind_horizontal_N6", lambda: {**gen_horizontal(bs, mods, 5, 2, 12, wind=WIND_README),
