@@ -12,6 +12,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "bsg_fastpow.h"
+
 namespace bsg {
 
 // ---- constants (bluesky.tools.aero; oracle/bluesky_subset.py) -----------------------
@@ -84,22 +86,35 @@ struct Atmos { double p, rho, T; };
 __device__ __forceinline__ Atmos vatmos(double h) {
   Atmos a;
   a.T = npmax(288.15 - 0.0065 * h, TSTRAT);
-  double rhotrop = 1.225 * pow(a.T / 288.15, 4.256848030018761);
+  double rhotrop = 1.225 * pow_trop(divk(a.T, 288.15));
   double dhstrat = npmax(0.0, h - 11000.0);
-  a.rho = rhotrop * exp(-dhstrat / 6341.552161);
+  // exp(-0.0) == 1 exactly: the troposphere skips the exp (a branch, not a select)
+  a.rho = dhstrat > 0.0 ? rhotrop * exp(divk(-dhstrat, 6341.552161)) : rhotrop * 1.0;
   a.p = a.rho * RGAS * a.T;
   return a;
 }
 
+// vatmos of the two fixed limit altitudes the Vertical/Descent autopilot commands (selalt
+// 1e6 -> allow_h = HMAX, selalt 0): the values NumPy computes (oracle/bluesky_subset.py
+// vatmos; tests/test_fastmath_cpu.py checks these literals against it)
+constexpr Atmos kAtmosHMAX = {0x1.27c7249336b51p+14, 0x1.37b10b426ceafp-2, 0x1.b14cccccccccdp+7};
+constexpr Atmos kAtmosSL = {0x1.8bccff9dc0a57p+16, 0x1.399999999999ap+0, 0x1.2026666666666p+8};
+
+__device__ __forceinline__ Atmos vatmos_limit(double h) {
+  if (bits(h) == bits(HMAX)) return kAtmosHMAX;
+  if (h == 0.0) return kAtmosSL;
+  return vatmos(h);
+}
+
 __device__ __forceinline__ double tas2cas_at(double tas, const Atmos& a) {
-  double qdyn = a.p * (pow(1.0 + a.rho * tas * tas / (7.0 * a.p), 3.5) - 1.0);
-  double cas = sqrt(7.0 * P0 / RHO0 * (pow(qdyn / P0 + 1.0, 2.0 / 7.0) - 1.0));
+  double qdyn = a.p * (pow_3p5(1.0 + a.rho * tas * tas / (7.0 * a.p)) - 1.0);
+  double cas = sqrt(7.0 * P0 / RHO0 * (pow_2o7(divk(qdyn, P0) + 1.0) - 1.0));
   return tas < 0 ? -1 * cas : cas;
 }
 
 __device__ __forceinline__ double cas2tas_at(double cas, const Atmos& a) {
-  double qdyn = P0 * (pow(1.0 + RHO0 * cas * cas / (7.0 * P0), 3.5) - 1.0);
-  double tas = sqrt(7.0 * a.p / a.rho * (pow(1.0 + qdyn / a.p, 2.0 / 7.0) - 1.0));
+  double qdyn = P0 * (pow_3p5(1.0 + divk(RHO0 * cas * cas, 7.0 * P0)) - 1.0);
+  double tas = sqrt(7.0 * a.p / a.rho * (pow_2o7(1.0 + qdyn / a.p) - 1.0));
   return cas < 0 ? -1 * tas : tas;
 }
 
@@ -130,7 +145,7 @@ __device__ __forceinline__ void kwikqdrdist(double lata, double lona, double lat
   double dlon = (pymod((lonb - lona) + 180.0, 360.0) - 180.0) * kD2R;
   double cavelat = cos(((lata + latb) * kD2R) * 0.5);
   double dangle = sqrt(dlat * dlat + dlon * dlon * cavelat * cavelat);
-  *dist = 6371000.0 * dangle / NM;
+  *dist = divk(6371000.0 * dangle, NM);
   *qdr = pymod(atan2(dlon * cavelat, dlat) * kR2D, 360.0);
 }
 
@@ -139,7 +154,7 @@ __device__ __forceinline__ double kwikdist(double lata, double lona, double latb
   double dlon = (pymod((lonb - lona) + 180.0, 360.0) - 180.0) * kD2R;
   double cavelat = cos(((lata + latb) * kD2R) * 0.5);
   double dangle = sqrt(dlat * dlat + dlon * dlon * cavelat * cavelat);
-  return 6371000.0 * dangle / NM;
+  return divk(6371000.0 * dangle, NM);
 }
 
 // kwikdist_matrix element (operation order of the matrix form, merge_env.py:195)
@@ -148,7 +163,7 @@ __device__ __forceinline__ double kwikdist_mat(double lata, double lona, double 
   double dlon = (pymod((lonb - lona) + 180.0, 360.0) - 180.0) * kD2R;
   double cavelat = cos(((latb + lata) * kD2R) * 0.5);
   double dangle = sqrt(dlat * dlat + (dlon * dlon) * (cavelat * cavelat));
-  return 6371000.0 * dangle / NM;
+  return divk(6371000.0 * dangle, NM);
 }
 
 // kwikqdrdist_matrix element (StateBased.detect), [i][j] = from a=i to b=j
@@ -158,7 +173,7 @@ __device__ __forceinline__ void kwikqdrdist_mat(double lata, double lona, double
   double dlon = (pymod((lonb - lona) + 180.0, 360.0) - 180.0) * kD2R;
   double cavelat = cos(((lata + latb) * kD2R) * 0.5);
   double dangle = sqrt(dlat * dlat + (dlon * dlon) * (cavelat * cavelat));
-  *dist = 6371000.0 * dangle / NM;
+  *dist = divk(6371000.0 * dangle, NM);
   *qdr = pymod(atan2(dlon * cavelat, dlat) * kR2D, 360.0);
 }
 
@@ -166,7 +181,7 @@ __device__ __forceinline__ void kwikpos(double latd1, double lond1, double qdr, 
                                         double* lat2, double* lon2) {
   double dx = dist * sin(qdr * kD2R);
   double dy = dist * cos(qdr * kD2R);
-  double dlat = dy / 60.0;
+  double dlat = divk(dy, 60.0);
   double dlon = dx / npmax(0.01, 60.0 * cos(latd1 * kD2R));
   *lat2 = latd1 + dlat;
   *lon2 = pymod((lond1 + dlon) + 180.0, 360.0) - 180.0;
@@ -252,7 +267,7 @@ __device__ __forceinline__ double qdrdist_exact_nm(double latd1, double latd2, d
         npmax(0.000001, fabs(latd1) + fabs(latd2));
   }
   double d = r * acos(x);
-  return d / NM;
+  return divk(d, NM);
 }
 
 // Bounds [lo, hi] (metres) on the distance the exact path would yield, (d / NM) * NM with

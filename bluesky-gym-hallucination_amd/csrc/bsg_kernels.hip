@@ -212,6 +212,8 @@ struct Memo {
   double coslat, sinlat;           // cos/sin(lat * D2R) of the current latitude
   uint64_t tr_bits;                // key of turnrate = deg(g0*tan(bank)/max(tas, eps))
   double turnrate;
+  uint64_t hdg_bits;               // key of (shdg, chdg) = sincos(hdg * D2R)
+  double shdg, chdg;
   uint64_t rad_bits;               // key of the LNAV turn radius tas^2/(g0*tan(bank))
   double turnrad;
   double last_alt;                 // altitude at the start of the latest substep
@@ -241,7 +243,7 @@ __device__ __forceinline__ double key_as_double(uint64_t k) { return __longlong_
 __device__ __forceinline__ double allow_h_of(double selalt) { return selalt > HMAX ? HMAX : selalt; }
 
 // OpenAP flight phase GD (on the ground): its own speed envelope and axmax
-__device__ __forceinline__ bool ground_phase(double alt) { return alt / FT <= GD_ALT_FT; }
+__device__ __forceinline__ bool ground_phase(double alt) { return divk(alt, FT) <= GD_ALT_FT; }
 
 __device__ __forceinline__ void memo_init(Memo& m, const AC& s) {
   m.alt_bits = kNoKey; m.spd_bits = kNoKey; m.spdalt_bits = kNoKey;
@@ -249,6 +251,7 @@ __device__ __forceinline__ void memo_init(Memo& m, const AC& s) {
   m.at = Atmos{0, 0, 0}; m.ap_tas = 0; m.allow_tas = 0;
   m.wp_k = -1; m.wp_lat = 0; m.wp_lon = 0; m.wp_nq = 0; m.wp_cos = 0; m.wp_sin = 0;
   m.tr_bits = kNoKey; m.turnrate = 0;
+  m.hdg_bits = kNoKey; m.shdg = 0; m.chdg = 0;
   m.rad_bits = kNoKey; m.turnrad = 0;
   m.last_alt = s.alt;
   m.cas_tas_bits = kNoKey; m.cas_alt_bits = kNoKey;
@@ -339,7 +342,7 @@ __device__ __forceinline__ void substep(AC& s, Memo& m, double dt, const RouteRe
     // the waypoint distance only feeds `dist < turndist` (turndist <= turnrad while the
     // leg change is <= 90 deg) and `dist/|gs| < 4 s`; beyond both it need not be exact
     if (bits(s.tas) != m.rad_bits) {
-      m.turnrad = s.tas * s.tas / (npmax(0.01, TAN_BANKDEF) * G0);
+      m.turnrad = divk(s.tas * s.tas, npmax(0.01, TAN_BANKDEF) * G0);
       m.rad_bits = bits(s.tas);
     }
     const double turnrad = m.turnrad;
@@ -429,7 +432,7 @@ __device__ __forceinline__ void substep(AC& s, Memo& m, double dt, const RouteRe
   const double allow_h = ap_alt > HMAX ? HMAX : ap_alt;
   const uint64_t hb = bits(allow_h);
   if (bits(m.ap_tas) != m.lim_tas_bits || hb != m.lim_h_bits || gd != m.lim_gd) {
-    const Atmos ah = (hb == ab) ? memo_at(m, s.alt, ab) : vatmos(allow_h);
+    const Atmos ah = (hb == ab) ? memo_at(m, s.alt, ab) : vatmos_limit(allow_h);
     const double intent_cas = tas2cas_at(m.ap_tas, ah);
     const double vmin = gd ? 0.0 : VMIN_CAS, vmax = gd ? VMAX_GD : VMAX_CAS;
     double allow_cas = intent_cas < vmin ? vmin : intent_cas;
@@ -443,7 +446,8 @@ __device__ __forceinline__ void substep(AC& s, Memo& m, double dt, const RouteRe
     m.lim_gd = gd;
   }
   const double allow_tas = m.allow_tas;
-  const double vs_max_with_acc = (1 - s.ax / axmax) * VSMAX;
+  // s.ax / axmax with axmax in {0.5, 2}: multiplying by the exact reciprocal is the same
+  const double vs_max_with_acc = (1 - s.ax * (gd ? 1.0 / AXMAX_GD : 1.0 / AXMAX)) * VSMAX;
   double vs_cmd = (vs_cmd0 > 0 && vs_cmd0 > VSMAX) ? vs_max_with_acc : vs_cmd0;
   vs_cmd = (vs_cmd0 < 0 && vs_cmd0 < VSMIN) ? VSMIN : vs_cmd;
   // update_airspeed (traf.cas is evaluated after the last substep, see step_kernel)
@@ -451,13 +455,19 @@ __device__ __forceinline__ void substep(AC& s, Memo& m, double dt, const RouteRe
   const bool need_ax = fabs(delta_spd) > fabs(dt * axmax);
   s.ax = (double)need_ax * sgn(delta_spd) * axmax;
   s.tas = need_ax ? s.tas + s.ax * dt : allow_tas;
-  if (bits(s.tas) != m.tr_bits) {
-    m.turnrate = (G0 * TAN_BANKDEF / npmax(s.tas, EPS_SPD)) * kR2D;
-    m.tr_bits = bits(s.tas);
-  }
-  const double turnrate = m.turnrate;
   const double delhdg = pymod(hdg_cmd - s.hdg + 180.0, 360.0) - 180.0;
-  const bool swhdgsel = fabs(delhdg) > fabs(dt * turnrate);
+  // |delhdg| > |dt*turnrate| is false at delhdg == 0 whatever turnrate is: a straight
+  // flying aircraft needs no turn rate (and no division)
+  bool swhdgsel = false;
+  double turnrate = 0.0;
+  if (delhdg != 0.0) {
+    if (bits(s.tas) != m.tr_bits) {
+      m.turnrate = (G0 * TAN_BANKDEF / npmax(s.tas, EPS_SPD)) * kR2D;
+      m.tr_bits = bits(s.tas);
+    }
+    turnrate = m.turnrate;
+    swhdgsel = fabs(delhdg) > fabs(dt * turnrate);
+  }
   s.hdg = pymod(swhdgsel ? s.hdg + dt * turnrate * sgn(delhdg) : hdg_cmd, 360.0);
   const double delta_alt = allow_h - s.alt;
   const bool swaltsel = fabs(delta_alt) > npmax(10 * FT, fabs(2 * fabs(dt * s.vs)));
@@ -468,8 +478,11 @@ __device__ __forceinline__ void substep(AC& s, Memo& m, double dt, const RouteRe
   s.vs = need_az ? s.vs + az * dt : target_vs;
   if (!isfinite(s.vs)) s.vs = 0.0;
   // update_groundspeed + update_pos
-  double shdg, chdg;
-  sincos(s.hdg * kD2R, &shdg, &chdg);
+  if (bits(s.hdg) != m.hdg_bits) {        // straight flight keeps its heading trig
+    sincos(s.hdg * kD2R, &m.shdg, &m.chdg);
+    m.hdg_bits = bits(s.hdg);
+  }
+  const double shdg = m.shdg, chdg = m.chdg;
   double gsnorth = s.tas * chdg;
   double gseast = s.tas * shdg;
   if constexpr (WIND) {
@@ -484,11 +497,11 @@ __device__ __forceinline__ void substep(AC& s, Memo& m, double dt, const RouteRe
       s.trk = s.hdg;
     }
   }
-  if (swaltsel) s.alt = rint((s.alt + s.vs * dt) * 1e6) / 1e6;   // a branch: level flight
+  if (swaltsel) s.alt = divk(rint((s.alt + s.vs * dt) * 1e6), 1e6);   // a branch: level flight
   else s.alt = allow_h;                                            // skips the division
-  s.lat = s.lat + (dt * gsnorth / Rearth) * kR2D;
+  s.lat = s.lat + divk(dt * gsnorth, Rearth) * kR2D;
   sincos(s.lat * kD2R, &m.sinlat, &m.coslat);
-  s.lon = s.lon + (dt * gseast / m.coslat / Rearth) * kR2D;
+  s.lon = s.lon + divk(dt * gseast / m.coslat, Rearth) * kR2D;
 }
 
 // ---- LDS staging (one wave per block; GS lanes per env) -------------------------------
@@ -640,7 +653,7 @@ __device__ __forceinline__ CdOut cd_pair(const LT& L, int i, int k) {
   const double dlon = (pymod((lonk - loni) + 180.0, 360.0) - 180.0) * kD2R;
   const double cavelat = cos(((lati + latk) * kD2R) * 0.5);
   const double dangle = sqrt(dlat * dlat + (dlon * dlon) * (cavelat * cavelat));
-  const double dist = (6371000.0 * dangle / NM) * NM + 0.0;     // + 1e9*I, I = 0
+  const double dist = divk(6371000.0 * dangle, NM) * NM + 0.0;     // + 1e9*I, I = 0
   const double du = cd_u(L, k) - cd_u(L, i);
   const double dv = cd_v(L, k) - cd_v(L, i);
   double dv2 = du * du + dv * dv;
@@ -976,7 +989,7 @@ __device__ __forceinline__ bool lane_obs(const LT& L, int base, int lane, double
   const double dlat = (latj - lat0) * kD2R;
   const double dlon = (pymod((lonj - lon0) + 180.0, 360.0) - 180.0) * kD2R;
   const double cavelat = cos(((lat0 + latj) * kD2R) * 0.5);
-  const double dist = 6371000.0 * sqrt(dlat * dlat + dlon * dlon * cavelat * cavelat) / NM;
+  const double dist = divk(6371000.0 * sqrt(dlat * dlat + dlon * dlon * cavelat * cavelat), NM);
   const double qdr = pymod(atan2(dlon * cavelat, dlat) * kR2D, 360.0);
   if constexpr (KIND == BSG_ENV_MERGE) {
     // merge_env.py:195-218
@@ -989,7 +1002,7 @@ __device__ __forceinline__ bool lane_obs(const LT& L, int base, int lane, double
       *sortkey = __builtin_inf();
       return false;
     }
-    const double dmat = 6371000.0 * sqrt(dlat * dlat + (dlon * dlon) * (cavelat * cavelat)) / NM;
+    const double dmat = divk(6371000.0 * sqrt(dlat * dlat + (dlon * dlon) * (cavelat * cavelat)), NM);
     const double x_r = (dist * 1.852 * 1000) * cb;
     const double y_r = (dist * 1.852 * 1000) * sb;
     // vx = cos(hdg)*tas == v = tas*cos(hdg) bitwise (LDS staging)
@@ -1054,39 +1067,39 @@ __device__ __forceinline__ void write_lane_obs(float* obs, float* fobs, float* l
   if constexpr (KIND == BSG_ENV_SECTOR_CR) {
     if (rank < K) {                         // sector_cr_env.py:280-291
       put(2 + rank, o[4]);                  // cos(track)
-      put(2 + K + rank, (o[6] - 50000.) / 15000.);   // distances
+      put(2 + K + rank, divk((o[6] - 50000.), 15000.0));   // distances
       put(3 + 2 * K + rank, o[5]);          // sin(track)
-      put(3 + 3 * K + rank, o[2] / 32);     // vx_r
-      put(3 + 4 * K + rank, o[3] / 66);     // vy_r
-      put(3 + 5 * K + rank, o[0] / 13000);  // x_r
-      put(3 + 6 * K + rank, o[1] / 13000);  // y_r
+      put(3 + 3 * K + rank, divk(o[2], 32.0));     // vx_r
+      put(3 + 4 * K + rank, divk(o[3], 66.0));     // vy_r
+      put(3 + 5 * K + rank, divk(o[0], 13000.0));  // x_r
+      put(3 + 6 * K + rank, divk(o[1], 13000.0));  // y_r
     }
   } else if constexpr (KIND == BSG_ENV_MERGE) {
     if (rank < K) {
       put(2 + rank, o[4]);                  // cos(track)
-      put(2 + K + rank, o[6] / 250);        // distances
+      put(2 + K + rank, divk(o[6], 250.0));        // distances
       put(4 + 2 * K + rank, o[5]);          // sin(track)
-      put(4 + 3 * K + rank, o[2] / 150);    // vx_r
-      put(4 + 4 * K + rank, o[3] / 150);    // vy_r
-      put(5 + 5 * K + rank, o[0] / 1000000);// x_r
-      put(5 + 6 * K + rank, o[1] / 1000000);// y_r
+      put(4 + 3 * K + rank, divk(o[2], 150.0));    // vx_r
+      put(4 + 4 * K + rank, divk(o[3], 150.0));    // vy_r
+      put(5 + 5 * K + rank, divk(o[0], 1000000.0));// x_r
+      put(5 + 6 * K + rank, divk(o[1], 1000000.0));// y_r
     }
   } else if constexpr (KIND == BSG_ENV_VERTICAL_CR) {
     const int NI = N - 1, i = j - 1;
-    put(1 + i, o[3] / 3000);                // altitude_difference
+    put(1 + i, divk(o[3], 3000.0));                // altitude_difference
     put(1 + NI + i, o[1]);                  // cos_difference_pos
-    put(1 + 2 * NI + i, o[0] / 200);        // intruder_distance
+    put(1 + 2 * NI + i, divk(o[0], 200.0));        // intruder_distance
     put(2 + 3 * NI + i, o[2]);              // sin_difference_pos
-    put(4 + 4 * NI + i, o[4] / 150);        // x_difference_speed
-    put(4 + 5 * NI + i, o[5] / 150);        // y_difference_speed
+    put(4 + 4 * NI + i, divk(o[4], 150.0));        // x_difference_speed
+    put(4 + 5 * NI + i, divk(o[5], 150.0));        // y_difference_speed
     put(4 + 6 * NI + i, o[6]);              // z_difference_speed
   } else if constexpr (KIND == BSG_ENV_HORIZONTAL_CR) {
     const int NI = N - 1, i = j - 1;
     put(i, o[1]);                           // cos_difference_pos
-    put(NI + 1 + i, o[0] / 150);            // intruder_distance
+    put(NI + 1 + i, divk(o[0], 150.0));            // intruder_distance
     put(2 * NI + 1 + i, o[2]);              // sin_difference_pos
-    put(3 * NI + 3 + i, o[4] / 150);        // x_difference_speed
-    put(4 * NI + 3 + i, o[5] / 150);        // y_difference_speed
+    put(3 * NI + 3 + i, divk(o[4], 150.0));        // x_difference_speed
+    put(4 * NI + 3 + i, divk(o[5], 150.0));        // y_difference_speed
   }
 }
 
@@ -1102,8 +1115,8 @@ __device__ __forceinline__ void own_obs(const KParams& p, const LT& L, int lane,
       double wn, we, sh, ch;
       wind_at(p.wind, lat, lon, L.alt[lane], &wn, &we);
       sincos(L.hdg[lane] * kD2R, &sh, &ch);
-      sc[5] = (wn * ch + we * sh) / 50;
-      sc[6] = (-wn * sh + we * ch) / 50;
+      sc[5] = divk((wn * ch + we * sh), 50.0);
+      sc[6] = divk((-wn * sh + we * ch), 50.0);
     }
   }
   if constexpr (KIND == BSG_ENV_MERGE) {
@@ -1113,7 +1126,7 @@ __device__ __forceinline__ void own_obs(const KParams& p, const LT& L, int lane,
     *drift = bound180(L.hdg[lane] - wqdr);
     double sd, cd;
     sincos(*drift * kD2R, &sd, &cd);
-    sc[0] = L.tas[lane]; sc[1] = cd; sc[2] = (double)ev.wpt_reach; sc[3] = sd; sc[4] = *wdist / 250;
+    sc[0] = L.tas[lane]; sc[1] = cd; sc[2] = (double)ev.wpt_reach; sc[3] = sd; sc[4] = divk(*wdist, 250.0);
   } else if constexpr (KIND == BSG_ENV_SECTOR_CR) {
     // sector_cr_env.py:233-243
     double wqdr, wd;
@@ -1121,7 +1134,7 @@ __device__ __forceinline__ void own_obs(const KParams& p, const LT& L, int lane,
     *drift = bound180(L.hdg[lane] - wqdr);
     double sd, cd;
     sincos(*drift * kD2R, &sd, &cd);
-    sc[0] = (L.tas[lane] - 150) / 6; sc[1] = cd; sc[2] = sd; sc[3] = 0.0; sc[4] = 0.0;
+    sc[0] = divk((L.tas[lane] - 150), 6.0); sc[1] = cd; sc[2] = sd; sc[3] = 0.0; sc[4] = 0.0;
   } else if constexpr (KIND == BSG_ENV_STATIC_OBSTACLE) {
     // static_obstacle_env.py:231-246 (waypoint terms; obstacles in static_obs_write)
     double wqdr, wd;
@@ -1130,7 +1143,7 @@ __device__ __forceinline__ void own_obs(const KParams& p, const LT& L, int lane,
     *drift = bound180(L.hdg[lane] - wqdr);
     double sd, cd;
     sincos(*drift * kD2R, &sd, &cd);
-    sc[0] = *wdist / 170; sc[1] = cd; sc[2] = sd; sc[3] = 0.0; sc[4] = 0.0;
+    sc[0] = divk(*wdist, 170.0); sc[1] = cd; sc[2] = sd; sc[3] = 0.0; sc[4] = 0.0;
   } else if constexpr (KIND == BSG_ENV_PLAN_WAYPOINT) {
     // plan_obs (five waypoints)
   } else if constexpr (KIND == BSG_ENV_HORIZONTAL_CR) {
@@ -1141,12 +1154,12 @@ __device__ __forceinline__ void own_obs(const KParams& p, const LT& L, int lane,
     *drift = bound180(L.hdg[lane] - wqdr);
     double sd, cd;
     sincos(*drift * kD2R, &sd, &cd);
-    sc[0] = cd; sc[1] = sd; sc[2] = *wdist / 150; sc[3] = 0.0; sc[4] = 0.0;
+    sc[0] = cd; sc[1] = sd; sc[2] = divk(*wdist, 150.0); sc[3] = 0.0; sc[4] = 0.0;
   } else {
     const double altitude = L.alt[lane], vz = L.vs[lane];
     *rwd = 200 - kwikdist(52.0, 4.0, lat, lon) * 1.852;
-    sc[0] = (altitude - 1500) / 3000; sc[1] = (vz - 0) / 5; sc[2] = (ev.target_alt - 1500) / 3000;
-    sc[3] = (*rwd - 100) / 200; sc[4] = 0.0;
+    sc[0] = divk((altitude - 1500), 3000.0); sc[1] = divk((vz - 0), 5.0); sc[2] = divk((ev.target_alt - 1500), 3000.0);
+    sc[3] = divk((*rwd - 100), 200.0); sc[4] = 0.0;
   }
 }
 
@@ -1210,8 +1223,8 @@ __device__ __forceinline__ void static_obs_write(const double* geo, double lat, 
     double sb, cb;
     sincos(bearing * kD2R, &sb, &cb);
     put(o, cb);                                         // cos_difference_restricted_area_pos
-    put(SO_NOBST + 3 + o, (d * 1.852) / 170);           // restricted_area_distance
-    put(2 * SO_NOBST + 3 + o, g[2] / 50);               // restricted_area_radius
+    put(SO_NOBST + 3 + o, divk((d * 1.852), 170.0));           // restricted_area_distance
+    put(2 * SO_NOBST + 3 + o, divk(g[2], 50.0));               // restricted_area_radius
     put(3 * SO_NOBST + 3 + o, sb);                      // sin_difference_restricted_area_pos
   }
 }
@@ -1232,7 +1245,7 @@ __device__ __forceinline__ void plan_obs(const double* geo, double lat, double l
     const double f = ((reach >> k) & 1) ? 0.0 : 1.0;
     po[k] = f * cd;                                  // cos_difference
     po[PW_NWPT + k] = f * sd;                        // sin_difference
-    po[2 * PW_NWPT + k] = f * dkm[k] / 75;           // waypoint_distance
+    po[2 * PW_NWPT + k] = divk(f * dkm[k], 75.0);           // waypoint_distance
   }
 }
 
@@ -1690,7 +1703,7 @@ __global__ __launch_bounds__(64) void step_kernel(KParams p) {
       wdist = own.wdist;
       drift = own.drift;
       sc[0] = L.tas[lane]; sc[1] = own.cd; sc[2] = (double)ev.wpt_reach; sc[3] = own.sd;
-      sc[4] = wdist / 250;
+      sc[4] = divk(wdist, 250.0);
     } else {
       own_obs<KIND>(p, L, lane, ev, sc, &wdist, &drift, &rwd);
     }

@@ -1,0 +1,84 @@
+// Host accuracy check of bsg_fastpow.h (container-only dev tool, no GPU):
+//   hipcc -O2 -x hip --offload-arch=gfx950 tools/fastpow/ulp_check.cpp -o /tmp/ulp_check && /tmp/ulp_check
+// The polynomials are FMA/mul/add chains, so the host evaluates them bit for bit as
+// gfx950 does (IEEE binary64, round to nearest).  For each power: N random arguments
+// uniform on its range plus a dense sweep; errors in ulps of the result against powl
+// (x87 extended, 64-bit mantissa) and against glibc pow (what NumPy's np.power calls).
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <random>
+
+#include "../../bluesky-gym-hallucination_amd/csrc/bsg_fastpow.h"
+
+static double ulp_of(double x) { return std::nextafter(std::fabs(x), INFINITY) - std::fabs(x); }
+
+struct Stat {
+  double max_ref = 0, max_glibc = 0;
+  long n = 0, same = 0, off1 = 0;
+  void add(double ours, double glibc, long double ref) {
+    const double u = ulp_of((double)ref);
+    const double er = (double)std::fabs((long double)ours - ref) / u;
+    const double eg = std::fabs(ours - glibc) / ulp_of(glibc);
+    if (er > max_ref) max_ref = er;
+    if (eg > max_glibc) max_glibc = eg;
+    ++n;
+    if (ours == glibc) ++same;
+    else if (eg <= 1.0) ++off1;
+  }
+};
+
+template <class F>
+static void run(const char* name, double lo, double hi, long double c, double cd, F f) {
+  Stat s;
+  std::mt19937_64 rng(12345);
+  std::uniform_real_distribution<double> U(lo, hi);
+  const long NR = 4000000, ND = 4000000;
+  for (long i = 0; i < NR + ND; ++i) {
+    const double x = i < NR ? U(rng) : lo + (hi - lo) * (double)(i - NR) / (double)(ND - 1);
+    s.add(f(x), std::pow(x, cd), powl((long double)x, c));
+  }
+  std::printf("%-24s [%g, %g]: %ld args  max err vs powl %.3f ulp  max |ours - glibc pow| %.3f ulp  "
+              "bit-identical to glibc %.2f%%  1 ulp apart %.2f%%\n",
+              name, lo, hi, s.n, s.max_ref, s.max_glibc, 100.0 * s.same / s.n, 100.0 * s.off1 / s.n);
+}
+
+// div_r / divk against IEEE '/' for the divisors the kernel uses: uniform numerators over
+// [-1e7, 1e7] and numerators placed next to a rounding boundary (x = RN(q*y) for q near a
+// midpoint), which are the cases a wrong reciprocal method gets wrong
+static void div_check() {
+  const double ys[] = {288.15, 709275.0, 101325.0, 6371000.0, 1e6, 0.3048, 1852.0, 150.0, 250.0,
+                       1000000.0, 3000.0, 200.0, 1000.0, 13000.0, 15000.0, 32.0, 66.0, 6.0, 170.0,
+                       75.0, 50.0, 5.0, 12.5, 6341.552161, 0.4663076581549986 * 9.80665};
+  std::mt19937_64 rng(7);
+  for (double y : ys) {
+    const double ry = 1.0 / y;
+    long bad = 0, n = 0;
+    std::uniform_real_distribution<double> U(-1e7, 1e7);
+    std::uniform_int_distribution<int> E(-30, 30);
+    for (long i = 0; i < 20000000; ++i) {
+      double x = U(rng);
+      if (i & 1) x = std::ldexp(x, E(rng));
+      if ((i & 3) == 3) {   // near-halfway: x = q*y with q's last bit flipped half-way
+        double q = x / y;
+        x = q * y;
+      }
+      ++n;
+      volatile double a = x, b = y;
+      if (bsg::div_r(x, y, ry) != a / b) ++bad;
+    }
+    std::printf("div by %-22.17g %ld numerators, %ld differ from IEEE division\n", y, n, bad);
+  }
+}
+
+int main() {
+  div_check();
+  const double cT = 4.256848030018761, c27 = 2.0 / 7.0;
+  run("pow(x, 4.256848030018761)", bsg::kPowT_LO, bsg::kPowT_HI, (long double)cT, cT,
+      [](double x) { return bsg::pow_trop(x); });
+  run("pow(z, 3.5)", bsg::kPow35_LO, bsg::kPow35_HI, 3.5L, 3.5, [](double x) { return bsg::pow_3p5(x); });
+  run("pow(y, 2.0/7.0)", bsg::kPow27_LO, bsg::kPow27_HI, (long double)c27, c27,
+      [](double x) { return bsg::pow_2o7(x); });
+  return 0;
+}
