@@ -3,8 +3,9 @@
 Contract (driver): `python bench.py --gpus N --steps K --warmup W`; N>1 is launched with
 torch.distributed.run, one rank per GPU.  Rank 0 prints ONE JSON line.
 
-Workload (BASELINE.json metric): MergeEnv-v0, 32 aircraft per env, 4096 envs per GPU
-(weak scaling: env shards are independent), ACTION_FREQUENCY=10 substeps of DT=5 s,
+Workload (BASELINE.json metric): MergeEnv-v0, 32 aircraft per env, 4096 envs in total
+split over the N GPUs (strong scaling, SURVEY C4: 4096/N envs per rank; `--weak` keeps
+4096 envs per GPU instead), ACTION_FREQUENCY=10 substeps of DT=5 s,
 StateBased all-pairs CPA on every step, Gymnasium NEXT_STEP autoreset inside the timed
 region.  Spawns are drawn on the device (Philox); actions come from a bank of U(-1,1)
 batches resident in HBM before timing starts.  With N>1 every step also all-gathers the
@@ -23,7 +24,8 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path[:0] = [REPO, os.path.join(REPO, "bluesky-gym-hallucination_amd")]
 
 METRIC = "env steps/sec (whole node), MergeEnv-v0 4096 envs × 32 aircraft, 1/2/4/8 GPUs"
-TIMING_EVERY = 10              # HIP event pair around every 10th launch of the timed region
+TIMING_EVERY = 10              # post-region cross-check: event pair around every 10th launch
+MIN_SAMPLES = 10               #   ... until at least this many launches are sampled
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md, chip table)
 
 
@@ -46,12 +48,12 @@ def layout_bytes_per_env_step(N, A=2, O=40, K=5, cd=True):
 
 
 def _cpu_worker(args):
-    """One host core: the batched NumPy oracle on 128 Merge envs x 32 aircraft, CD on,
+    """One host core: the batched NumPy oracle on E Merge envs x 32 aircraft (128: the
+    batched form; 1: one env per process, the reference's SubprocVecEnv layout), CD on,
     NEXT_STEP autoreset, stepped for `seconds`.  Returns (env-steps, elapsed s)."""
-    seconds, seed = args
+    seconds, seed, E = args
     import numpy as np
     from oracle import batched as ob
-    E = 128
     o = ob.MergeOracle(E, num_ac=32, seed=seed, compute_cd=True)
     o.reset()
     rng = np.random.default_rng(seed)
@@ -83,9 +85,11 @@ def cpu_baseline(seconds: float):
     for v in ("OMP_NUM_THREADS", "OPENBLAS_NUM_THREADS", "MKL_NUM_THREADS"):
         os.environ[v] = "1"
     with mp.get_context("fork").Pool(P) as pool:
-        res = pool.map(_cpu_worker, [(seconds, 11 + w) for w in range(P)])
+        res = pool.map(_cpu_worker, [(seconds, 11 + w, 128) for w in range(P)])
+        res1 = pool.map(_cpu_worker, [(seconds / 3, 11 + w, 1) for w in range(P)])
     value = sum(n / el for n, el in res)
     per = [n / el for n, el in res]
+    per1 = [n / el for n, el in res1]
     model = platform.processor() or "unknown"
     try:
         with open("/proc/cpuinfo") as f:
@@ -99,7 +103,12 @@ def cpu_baseline(seconds: float):
             "sample": f"oracle/batched.py MergeOracle, {P} processes x 128 envs x 32 aircraft, "
                       f"CD on, {seconds:.0f} s each ({min(per):.0f}-{max(per):.0f} env-steps/s "
                       f"per core), NumPy fp64 one thread per process on '{model}' "
-                      f"({avail} CPUs available to this process, {os.cpu_count()} on the host)"}
+                      f"({avail} CPUs available to this process, {os.cpu_count()} on the host)",
+            # one env per process, as the reference runs (SubprocVecEnv): the same oracle at E=1
+            "per_env": {"value": sum(per1), "unit": "env_steps/s", "cores": P,
+                        "sample": f"MergeOracle with 1 env x 32 aircraft per process, {P} processes, "
+                                  f"{seconds / 3:.0f} s each ({min(per1):.0f}-{max(per1):.0f} "
+                                  f"env-steps/s per core)"}}
 
 
 def load_profile(E):
@@ -121,8 +130,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--envs", type=int, default=4096, help="envs per GPU (weak scaling)")
-    ap.add_argument("--total-envs", type=int, default=0, help="strong scaling: total envs")
+    ap.add_argument("--total-envs", type=int, default=4096,
+                    help="strong scaling (default, SURVEY C4): envs over all GPUs")
+    ap.add_argument("--weak", action="store_true", help="weak scaling: --envs-per-gpu on every GPU")
+    ap.add_argument("--envs-per-gpu", type=int, default=4096)
     ap.add_argument("--num-ac", type=int, default=32)
     ap.add_argument("--no-cd", action="store_true")
     ap.add_argument("--no-gather", action="store_true")
@@ -152,7 +163,9 @@ def main():
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
-    E = args.envs if not args.total_envs else args.total_envs // world
+    E = args.envs_per_gpu if args.weak else args.total_envs // world
+    if not args.weak and E * world != args.total_envs:
+        raise SystemExit(f"--total-envs {args.total_envs} does not split over {world} GPUs")
     gather = world > 1 and not args.no_gather
     make_local = lambda **kw: MergeVectorEnv(num_ac=args.num_ac, seed=1234,  # noqa: E731
                                              compute_cd=not args.no_cd, **kw)
@@ -180,24 +193,35 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    batch.step_timing()                       # discard
-    batch.set_timing(TIMING_EVERY)
+    # HIP events on the launch stream (torch's current stream: core.DeviceBatch launches
+    # there) bracket the K back-to-back launches; nothing is inserted between launches
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
+    ev0.record()
     for k in range(args.steps):
         one(k)
+    ev1.record()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
+    kern_avg_ms = ev0.elapsed_time(ev1) / args.steps
+    # cross-check after the timed region: an event pair around every TIMING_EVERY-th launch
+    # (each pair serialises the stream, so it is kept out of the timed region), >= 10 samples
+    batch.step_timing()                       # discard
+    batch.set_timing(TIMING_EVERY)
+    for k in range(TIMING_EVERY * MIN_SAMPLES):
+        one(k)
+    torch.cuda.synchronize()
     batch.set_timing(False)
-    kern_ms, launches = batch.step_timing()
+    samp_ms, samples = batch.step_timing()
+    samp_ms = samp_ms / max(samples, 1)
     if world > 1:
-        t = torch.tensor([el, kern_ms / max(launches, 1)], dtype=torch.float64, device=dev)
+        t = torch.tensor([el, kern_avg_ms, samp_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el, kern_avg_ms = float(t[0]), float(t[1])
-    else:
-        kern_avg_ms = kern_ms / max(launches, 1)
+        el, kern_avg_ms, samp_ms = float(t[0]), float(t[1]), float(t[2])
 
     if rank == 0:
         total = world * E * args.steps
@@ -224,14 +248,15 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": el * 1e3 / args.steps,
             "higher_is_better": True,
-            "scaling": "strong" if args.total_envs else "weak",
+            "scaling": "weak" if args.weak else "strong",
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic: device Philox spawns (merge_env.py distributions), U(-1,1) actions",
             "config": {
-                "workload": f"MergeEnv-v0 {E} envs x {N} aircraft per GPU, 10 substeps x DT 5 s, "
+                "workload": f"MergeEnv-v0 {world * E} envs x {N} aircraft ({E} per GPU), 10 substeps x DT 5 s, "
                             f"StateBased CD {'off' if args.no_cd else 'on'}, NEXT_STEP autoreset"
                             + (", RCCL all_gather of [E, obs+3] fp32 per step" if gather else ""),
+                "envs_total": world * E,
                 "envs_per_gpu": E,
                 "num_ac": N,
                 "parallelism": f"env-shard x{world}" + ((" + RCCL all_gather (overlapped)" if backend == "nccl"
@@ -239,16 +264,26 @@ def main():
                 "backend": backend if world > 1 else None,
             },
             "roofline": {
-                "bound": "hbm",
+                # the binding limit is fp64 VALU dependency latency; `frac`
+                # is the HBM fraction the roofline contract asks for, `valu` the VALU view
+                "bound": "valu-latency",
                 "achieved": achieved,
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": prof["hbm_bytes_per_launch"] if prof else None,
+                "traffic_source": (f"profiles/traffic.json: rocprofv3 FETCH_SIZE/WRITE_SIZE passes of "
+                                   f"this workload ({prof.get('source', '')}), not this run")
+                                  if prof else None,
                 "kernel": "bsg::step_kernel<MERGE,32>",
                 "kernel_avg_ms": kern_avg_ms,
-                "kernel_timing": f"HIP event pair on the launch stream around every "
-                                 f"{TIMING_EVERY}th launch of the timed region ({launches} launches)",
+                "kernel_timing": f"HIP events on the launch stream bracketing the {args.steps} "
+                                 f"back-to-back launches of the timed region (GPU time per launch, "
+                                 f"incl. the dispatch gap between launches)",
+                "sampled_launch_ms": samp_ms,
+                "sampled_launch_timing": f"cross-check after the timed region: event pair around "
+                                         f"every {TIMING_EVERY}th launch, {samples} samples "
+                                         f"(each pair serialises the stream)",
                 "bytes_per_env_step": B,
                 "layout_bytes_per_env_step": layout_bytes_per_env_step(N, cd=not args.no_cd),
                 "valu": valu,

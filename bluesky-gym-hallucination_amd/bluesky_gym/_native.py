@@ -18,7 +18,7 @@ WIND_NALT = 451
 
 ENV_MERGE, ENV_VERTICAL_CR, ENV_DESCENT, ENV_HORIZONTAL_CR = 0, 1, 2, 3
 ENV_STATIC_OBSTACLE, ENV_SECTOR_CR, ENV_PLAN_WAYPOINT = 4, 5, 6
-FLAG_RESET_PENDING, FLAG_AC_PRESENT = 1, 2
+FLAG_RESET_PENDING, FLAG_AC_PRESENT, FLAG_SPAWN_OVERFLOW = 1, 2, 4   # include/bsg.h BSG_FLAG_*
 AUTORESET_NONE, AUTORESET_NEXT_STEP, AUTORESET_SAME_STEP = 0, 1, 2
 
 E_CODES = {-1: "BSG_E_INVALID_ARG", -2: "BSG_E_HIP", -3: "BSG_E_STATE", -4: "BSG_E_UNSUPPORTED"}

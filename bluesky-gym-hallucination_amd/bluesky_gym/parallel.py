@@ -72,21 +72,38 @@ class ShardedVectorEnv:
         self.overlap = overlap and self.world > 1
         self._work = [None, None]
 
-    def reset(self, **kw):
-        return self.local.reset(**kw)
-
-    def step(self, local_actions):
-        """Steps the local shard; returns (gathered rows [total_envs, obs+3], Ready).  The
-        rows of this step may be read after ready.wait(), until the step after next."""
+    def _swap_in(self):
+        """rows[cur] becomes the kernel's learner output, once the gather two launches ago
+        (which reads the same buffer) is done."""
         b = self.local.batch
         cur = self._cur
         w = self._work[cur]
-        if w is not None:                 # the gather two steps ago still reads rows[cur]
+        if w is not None:
             w.wait()
             self._work[cur] = None
         if b.learner is not self._rows[cur]:
             b.set_learner(self._rows[cur])
+        return cur
+
+    def reset(self, **kw):
+        """Resets the local shard and gathers every rank's reset rows (obs, reward 0,
+        terminated 0, truncated 0): returns (gathered rows [total_envs, obs+3], Ready) like
+        step(), so a learner on any rank sees the node's first observations.  The local
+        shard's Dict observation stays available as self.local_obs."""
+        cur = self._swap_in()
+        # (a reset(seed=) that rebuilds the batch keeps the learner buffer: vector.py)
+        self.local_obs, self.local_info = self.local.reset(**kw)
+        assert self.local.batch.learner is self._rows[cur]
+        return self._gather(cur)
+
+    def step(self, local_actions):
+        """Steps the local shard; returns (gathered rows [total_envs, obs+3], Ready).  The
+        rows of this step may be read after ready.wait(), until the step after next."""
+        cur = self._swap_in()
         self.local.step_tensors(local_actions)
+        return self._gather(cur)
+
+    def _gather(self, cur):
         if self.world == 1:
             self._gathered[cur][: self.n_local].copy_(self._rows[cur])
             ready = Ready()

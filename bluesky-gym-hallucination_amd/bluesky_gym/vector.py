@@ -55,11 +55,15 @@ class BlueSkyVectorEnv(_gym.VectorEnv):
             {k: _gym.spaces.Box(-np.inf, np.inf, shape=(self.num_envs, n), dtype=np.float64)
              for k, n in self.layout.sizes.items()})
         self.action_space = _gym.spaces.Box(-1, 1, shape=(self.num_envs, act), dtype=np.float64)
+        if spawn == "host" and autoreset == nat.AUTORESET_SAME_STEP:
+            # SAME_STEP resets inside the step kernel, before the host knows which envs end;
+            # host rows (reference-order RNG per env) can only be supplied for NEXT_STEP
+            raise ValueError("spawn='host' needs NEXT_STEP autoreset (SAME_STEP respawns on the "
+                             "device inside the step); use spawn='device' with SAME_STEP")
         self._seed = seed
         self._host_rngs = None
         self._wind = None
-        self.batch = DeviceBatch(kind_cfg, self.num_envs, autoreset=autoreset, compute_cd=compute_cd,
-                                 seed=seed, device=device, learner=learner, env_offset=env_offset)
+        self.batch = self._new_batch(seed)
 
     def set_wind(self, table, augment_obs=False):
         """Wind field for every env of the batch (bluesky_gym.wrappers.wind)."""
@@ -71,6 +75,22 @@ class BlueSkyVectorEnv(_gym.VectorEnv):
         self.observation_space = _gym.spaces.Dict(
             {key: _gym.spaces.Box(-np.inf, np.inf, shape=(self.num_envs, n), dtype=np.float64)
              for key, n in self.layout.sizes.items()})
+
+    def _new_batch(self, seed):
+        return DeviceBatch(self.kind_cfg, self.num_envs, autoreset=self.autoreset,
+                           compute_cd=self.compute_cd, seed=seed, device=self.device,
+                           learner=self.learner, env_offset=self.env_offset)
+
+    def _check_overflow(self):
+        """SectorCR: an episode that drew more aircraft than the capacity raises, as the
+        host-spawn path does (bsg.h BSG_FLAG_SPAWN_OVERFLOW; sector_cr_env.py:95-100)."""
+        if self.kind_cfg.kind != nat.ENV_SECTOR_CR:
+            return
+        over = (self.batch.envs["flags"] & nat.FLAG_SPAWN_OVERFLOW) != 0
+        if bool(over.any()):
+            e = int(torch.nonzero(over)[0, 0])
+            raise RuntimeError(f"SectorCR env {e}: the episode drew more aircraft than "
+                               f"num_ac={self.kind_cfg.num_ac}; construct with a larger num_ac")
 
     # ---------------------------------------------------------------- spawns
     def _host_spawn(self, mask=None):
@@ -105,17 +125,22 @@ class BlueSkyVectorEnv(_gym.VectorEnv):
 
     # ---------------------------------------------------------------- API
     def reset(self, *, seed=None, options=None):
-        if seed is not None and seed != self._seed:
+        """Gymnasium reset.  reset(seed=s) always restarts from s -- fresh host RNG streams
+        and episode counters (the Philox key) -- so two resets with the same seed give the
+        same episodes; reset() without a seed continues the streams."""
+        if seed is not None:
             self._seed = seed
             self._host_rngs = None
+            learner = self.batch.learner
             self.batch.close()
-            self.batch = DeviceBatch(self.kind_cfg, self.num_envs, autoreset=self.autoreset,
-                                     compute_cd=self.compute_cd, seed=seed, device=self.device,
-                                     learner=self.learner, env_offset=self.env_offset)
+            self.batch = self._new_batch(seed)
+            if self.learner and learner is not None:
+                self.batch.set_learner(learner)
             if self._wind is not None:
                 self.batch.set_wind(*self._wind)
         sp = self._host_spawn() if self.spawn_mode == "host" else None
         self.batch.reset(spawn=sp)
+        self._check_overflow()
         return self.layout.split(self.batch.obs.cpu().numpy()), self._infos(done=None)
 
     def step_tensors(self, actions):
@@ -125,7 +150,9 @@ class BlueSkyVectorEnv(_gym.VectorEnv):
         if self.spawn_mode == "host":
             pend = self.batch.envs["flags"].cpu().numpy() & 1
             sp = self._host_spawn(pend.astype(bool)) if pend.any() else None
-        return self.batch.step(actions, spawn=sp)
+        out = self.batch.step(actions, spawn=sp)
+        self._check_overflow()
+        return out
 
     def step(self, actions):
         a = actions if isinstance(actions, torch.Tensor) else torch.as_tensor(np.asarray(actions, np.float64))

@@ -31,6 +31,8 @@ struct bsg_ctx {
   unsigned lds_pad = 0;
   std::vector<hipEvent_t> ev_pool;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> pending;
+  double folded_ms = 0.0;          // timed launches already folded out of `pending`
+  int folded_n = 0;
 };
 
 namespace {
@@ -96,6 +98,44 @@ bsg::KParams make_params(const bsg_ctx* c, int mode) {
   return p;
 }
 
+// A caller that enables timing and never polls bsg_step_timing must not grow `pending`
+// (and live hipEvents) without bound: past kMaxPending pairs, completed pairs are folded
+// into running totals and their events recycled; if none has completed, the oldest is
+// waited for.
+constexpr size_t kMaxPending = 1024;
+
+int fold_pair(bsg_ctx* c, size_t i) {
+  auto pr = c->pending[i];
+  hipError_t e = hipEventSynchronize(pr.second);
+  if (e != hipSuccess) return hip_fail(e, "hipEventSynchronize");
+  float ms = 0.f;
+  e = hipEventElapsedTime(&ms, pr.first, pr.second);
+  if (e != hipSuccess) return hip_fail(e, "hipEventElapsedTime");
+  c->folded_ms += ms;
+  ++c->folded_n;
+  c->ev_pool.push_back(pr.first);
+  c->ev_pool.push_back(pr.second);
+  return BSG_OK;
+}
+
+int trim_pending(bsg_ctx* c) {
+  if (c->pending.size() < kMaxPending) return BSG_OK;
+  size_t keep = 0;
+  for (size_t i = 0; i < c->pending.size(); ++i) {
+    if (hipEventQuery(c->pending[i].second) == hipSuccess) {
+      if (int r = fold_pair(c, i)) return r;
+    } else {
+      c->pending[keep++] = c->pending[i];
+    }
+  }
+  c->pending.resize(keep);
+  if (keep >= kMaxPending) {            // nothing finished yet: wait for the oldest
+    if (int r = fold_pair(c, 0)) return r;
+    c->pending.erase(c->pending.begin());
+  }
+  return BSG_OK;
+}
+
 int launch(bsg_ctx* c, const bsg::KParams& p, void* stream) {
   hipError_t e = hipSetDevice(c->cfg.device);
   if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
@@ -103,15 +143,31 @@ int launch(bsg_ctx* c, const bsg::KParams& p, void* stream) {
   hipEvent_t t0 = nullptr, t1 = nullptr;
   const bool timed = c->timing > 0 && (c->launch_count++ % c->timing) == 0;
   if (timed) {
+    if (int r = trim_pending(c)) return r;
     t0 = take_event(c);
     t1 = take_event(c);
-    if (!t0 || !t1) return fail(BSG_E_HIP, "hipEventCreate failed%s%lld");
-    if ((e = hipEventRecord(t0, st)) != hipSuccess) return hip_fail(e, "hipEventRecord");
+    if (!t0 || !t1) {
+      if (t0) c->ev_pool.push_back(t0);
+      if (t1) c->ev_pool.push_back(t1);
+      return fail(BSG_E_HIP, "hipEventCreate failed%s%lld");
+    }
+    if ((e = hipEventRecord(t0, st)) != hipSuccess) {
+      c->ev_pool.push_back(t0);
+      c->ev_pool.push_back(t1);
+      return hip_fail(e, "hipEventRecord");
+    }
   }
   e = bsg::launch_step(p, st);
-  if (e != hipSuccess) return hip_fail(e, "kernel launch");
+  if (e != hipSuccess) {
+    if (timed) { c->ev_pool.push_back(t0); c->ev_pool.push_back(t1); }
+    return hip_fail(e, "kernel launch");
+  }
   if (timed) {
-    if ((e = hipEventRecord(t1, st)) != hipSuccess) return hip_fail(e, "hipEventRecord");
+    if ((e = hipEventRecord(t1, st)) != hipSuccess) {
+      c->ev_pool.push_back(t0);
+      c->ev_pool.push_back(t1);
+      return hip_fail(e, "hipEventRecord");
+    }
     c->pending.emplace_back(t0, t1);
   }
   return BSG_OK;
@@ -334,8 +390,10 @@ int32_t bsg_set_timing(bsg_ctx* c, int32_t enable) {
 
 int32_t bsg_step_timing(bsg_ctx* c, double* total_ms, int32_t* launches) {
   if (!c || !total_ms || !launches) return fail(BSG_E_INVALID_ARG, "bsg_step_timing: null argument%s%lld");
-  double tot = 0.0;
-  int n = 0;
+  double tot = c->folded_ms;
+  int n = c->folded_n;
+  c->folded_ms = 0.0;
+  c->folded_n = 0;
   for (auto& pr : c->pending) {
     hipError_t e = hipEventSynchronize(pr.second);
     if (e != hipSuccess) return hip_fail(e, "hipEventSynchronize");

@@ -182,6 +182,7 @@ struct SectorPlan {                      // per env (LDS), device-drawn resets o
   double draw[64];                       // waypoint perimeter distance by aircraft draw
   double perim, minx, maxx, miny, maxy;
   int nv, nac;
+  int over;                              // the drawn count exceeded the capacity N
 };
 
 __device__ __forceinline__ void nm_to_latlong_sector(double x, double y, double* lat, double* lon) {
@@ -210,6 +211,7 @@ __device__ __forceinline__ void sector_plan_polygon(SectorPlan& P, double* geo, 
     dens = 0.003 + (0.007 - 0.003) * u01_53(r.x, r.y);
   }
   int nac = (int)npmax(ceil(dens * area), 5.0);
+  P.over = nac > N;                      // flagged (BSG_FLAG_SPAWN_OVERFLOW), not silent
   if (nac > N) nac = N;
   double perim = 0.0, minx = P.px[0], maxx = P.px[0], miny = P.py[0], maxy = P.py[0];
   for (int i = 0; i < nv; ++i) {

@@ -73,7 +73,7 @@ __host__ __device__ __forceinline__ double pow_2o7(double y) {
 // sequence the compiler emits for '/'.  Valid for normal, non-overflowing quotients
 // (every use here: physical quantities); a zero numerator keeps its sign and an infinite
 // one stays infinite, as with '/'.
-// Verified against '/' on 10^8 random and near-halfway numerators per divisor used
+// Verified against '/' on 2*10^7 random and near-halfway numerators per divisor used
 // (tools/fastpow/ulp_check.cpp).
 __host__ __device__ __forceinline__ double div_r(double x, double y, double ry) {
   const double q = x * ry;

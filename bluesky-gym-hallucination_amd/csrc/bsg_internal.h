@@ -43,4 +43,14 @@ struct KParams {
 
 hipError_t launch_step(const KParams& p, hipStream_t stream);
 
+// per-kind launchers, one translation unit each (bsg_kernels.hip -DBSG_KIND_TU=<kind>;
+// the suffix is the BSG_ENV_* value)
+hipError_t launch_kind_0(const KParams& p, hipStream_t stream);
+hipError_t launch_kind_1(const KParams& p, hipStream_t stream);
+hipError_t launch_kind_2(const KParams& p, hipStream_t stream);
+hipError_t launch_kind_3(const KParams& p, hipStream_t stream);
+hipError_t launch_kind_4(const KParams& p, hipStream_t stream);
+hipError_t launch_kind_5(const KParams& p, hipStream_t stream);
+hipError_t launch_kind_6(const KParams& p, hipStream_t stream);
+
 }  // namespace bsg

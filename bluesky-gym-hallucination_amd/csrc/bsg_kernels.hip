@@ -928,6 +928,7 @@ struct EnvScalars {
   double aux[4];                    // env_aux (StaticObstacle: last obs waypoint distance km,
                                     // last drift deg, drift samples, crashed)
   int nac;                          // aircraft of this episode (SectorCR; else N)
+  int over;                         // SectorCR reset drew more than N aircraft
 };
 
 __device__ __forceinline__ void load_env(const Buffers& b, int e, EnvScalars& v) {
@@ -1305,6 +1306,7 @@ __device__ __forceinline__ void sector_reset_plan(const KParams& p, int e, int j
     if (rs) {
       const double* row = p.spawn + (size_t)e * p.spawn_width;
       const int nac = (int)row[0] < N ? (int)row[0] : N;
+      ev.over = (int)row[0] > N;
       const int nv = (int)row[1];
       if (j == 0) {
         geo[0] = (double)nac;
@@ -1330,6 +1332,7 @@ __device__ __forceinline__ void sector_reset_plan(const KParams& p, int e, int j
   if (rs && j == 0) sector_plan_polygon(P, geo, env, ev.episode, p.seed, N, p.cfg.kind_option);
   __syncthreads();
   const int nac = rs ? P.nac : 0;
+  if (rs) ev.over = P.over;
   double dj = 0.0;
   if (rs && j < nac) {
     U4 r = philox4x32_10(env, ev.episode, (uint32_t)(128 + j), TAG_SECT, p.seed);
@@ -1546,16 +1549,14 @@ __global__ __launch_bounds__(64) void step_kernel(KParams p) {
     AC s = (!resetting || keep) ? s_in : AC{};
     if (ok) {
       if (resetting) spawn<KIND>(p, e, j, ev.episode, s, aux, keep);
-#if defined(BSG_EXP_SKIP_OWN) && BSG_EXP_SKIP_OWN
-      // experiment build only (tools/ablate.py): the ownship does not move
-      if (stepping && on && j != 0) propagate<KIND, WIND>(p, e, j, a, s, ev, sub_reward, sub_done, act, mc, oat);
-#else
       if (stepping && on) propagate<KIND, WIND>(p, e, j, a, s, ev, sub_reward, sub_done, act, mc, oat);
-#endif
       if (active) store_ac_changed<WIND>(b, a, s, s_in);
       if (resetting && b.memo_cache) memo_invalidate(b.memo_cache, a, (size_t)p.E * N);
     }
-    if (resetting && j == 0) reset_scalars<KIND>(ev, aux);
+    if (resetting && j == 0) {
+      reset_scalars<KIND>(ev, aux);
+      if (ev.over) ev.flags |= BSG_FLAG_SPAWN_OVERFLOW;
+    }
     stage(L, lane, s);
   }
   __syncthreads();
@@ -1610,11 +1611,7 @@ __global__ __launch_bounds__(64) void step_kernel(KParams p) {
     // LDS word (L.lm, re-zeroed before phase 2).
     __syncthreads();
     uint64_t cand = 0;
-#if defined(BSG_EXP_CD_NOTEST) && BSG_EXP_CD_NOTEST
-    if (false) {                                     // experiment: no phase-1 tests at all
-#else
     if (on) {
-#endif
       const int nac = ev.nac;
       const float4 pi = L.fpk[lane];
       const float flati = pi.x, floni = pi.y, fui = pi.z, fvi = pi.w;
@@ -1633,11 +1630,7 @@ __global__ __launch_bounds__(64) void step_kernel(KParams p) {
         dl = dl > 180.0f ? 360.0f - dl : dl;
         const float x = fmaxf(fali, fabsf(pk.x));
         const float du = pk.z - fui, dv = pk.w - fvi;
-#if defined(BSG_EXP_CD_NOP1) && BSG_EXP_CD_NOP1
-        if (du > -1e30f) mine |= 1ull << (sft - 1);      // experiment: every pair a candidate
-#else
         if (cd_candidate_f(dlat, dl, x, du * du + dv * dv)) mine |= 1ull << (sft - 1);
-#endif
       }
       for (uint64_t mm = mine; mm; mm &= mm - 1) {
         int k = j + 1 + __builtin_ctzll(mm);
@@ -1667,11 +1660,7 @@ __global__ __launch_bounds__(64) void step_kernel(KParams p) {
     BSG_STAMP(4, stamp_clock() | ((unsigned long long)total << 48));
 #endif
     // phase 2: dense exact StateBased over the surviving pairs
-#if defined(BSG_EXP_CD_NOP2) && BSG_EXP_CD_NOP2
-    for (int t = lane; t < 0; t += 64) {            // experiment: phase 2 skipped
-#else
     for (int t = lane; t < total; t += 64) {
-#endif
       const int pr = cd_list[t];
       const int li = pr >> 6, lk = pr & 63;
       const CdOut r = cd_pair(L, li, lk);
@@ -1856,7 +1845,10 @@ __global__ __launch_bounds__(64) void step_kernel(KParams p) {
         store_ac<WIND>(b, a, s);
         if (b.memo_cache) memo_invalidate(b.memo_cache, a, (size_t)p.E * N);
       }
-      if (same_step_reset && j == 0) reset_scalars<KIND>(ev, aux);
+      if (same_step_reset && j == 0) {
+        reset_scalars<KIND>(ev, aux);
+        if (ev.over) ev.flags |= BSG_FLAG_SPAWN_OVERFLOW;
+      }
       if (same_step_reset) stage(L, lane, s);
     }
     __syncthreads();
@@ -1910,9 +1902,6 @@ template <int KIND, bool WIND>
 static hipError_t launch_kind_w(const KParams& p, hipStream_t st) {
   int gs = 1;
   while (gs < p.N) gs <<= 1;
-#if defined(BSG_EXP_GS64) && BSG_EXP_GS64
-  gs = 64;   // experiment: one env per wave (upper lanes idle)
-#endif
   const int epb = 64 / gs;
   const int grid = (p.E + epb - 1) / epb;
 #define BSG_CASE(G) \
@@ -1937,23 +1926,15 @@ static hipError_t launch_kind(const KParams& p, hipStream_t st) {
   return p.wind.np > 0 ? launch_kind_w<KIND, true>(p, st) : launch_kind_w<KIND, false>(p, st);
 }
 
-hipError_t launch_step(const KParams& p, hipStream_t st) {
-#if defined(BSG_ONLY_MERGE) && BSG_ONLY_MERGE
-  // experiment builds (tools/flag_sweep.sh, tools/variants.sh): Merge only, for fast sweeps
-  if (p.cfg.env_kind == BSG_ENV_MERGE) return launch_kind<BSG_ENV_MERGE>(p, st);
-  return hipErrorInvalidValue;
-#else
-  switch (p.cfg.env_kind) {
-    case BSG_ENV_MERGE: return launch_kind<BSG_ENV_MERGE>(p, st);
-    case BSG_ENV_VERTICAL_CR: return launch_kind<BSG_ENV_VERTICAL_CR>(p, st);
-    case BSG_ENV_DESCENT: return launch_kind<BSG_ENV_DESCENT>(p, st);
-    case BSG_ENV_HORIZONTAL_CR: return launch_kind<BSG_ENV_HORIZONTAL_CR>(p, st);
-    case BSG_ENV_STATIC_OBSTACLE: return launch_kind<BSG_ENV_STATIC_OBSTACLE>(p, st);
-    case BSG_ENV_SECTOR_CR: return launch_kind<BSG_ENV_SECTOR_CR>(p, st);
-    case BSG_ENV_PLAN_WAYPOINT: return launch_kind<BSG_ENV_PLAN_WAYPOINT>(p, st);
-    default: return hipErrorInvalidValue;
-  }
-#endif
+// One translation unit per env kind (the Makefile compiles this file once per kind with
+// -DBSG_KIND_TU=<kind>, so the seven kinds build in parallel); launch_step dispatches
+// (bsg_dispatch.cpp).
+#ifdef BSG_KIND_TU
+#define BSG_CAT2(a, b) a##b
+#define BSG_CAT(a, b) BSG_CAT2(a, b)
+hipError_t BSG_CAT(launch_kind_, BSG_KIND_TU)(const KParams& p, hipStream_t st) {
+  return launch_kind<BSG_KIND_TU>(p, st);
 }
+#endif
 
 }  // namespace bsg

@@ -46,11 +46,15 @@ enum { BSG_ENV_MERGE = 0, BSG_ENV_VERTICAL_CR = 1, BSG_ENV_DESCENT = 2,
 
 /* bsg_buffers.flags bits */
 enum { BSG_FLAG_RESET_PENDING = 1,   /* NEXT_STEP autoreset due on the next step */
-       BSG_FLAG_AC_PRESENT = 2 };    /* Descent / PlanWaypoint: KL001 exists.  Their reset()
+       BSG_FLAG_AC_PRESENT = 2,      /* Descent / PlanWaypoint: KL001 exists.  Their reset()
                                         does not clear the traffic, so a reset after a
                                         truncation keeps the aircraft (cre refused,
                                         descent_env.py:173, plan_waypoint_env.py:164); the
                                         terminal step deletes it (:201-204, :189-193) */
+       BSG_FLAG_SPAWN_OVERFLOW = 4 };/* SectorCR: this episode drew more aircraft than the
+                                        capacity N (sector_cr_env.py:95-100 has no cap); the
+                                        device spawned N of them.  The Python layer raises
+                                        on it, as the host-spawn path does */
 
 /* Vector-env autoreset conventions:
  *   NEXT_STEP: Gymnasium >= 1.0 VectorEnv default -- the step AFTER a done step resets
@@ -130,7 +134,9 @@ typedef struct bsg_buffers {
   uint64_t *conf_mask;       /* [E, N] StateBased swconfl, bit j of row i (compute_cd) */
   uint64_t *los_mask;        /* [E, N] StateBased swlos, bit j of row i (compute_cd) */
   float *tcpamax;            /* [E, N] StateBased tcpamax (compute_cd) */
-  float *min_sep;            /* [E] min pairwise horizontal distance, m (compute_cd) */
+  float *min_sep;            /* [E] min StateBased dist (m) over the pairs inside the CD
+                                horizon RPZ + 300 s * vrel; +inf if no pair is inside it,
+                                so well-separated envs read +inf (compute_cd) */
   double *ep_info;           /* [E, 4] written when an episode ends: total_reward,
                                 total_intrusions, faf_reach | final_altitude,
                                 average_drift (Merge) -- the info dict at done

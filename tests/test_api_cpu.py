@@ -122,3 +122,12 @@ def test_plan_host_spawn_consumes_np_random_like_reference(name):
     np.random.seed(int(g["seed"]))
     for ep in range(len(g["length"])):
         assert np.array_equal(spawn.plan_spawn(), g["spawn"][ep])
+
+
+def test_host_spawn_with_same_step_is_rejected():
+    """SAME_STEP respawns inside the step kernel, before the host knows which envs end, so
+    reference-order host spawn rows cannot be supplied: refused up front."""
+    from bluesky_gym import _native as nat
+    from bluesky_gym.vector import MergeVectorEnv
+    with pytest.raises(ValueError, match="NEXT_STEP"):
+        MergeVectorEnv(num_envs=4, spawn="host", autoreset=nat.AUTORESET_SAME_STEP)

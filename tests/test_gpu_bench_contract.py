@@ -24,10 +24,16 @@ def test_bench_json_line():
         assert r["metric"] == json.load(f)["metric"]
     assert r["value"] > 0 and r["unit"] == "env_steps/s" and r["n_gpus"] == 1
     assert r["steps"] == 5 and r["warmup"] == 2 and r["higher_is_better"] is True
-    assert r["scaling"] == "weak" and r["vs_baseline"] is None and r["dtype"] == "f64"
+    assert r["scaling"] == "strong" and r["vs_baseline"] is None and r["dtype"] == "f64"
+    assert r["config"]["envs_total"] == 4096
     rf = r["roofline"]
-    assert rf["bound"] == "hbm" and rf["unit"] == "GB/s" and rf["peak"] == 8000.0
+    assert rf["bound"] == "valu-latency" and rf["unit"] == "GB/s" and rf["peak"] == 8000.0
     assert rf["achieved"] > 0 and abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-12
+    # the kernel time comes from events bracketing the timed region: never above the wall
+    # time per step, and the post-region sampled event pairs hold >= 10 launches
+    assert 0 < rf["kernel_avg_ms"] <= r["ms_per_step"] * 1.001
+    assert "launch, 10 samples" in rf["sampled_launch_timing"]
     cb = r["cpu_baseline"]
     assert cb["value"] > 0 and cb["cores"] >= 1 and cb["kind"] in ("port", "reference")
+    assert cb["per_env"]["value"] > 0
     assert "workload" in r["config"]

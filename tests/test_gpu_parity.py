@@ -245,10 +245,54 @@ def test_descent_batch_autoreset_parity(bg):
         _compare_step(b, r, 1, "descent", t)
 
 
+def _subset_compare(b, r, ids, N, kind, t, errs):
+    """Every output of a strided subset of a full-size device batch vs the subset oracle
+    (same global env ids -> same Philox spawns): obs and reward within tolerance,
+    terminated / truncated / top-K / intrusion / conflict / LoS bit-exact, tcpamax and
+    min_sep within tolerance.  errs accumulates the per-obs-key max |gpu - ref|."""
+    o = b.obs.cpu().numpy()[ids]
+    close(o, r["obs"], f"obs t={t}")
+    for key, (a, z) in errs["slices"].items():
+        errs["max"][key] = max(errs["max"].get(key, 0.0),
+                               float(np.abs(o[:, a:z].astype(np.float64) - r["obs"][:, a:z]).max()))
+    rw = b.reward.cpu().numpy()[ids].astype(np.float64)
+    close(rw, r["reward"], f"reward t={t}")
+    errs["max"]["(reward)"] = max(errs["max"].get("(reward)", 0.0), float(np.abs(rw - r["reward"]).max()))
+    assert np.array_equal(b.terminated.cpu().numpy()[ids].astype(bool), r["terminated"]), t
+    assert np.array_equal(b.truncated.cpu().numpy()[ids].astype(bool), r["truncated"]), t
+    if kind == "descent":
+        return
+    live = ~r["was_reset"]
+    gi = b.intr_mask.cpu().numpy()[ids].astype(np.uint64)
+    assert np.array_equal(gi[live], r["intr_mask"][live]), t
+    assert np.array_equal(b.conf_mask.cpu().numpy()[ids].astype(np.uint64), r["conf_mask"]), t
+    assert np.array_equal(b.los_mask.cpu().numpy()[ids].astype(np.uint64), r["los_mask"]), t
+    close(b.tcpamax.cpu().numpy()[ids], r["tcpamax"], f"tcpamax t={t}", atol=TCPA_ATOL)
+    ms_g = b.min_sep.cpu().numpy()[ids].astype(np.float64)
+    assert np.array_equal(np.isinf(ms_g), np.isinf(r["min_sep"])), t
+    fin = np.isfinite(r["min_sep"])
+    close(ms_g[fin], r["min_sep"][fin], f"min_sep t={t}")
+    if kind == "merge":
+        assert np.array_equal(b.topk.cpu().numpy()[ids][live], r["topk"][live]), t
+
+
+def _obs_slices(b):
+    from bluesky_gym.obs_layout import ObsLayout
+    lay = ObsLayout(b.cfg.kind, b.cfg.num_ac, b.cfg.num_ac_state)
+    return {k: (sl.start, sl.stop) for k, sl in lay.slices.items()}
+
+
+def _report(errs, what):
+    print(f"\n{what}: per-key max |gpu - oracle| over the subset and all compared steps")
+    for k, v in sorted(errs["max"].items()):
+        print(f"  {k:24s} {v:.3e}")
+
+
 def test_merge_full_size_subset_parity(bg):
     """BASELINE workload (4096 envs x 32 aircraft): run the full batch on the GPU and
-    check a strided subset of 64 envs against the oracle (envs are independent, so the
-    subset oracle with the same global env ids sees identical spawns)."""
+    check a strided subset of 64 envs against the oracle on every output, every step
+    (envs are independent, so the subset oracle with the same global env ids sees
+    identical spawns)."""
     core, config, nat = bg
     E, N, T = 4096, 32, 60
     b = core.DeviceBatch(config.merge_config(num_ac=N), E, compute_cd=True, seed=42)
@@ -256,14 +300,14 @@ def test_merge_full_size_subset_parity(bg):
     o = ob.MergeOracle(len(ids), num_ac=N, seed=42, compute_cd=True)
     o.env_ids = ids
     close(b.reset().cpu().numpy()[ids], o.reset()["obs"], "reset obs")
+    errs = {"slices": _obs_slices(b), "max": {}}
     rng = np.random.default_rng(1)
     for t in range(T):
         a = rng.uniform(-1, 1, (E, 2))
         b.step(torch.from_numpy(a))
         r = o.step(a[ids])
-        close(b.obs.cpu().numpy()[ids], r["obs"], f"obs t={t}")
-        assert np.array_equal(b.terminated.cpu().numpy()[ids].astype(bool), r["terminated"])
-        assert np.array_equal(b.conf_mask.cpu().numpy()[ids].astype(np.uint64), r["conf_mask"])
+        _subset_compare(b, r, ids, N, "merge", t, errs)
+    _report(errs, "merge 4096x32")
     # size-independent properties over the whole batch
     obs = b.obs.cpu().numpy()
     assert np.isfinite(obs).all()
@@ -277,6 +321,35 @@ def test_merge_full_size_subset_parity(bg):
     # near-threshold pair, so only require near-symmetry
     bm = bits(cm, N)
     assert (bm != bm.transpose(0, 2, 1)).sum() <= max(4, bm.sum() // 1000)
+
+
+def test_descent_full_size_subset_parity(bg):
+    """BASELINE configs[4]'s env batch: DescentEnv-v0 x 4096 envs on one GPU (the
+    8-GPU run shards the same envs), NEXT_STEP autoreset over 320 steps (every env
+    terminates or truncates at least once), a strided 128-env subset vs DescentOracle
+    every step, plus whole-batch properties."""
+    core, config, nat = bg
+    E, T = 4096, 320
+    b = core.DeviceBatch(config.descent_config(), E, seed=8)
+    ids = np.arange(0, E, 32)
+    o = ob.DescentOracle(len(ids), seed=8)
+    o.env_ids = ids
+    close(b.reset().cpu().numpy()[ids], o.reset()["obs"], "reset obs")
+    errs = {"slices": _obs_slices(b), "max": {}}
+    rng = np.random.default_rng(21)
+    done = np.zeros(E, bool)
+    for t in range(T):
+        a = rng.uniform(-1, 1, (E, 1))
+        b.step(torch.from_numpy(a))
+        r = o.step(a[ids])
+        _subset_compare(b, r, ids, 1, "descent", t, errs)
+        done |= (b.terminated | b.truncated).cpu().numpy().astype(bool)
+    _report(errs, "descent 4096")
+    assert done.all()
+    assert np.isfinite(b.obs.cpu().numpy()).all()
+    for f, v in b.state.items():
+        if v.dtype == torch.float64:
+            assert torch.isfinite(v).all(), f
 
 
 @pytest.mark.parametrize("kind,E,N,T,stride", [
@@ -399,20 +472,18 @@ def test_merge_full_size_soak_300_steps(bg):
     o.env_ids = ids
     b.reset()
     o.reset()
+    errs = {"slices": _obs_slices(b), "max": {}}
     rng = np.random.default_rng(77)
     for t in range(T):
         a = rng.uniform(-1, 1, (E, 2))
         b.step(torch.from_numpy(a))
         r = o.step(a[ids])
         if t % 10 == 9:
-            close(b.obs.cpu().numpy()[ids], r["obs"], f"obs t={t}")
-            assert np.array_equal(b.terminated.cpu().numpy()[ids].astype(bool), r["terminated"]), t
-            assert np.array_equal(b.truncated.cpu().numpy()[ids].astype(bool), r["truncated"]), t
-            assert np.array_equal(b.conf_mask.cpu().numpy()[ids].astype(np.uint64), r["conf_mask"]), t
-            assert np.array_equal(b.los_mask.cpu().numpy()[ids].astype(np.uint64), r["los_mask"]), t
+            _subset_compare(b, r, ids, N, "merge", t, errs)
     for f, v in b.state.items():
         if v.dtype == torch.float64:
             assert torch.isfinite(v).all(), f
+    _report(errs, "merge 4096x32, 300-step soak")
     sc = b.envs["step_count"].cpu().numpy()
     assert sc.min() >= 0 and sc.max() <= 50
     tk = b.topk.cpu().numpy()

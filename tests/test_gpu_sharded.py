@@ -1,0 +1,133 @@
+"""The multi-GPU code path on the one-GPU box: ShardedVectorEnv with 2 ranks (gloo, both
+on cuda:0) against one un-sharded DeviceBatch of all the envs -- the gathered
+[E, obs+3] learner rows must be bit-identical every step, through reset and autoresets,
+with the asynchronous gather overlapped (Work handles, double-buffered rows, the
+pointer swap two steps later).  Replaces the reference's SubprocVecEnv
+(scripts/multi_processing_example.py:51-53).  Also: the Gymnasium reset-seeding
+contract, the SAME_STEP/host-spawn guard and the SectorCR capacity flag."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+E_LOCAL, T, SEED, MAXEP = 128, 64, 77, 20
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _actions(total):
+    g = torch.Generator().manual_seed(5)
+    return torch.rand((T, total, 2), dtype=torch.float64, generator=g) * 2 - 1
+
+
+def _shard_worker(rank, world, port, overlap, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                      HSA_ENABLE_IPC_MODE_LEGACY="0")
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from bluesky_gym.parallel import ShardedVectorEnv
+        from bluesky_gym.vector import MergeVectorEnv
+        total = world * E_LOCAL
+        env = ShardedVectorEnv(lambda **kw: MergeVectorEnv(num_ac=32, seed=SEED, compute_cd=True,
+                                                           max_episode_steps=MAXEP, **kw),
+                               total, overlap=overlap)
+        acts = _actions(total)
+        rows, ready = env.reset()
+        ready.wait()
+        torch.cuda.synchronize()
+        out = [rows.cpu().numpy().copy()]
+        for t in range(T):
+            a = acts[t, env.offset:env.offset + env.n_local].cuda()
+            rows, ready = env.step(a)
+            ready.wait()
+            torch.cuda.synchronize()
+            out.append(rows.cpu().numpy().copy())
+        env.close()
+        q.put((rank, np.stack(out) if rank == 0 else None, None))
+    except Exception as ex:  # pragma: no cover - reported to the parent
+        q.put((rank, None, repr(ex)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("overlap", [True, False])
+def test_sharded_rows_match_one_batch(overlap):
+    import torch.multiprocessing as mp
+    from bluesky_gym import config, core
+    world = 2
+    total = world * E_LOCAL
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_shard_worker, args=(r, world, port, overlap, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        r, arr, err = q.get(timeout=240)
+        assert err is None, f"rank {r}: {err}"
+        res[r] = arr
+    for p in procs:
+        p.join(timeout=60)
+    got = res[0]
+    # the same envs as one batch (global env ids 0..total-1 -> same Philox spawns)
+    b = core.DeviceBatch(config.merge_config(num_ac=32, max_episode_steps=MAXEP), total,
+                         compute_cd=True, seed=SEED, learner=True)
+    acts = _actions(total)
+    b.reset()
+    torch.cuda.synchronize()
+    want = [b.learner.cpu().numpy().copy()]
+    done = 0
+    for t in range(T):
+        b.step(acts[t].cuda())
+        want.append(b.learner.cpu().numpy().copy())
+        done += int((b.terminated | b.truncated).sum())
+    want = np.stack(want)
+    assert done >= total * (T // MAXEP), done        # autoresets happened in the window
+    assert got.shape == want.shape
+    assert np.array_equal(got.view(np.uint32), want.view(np.uint32)), \
+        np.argwhere(got.view(np.uint32) != want.view(np.uint32))[:5]
+
+
+def test_reset_with_seed_is_reproducible():
+    from bluesky_gym.vector import MergeVectorEnv
+    env = MergeVectorEnv(num_envs=64, num_ac=16, seed=0)
+    o1, _ = env.reset(seed=3)
+    a = np.random.default_rng(0).uniform(-1, 1, (64, 2))
+    s1 = env.step(a)[0]
+    o2, _ = env.reset(seed=3)
+    s2 = env.step(a)[0]
+    for k in o1:
+        assert np.array_equal(o1[k], o2[k]), k
+        assert np.array_equal(s1[k], s2[k]), k
+    o3, _ = env.reset()                       # no seed: the episode streams continue
+    assert any(not np.array_equal(o1[k], o3[k]) for k in o1)
+    env.close()
+
+
+def test_sector_capacity_overflow_raises():
+    """SectorCR draws 5..~40 aircraft per episode (sector_cr_env.py:95-100); with capacity
+    num_ac=8 most episodes overflow: the device flags them and the env raises, as the
+    host-spawn path does."""
+    from bluesky_gym.vector import SectorCRVectorEnv
+    env = SectorCRVectorEnv(num_envs=64, num_ac=8, seed=1)
+    with pytest.raises(RuntimeError, match="more aircraft"):
+        env.reset()
+    env.close()
+    ok = SectorCRVectorEnv(num_envs=64, num_ac=64, seed=1)   # capacity 64: P(overflow) ~ 0
+    ok.reset()
+    for _ in range(3):
+        ok.step(np.zeros((64, 2)))
+    ok.close()

@@ -15,7 +15,7 @@ V[licm]=""
 if [ "${1:-}" = build ]; then
   mkdir -p $OUT
   for k in "${!V[@]}"; do
-    /opt/rocm/bin/hipcc $BASE ${V[$k]} -shared -o $OUT/libbsg_$k.so $CS/bsg_kernels.hip -x hip $CS/bsg_abi.cpp &
+    ( o=$OUT/obj_$k && mkdir -p $o && /opt/rocm/bin/hipcc $BASE ${V[$k]} -DBSG_KIND_TU=0 -c -o $o/k.o $CS/bsg_kernels.hip && /opt/rocm/bin/hipcc $BASE ${V[$k]} -x hip -c -o $o/d.o $CS/bsg_dispatch.cpp && /opt/rocm/bin/hipcc $BASE ${V[$k]} -x hip -c -o $o/a.o $CS/bsg_abi.cpp && /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o $OUT/libbsg_$k.so $o/k.o $o/d.o $o/a.o ) &
   done
   wait
   ls -la $OUT

@@ -17,9 +17,9 @@ run() {  # name seconds cmd...
   return $rc
 }
 if [ -n "$KEXPR" ]; then
-  run gpu_tests 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "$KEXPR" || exit 1
+  run gpu_tests 900 python -u -m pytest tests -m gpu -x -v -rP --timeout 300 --timeout-method thread -k "$KEXPR" || exit 1
 else
-  run gpu_tests 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread || exit 1
+  run gpu_tests 900 python -u -m pytest tests -m gpu -x -v -rP --timeout 300 --timeout-method thread || exit 1
 fi
 [ "${SKIP_BENCH:-0}" = 1 ] && exit 0
 run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit 1

@@ -11,7 +11,7 @@ if [ "$mode" = build ]; then
   for kv in "$@"; do
     k=${kv%%=*}; d=${kv#*=}; x=""
     case "$d" in *:*) x=${d#*:}; d=${d%%:*};; esac
-    /opt/rocm/bin/hipcc $FLAGS $x -shared -o $OUT/libbsg_$k.so $d/bsg_kernels.hip -x hip $d/bsg_abi.cpp &
+    ( o=$OUT/obj_$k && mkdir -p $o && /opt/rocm/bin/hipcc $FLAGS $x -DBSG_KIND_TU=0 -c -o $o/k.o $d/bsg_kernels.hip && /opt/rocm/bin/hipcc $FLAGS $x -x hip -c -o $o/d.o $d/bsg_dispatch.cpp && /opt/rocm/bin/hipcc $FLAGS $x -x hip -c -o $o/a.o $d/bsg_abi.cpp && /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o $OUT/libbsg_$k.so $o/k.o $o/d.o $o/a.o ) &
   done
   wait
   ls -la $OUT
