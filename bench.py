@@ -139,7 +139,13 @@ def main():
     ap.add_argument("--no-gather", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--skip-cpu-baseline", action="store_true")
+    ap.add_argument("--workload", default="merge", choices=("merge", "descent-sac"),
+                    help="merge: the BASELINE metric (default); descent-sac: BASELINE configs[4], "
+                         "DescentEnv-v0 with the SAC learner in the loop")
+    ap.add_argument("--no-graph", action="store_true", help="descent-sac: eager, no HIP graph")
     args = ap.parse_args()
+    if args.workload == "descent-sac":
+        return bench_descent_sac(args)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -291,6 +297,112 @@ def main():
         }
         if cpu is not None:
             out["cpu_baseline"] = cpu
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def bench_descent_sac(args):
+    """BASELINE configs[4]: DescentEnv-v0 x 4096 envs (4096/N per rank) with the learner in
+    the loop (scripts/descent_env_sac.py:25-34: SB3 SAC, MultiInputPolicy, lr 3e-4, batch
+    256, buffer 1e6, train_freq 1, gradient_steps 1).  Three rates over the same envs:
+    env only (U(-1,1) actions from HBM), env + policy (the reference's saved SAC actor,
+    stochastic, forward on the kernel's fp32 obs rows), env + policy + one SAC update per
+    vector step (tools/sac_torch.py; HIP graph of the whole iteration on one GPU, eager with
+    an RCCL gradient all-reduce across ranks).  value = the last, whole job."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    sys.path.insert(0, os.path.join(REPO, "tools"))
+    import sac_torch
+    from bluesky_gym import _native as nat, config, core
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local % torch.cuda.device_count())
+        dist.init_process_group("nccl", device_id=torch.device("cuda", torch.cuda.current_device()))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    E = args.total_envs // world
+    cfg = config.descent_config()
+    b = core.DeviceBatch(cfg, E, autoreset=nat.AUTORESET_SAME_STEP, compute_cd=False,
+                         seed=1234, env_offset=rank * E)
+    b.reset()
+    W = dict(np.load(os.path.join(REPO, "tests", "golden", "sac_actors.npz")))
+    sac = sac_torch.SAC(b.obs_dim, b.act_dim, dev, group=dist.group.WORLD if world > 1 else None,
+                        seed=rank)
+    sac.actor.load_sb3(W, "descent")
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(17 + rank)
+    bank = torch.rand((16, E, 1), dtype=torch.float64, device=dev, generator=gen) * 2 - 1
+
+    def timed(fn, steps):
+        for k in range(args.warmup):
+            fn(k)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for k in range(steps):
+            fn(k)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([el], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t[0])
+        return el
+
+    el_env = timed(lambda k: b.step(bank[k % 16]), args.steps)
+    pol = sac_torch.RLLoop(b, sac, learn=False)
+    pol.obs.copy_(b.obs)
+    el_pol = timed(lambda k: pol.step(), args.steps)
+    rl = sac_torch.RLLoop(b, sac, learn=True)
+    rl.obs.copy_(b.obs)
+    for _ in range(8):                                # fill the buffer past one batch
+        rl.step()
+    graph = world == 1 and not args.no_graph
+    if graph:
+        rl.capture()
+    el_rl = timed((lambda k: rl.replay()) if graph else (lambda k: rl.step()), args.steps)
+    lq, la = sac.update()                             # one more update: finite losses
+    if rank == 0:
+        total = world * E * args.steps
+        out = {
+            "metric": "env steps/sec incl. SAC learner (whole node), DescentEnv-v0 4096 envs, "
+                      "1/2/4/8 GPUs (BASELINE configs[4])",
+            "value": total / el_rl,
+            "unit": "env_steps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": el_rl * 1e3 / args.steps,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f64 env / fp32 learner",
+            "data": "synthetic: device Philox spawns (descent_env.py distributions); actor "
+                    "initialised from the reference's saved SAC actor (weights only)",
+            "config": {"workload": f"DescentEnv-v0 {world * E} envs ({E} per GPU), 30 substeps x "
+                                   f"DT 1 s, SAME_STEP autoreset + final_obs, SAC batch 256 "
+                                   f"buffer 1e6 train_freq 1 gradient_steps 1",
+                       "envs_total": world * E, "envs_per_gpu": E,
+                       "parallelism": f"env-shard x{world}" + (" + RCCL gradient all_reduce "
+                                                               "(data-parallel SAC)" if world > 1 else ""),
+                       "hip_graph": graph},
+            "env_only": {"value": total / el_env, "ms_per_step": el_env * 1e3 / args.steps},
+            "env_policy": {"value": total / el_pol, "ms_per_step": el_pol * 1e3 / args.steps},
+            "env_policy_learner": {"value": total / el_rl, "ms_per_step": el_rl * 1e3 / args.steps,
+                                   "critic_loss": float(lq), "actor_loss": float(la)},
+        }
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()

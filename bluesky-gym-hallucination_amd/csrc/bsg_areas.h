@@ -88,7 +88,7 @@ __device__ __forceinline__ int build_ring(double* px, double* py, double R, UFN 
   for (int k = 0; k < nmax; ++k) {
     if (fixed_n >= 3 ? k >= fixed_n : (k >= 3 && area >= min_area)) break;
     const double alpha = TWO_PI * ufn(k);
-    ring_insert(px, py, n, R * cos(alpha), R * sin(alpha));
+    ring_insert(px, py, n, R * cos_t(alpha), R * sin_t(alpha));
     ++n;
     if (n >= 3) area = ring_area(px, py, n);
   }
@@ -100,8 +100,8 @@ __device__ __forceinline__ int build_ring(double* px, double* py, double R, UFN 
 __device__ __forceinline__ double get_hdg(double lat1d, double lon1d, double lat2d, double lon2d) {
   const double lat1 = lat1d * kD2R, lon1 = lon1d * kD2R, lat2 = lat2d * kD2R, lon2 = lon2d * kD2R;
   const double dlon = lon2 - lon1;
-  const double x = sin(dlon) * cos(lat2);
-  const double y = cos(lat1) * sin(lat2) - sin(lat1) * cos(lat2) * cos(dlon);
+  const double x = sin_t(dlon) * cos_t(lat2);
+  const double y = cos_t(lat1) * sin_t(lat2) - sin_t(lat1) * cos_t(lat2) * cos_t(dlon);
   return pymod(atan2(x, y) * kR2D + 360.0, 360.0);
 }
 
@@ -149,7 +149,7 @@ __device__ __forceinline__ void static_build(double* geo, const double* row, uin
       return u01_53(r.x, r.y);
     };
     const int n = build_ring(px, py, R, ufn, SO_VMAX, 50.0, fixed_n, &area);
-    const double ccos = 60.0 * cos(clat * kD2R);
+    const double ccos = 60.0 * cos_t(clat * kD2R);
     for (int k = 0; k < n; ++k) {              // nm_to_latlong(centre, point)
       px[k] = clat + (px[k] / 60.0);
       py[k] = clon + (py[k] / ccos);
@@ -187,7 +187,7 @@ struct SectorPlan {                      // per env (LDS), device-drawn resets o
 
 __device__ __forceinline__ void nm_to_latlong_sector(double x, double y, double* lat, double* lon) {
   *lat = SC_CLAT + (x / 60.0);
-  *lon = SC_CLON + (y / (60.0 * cos(SC_CLAT * kD2R)));
+  *lon = SC_CLON + (y / (60.0 * cos_t(SC_CLAT * kD2R)));
 }
 
 // lane 0 of a resetting env: polygon (sector_cr_env.py:140-158), aircraft count (:95-100),
@@ -206,7 +206,7 @@ __device__ __forceinline__ void sector_plan_polygon(SectorPlan& P, double* geo, 
   if (mode == 0) {                       // np.random.normal(0.005, 0.001) via Box-Muller
     const double u1 = 1.0 - u01_53(r.x, r.y);
     const double u2 = u01_53(r.z, r.w);
-    dens = 0.005 + 0.001 * (sqrt(-2.0 * log(u1)) * cos(TWO_PI * u2));
+    dens = 0.005 + 0.001 * (sqrt(-2.0 * log(u1)) * cos_t(TWO_PI * u2));
   } else {                               // np.random.uniform(0.003, 0.007)
     dens = 0.003 + (0.007 - 0.003) * u01_53(r.x, r.y);
   }

@@ -12,7 +12,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include "bsg_fastpow.h"
+#include "bsg_fastmath.h"
 
 namespace bsg {
 
@@ -143,7 +143,7 @@ __device__ __forceinline__ void kwikqdrdist(double lata, double lona, double lat
                                             double* qdr, double* dist) {
   double dlat = (latb - lata) * kD2R;
   double dlon = (pymod((lonb - lona) + 180.0, 360.0) - 180.0) * kD2R;
-  double cavelat = cos(((lata + latb) * kD2R) * 0.5);
+  double cavelat = cos_t(((lata + latb) * kD2R) * 0.5);
   double dangle = sqrt(dlat * dlat + dlon * dlon * cavelat * cavelat);
   *dist = divk(6371000.0 * dangle, NM);
   *qdr = pymod(atan2(dlon * cavelat, dlat) * kR2D, 360.0);
@@ -152,7 +152,7 @@ __device__ __forceinline__ void kwikqdrdist(double lata, double lona, double lat
 __device__ __forceinline__ double kwikdist(double lata, double lona, double latb, double lonb) {
   double dlat = (latb - lata) * kD2R;
   double dlon = (pymod((lonb - lona) + 180.0, 360.0) - 180.0) * kD2R;
-  double cavelat = cos(((lata + latb) * kD2R) * 0.5);
+  double cavelat = cos_t(((lata + latb) * kD2R) * 0.5);
   double dangle = sqrt(dlat * dlat + dlon * dlon * cavelat * cavelat);
   return divk(6371000.0 * dangle, NM);
 }
@@ -161,7 +161,7 @@ __device__ __forceinline__ double kwikdist(double lata, double lona, double latb
 __device__ __forceinline__ double kwikdist_mat(double lata, double lona, double latb, double lonb) {
   double dlat = (latb - lata) * kD2R;
   double dlon = (pymod((lonb - lona) + 180.0, 360.0) - 180.0) * kD2R;
-  double cavelat = cos(((latb + lata) * kD2R) * 0.5);
+  double cavelat = cos_t(((latb + lata) * kD2R) * 0.5);
   double dangle = sqrt(dlat * dlat + (dlon * dlon) * (cavelat * cavelat));
   return divk(6371000.0 * dangle, NM);
 }
@@ -171,7 +171,7 @@ __device__ __forceinline__ void kwikqdrdist_mat(double lata, double lona, double
                                                 double* qdr, double* dist) {
   double dlat = (latb - lata) * kD2R;
   double dlon = (pymod((lonb - lona) + 180.0, 360.0) - 180.0) * kD2R;
-  double cavelat = cos(((lata + latb) * kD2R) * 0.5);
+  double cavelat = cos_t(((lata + latb) * kD2R) * 0.5);
   double dangle = sqrt(dlat * dlat + (dlon * dlon) * (cavelat * cavelat));
   *dist = divk(6371000.0 * dangle, NM);
   *qdr = pymod(atan2(dlon * cavelat, dlat) * kR2D, 360.0);
@@ -179,10 +179,10 @@ __device__ __forceinline__ void kwikqdrdist_mat(double lata, double lona, double
 
 __device__ __forceinline__ void kwikpos(double latd1, double lond1, double qdr, double dist,
                                         double* lat2, double* lon2) {
-  double dx = dist * sin(qdr * kD2R);
-  double dy = dist * cos(qdr * kD2R);
+  double dx = dist * sin_t(qdr * kD2R);
+  double dy = dist * cos_t(qdr * kD2R);
   double dlat = divk(dy, 60.0);
-  double dlon = dx / npmax(0.01, 60.0 * cos(latd1 * kD2R));
+  double dlon = dx / npmax(0.01, 60.0 * cos_t(latd1 * kD2R));
   *lat2 = latd1 + dlat;
   *lon2 = pymod((lond1 + dlon) + 180.0, 360.0) - 180.0;
 }
@@ -192,7 +192,7 @@ __device__ __forceinline__ double rwgs84(double latd) {
   const double a = 6378137.0;
   const double b = 6356752.314245;
   double coslat, sinlat;
-  sincos(lat, &sinlat, &coslat);
+  sincos_t(lat, &sinlat, &coslat);
   double an = a * a * coslat;
   double bn = b * b * sinlat;
   double ad = a * coslat;
@@ -216,11 +216,11 @@ __device__ __forceinline__ void qdrdist(double latd1, double lond1, double latd2
   }
   double lat1 = latd1 * kD2R, lon1 = lond1 * kD2R;
   double lat2 = latd2 * kD2R, lon2 = lond2 * kD2R;
-  double coslat1 = cos(lat1), coslat2 = cos(lat2);
-  double sinlat1 = sin(lat1), sinlat2 = sin(lat2);
-  double cosdlon = cos(lon2 - lon1);
+  double coslat1 = cos_t(lat1), coslat2 = cos_t(lat2);
+  double sinlat1 = sin_t(lat1), sinlat2 = sin_t(lat2);
+  double cosdlon = cos_t(lon2 - lon1);
   double d = r * acos(coslat1 * coslat2 * cosdlon + sinlat1 * sinlat2);
-  *qdr = atan2(sin(lon2 - lon1) * coslat2, coslat1 * sinlat2 - sinlat1 * coslat2 * cosdlon) * kR2D;
+  *qdr = atan2(sin_t(lon2 - lon1) * coslat2, coslat1 * sinlat2 - sinlat1 * coslat2 * cosdlon) * kR2D;
   *distnm = d / NM;
 }
 
@@ -246,7 +246,7 @@ __device__ __forceinline__ bool qdr_x(double latd1, double lond1, double coslat1
                                       double latd2, double lond2, double coslat2, double sinlat2,
                                       double far_m, double* qdr, double* x) {
   double sdl, cdl;
-  sincos(lond2 * kD2R - lond1 * kD2R, &sdl, &cdl);
+  sincos_t(lond2 * kD2R - lond1 * kD2R, &sdl, &cdl);
   *qdr = atan2(sdl * coslat2, coslat1 * sinlat2 - sinlat1 * coslat2 * cdl) * kR2D;
   *x = coslat1 * coslat2 * cdl + sinlat1 * sinlat2;
   const double t = far_m * (1.0 / 6356752.314245);
@@ -311,8 +311,8 @@ __device__ __forceinline__ void get_point_at_distance(double lat1d, double lon1d
   double lat1 = lat1d * kD2R;
   double lon1 = lon1d * kD2R;
   double a = bearing * kD2R;
-  double lat2 = asin(sin(lat1) * cos(d / R) + cos(lat1) * sin(d / R) * cos(a));
-  double lon2 = lon1 + atan2(sin(a) * sin(d / R) * cos(lat1), cos(d / R) - sin(lat1) * sin(lat2));
+  double lat2 = asin(sin_t(lat1) * cos_t(d / R) + cos_t(lat1) * sin_t(d / R) * cos_t(a));
+  double lon2 = lon1 + atan2(sin_t(a) * sin_t(d / R) * cos_t(lat1), cos_t(d / R) - sin_t(lat1) * sin_t(lat2));
   *lat2d = lat2 * kR2D;
   *lon2d = lon2 * kR2D;
 }

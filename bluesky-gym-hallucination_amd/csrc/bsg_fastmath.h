@@ -1,0 +1,169 @@
+// bsg_fastmath.h -- the three fixed-exponent powers of the BlueSky atmosphere and the
+// CAS/TAS conversions, as short polynomials instead of the generic libm pow.
+//
+// bluesky.tools.aero (oracle/bluesky_subset.py: vatmos, vtas2cas, vcas2tas) evaluates
+//   pow(T/288.15, 4.256848030018761)   T/288.15 in [0.7519, 1] below 11 km .. above
+//   pow(z, 3.5)                        z = 1 + rho*v^2/(7p) = 1 + M^2/5, subsonic z < 1.3
+//   pow(y, 2.0/7.0)                    y = 1 + qdyn/p, in [1, 2] up to M ~ 1.1
+// The device libm's pow is 215 VALU instructions of one dependency chain (a dump of
+// ocml's pow at -O3); each conversion runs two of them in series, and the per-substep
+// speed chain of a climbing/descending aircraft runs seven.  On its argument range each
+// power here is one Horner chain of 12 or 20 FMAs on d = x - x0 (exact, Sterbenz),
+// with Chebyshev coefficients fitted to the exact binary64 exponent
+// (tools/fastmath/gen_coeffs.py, fit error <= 1.2e-18 relative); outside the range the
+// libm pow runs as before.  Accuracy against the correctly rounded power (glibc pow,
+// which NumPy calls): tools/fastmath/ulp_check.cpp on the host (the same FMA/mul
+// arithmetic) and tools/probe/fastmath_probe.hip on gfx950.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "bsg_fastmath_coeffs.h"
+
+namespace bsg {
+
+// Horner in plain FMAs down to the quadratic coefficient, then the last three steps in
+// double-double (TwoProd by FMA, Fast2Sum: |c_k| >= |(rest)*d| on the range, asserted by
+// the generator) with c2, c1, c0 carried as hi + lo.  Rounding c0..c2 and the last steps
+// in plain binary64 costs up to ~2.5 ulp where the result is small against c0 (pow_trop
+// near 0.75); this way the one rounding that remains is the final add (~0.5 ulp).
+template <int DEG>
+__host__ __device__ __forceinline__ double poly_dd(const double (&c)[DEG + 1],
+                                                   const double (&clo)[3], double d) {
+  double p = c[0];
+#pragma unroll
+  for (int k = 1; k <= DEG - 3; ++k) p = fma(p, d, c[k]);
+  double uh = p, ul = 0.0;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    // (uh + ul) <- c + (uh + ul) * d
+    const double ck = c[DEG - 2 + k];
+    const double qh = uh * d, ql = fma(uh, d, -qh);
+    const double sh = ck + qh;
+    const double sl = qh - (sh - ck);
+    ul = (sl + ql) + fma(ul, d, clo[k]);
+    uh = sh;
+  }
+  return uh + ul;
+}
+
+// pow(x, 4.256848030018761), the troposphere density ratio of vatmos
+__host__ __device__ __forceinline__ double pow_trop(double x) {
+  if (x >= kPowT_LO && x <= kPowT_HI) return poly_dd<kPowT_DEG>(kPowT_C, kPowT_CLO, x - kPowT_X0);
+  return pow(x, 4.256848030018761);
+}
+
+// pow(z, 3.5)
+__host__ __device__ __forceinline__ double pow_3p5(double z) {
+  if (z >= kPow35_LO && z <= kPow35_HI) return poly_dd<kPow35_DEG>(kPow35_C, kPow35_CLO, z - kPow35_X0);
+  return pow(z, 3.5);
+}
+
+// pow(y, 2.0 / 7.0)
+__host__ __device__ __forceinline__ double pow_2o7(double y) {
+  if (y >= kPow27_LO && y <= kPow27_HI) return poly_dd<kPow27_DEG>(kPow27_C, kPow27_CLO, y - kPow27_X0);
+  return pow(y, 2.0 / 7.0);
+}
+
+// ---- correctly rounded division by a known divisor -------------------------------------
+// x / y given ry = RN(1/y): q = RN(x*ry) is within 1 ulp of x/y, the remainder x - q*y is
+// exact by FMA, and q + rem*ry rounded once is RN(x/y) (Markstein's theorem; Muller et
+// al., Handbook of Floating-Point Arithmetic, "Markstein's iteration").  3 dependent
+// FMA-class instructions instead of the 10-instruction v_div_scale/rcp/fma/fmas/fixup
+// sequence the compiler emits for '/'.  Valid for normal, non-overflowing quotients
+// (every use here: physical quantities); a zero numerator keeps its sign and an infinite
+// one stays infinite, as with '/'.
+// Verified against '/' on 2*10^7 random and near-halfway numerators per divisor used
+// (tools/fastmath/ulp_check.cpp).
+__host__ __device__ __forceinline__ double div_r(double x, double y, double ry) {
+  const double q = x * ry;
+  const double rem = fma(-q, y, x);
+  const double r = fma(rem, ry, q);
+  return (x == 0.0 || !__builtin_isfinite(q)) ? q : r;
+}
+
+// divisor known at compile time: 1.0 / y folds to RN(1/y)
+__host__ __device__ __forceinline__ double divk(double x, double y) { return div_r(x, y, 1.0 / y); }
+
+// ---- sin / cos ------------------------------------------------------------------------
+// The device libm's sincos spends ~75 VALU on its small-argument path (3-part
+// double-double reduction, two polynomials whose 64-bit coefficients are each moved into
+// VGPRs, quadrant selection); cos alone ~70.  Every substep of every aircraft needs three
+// (heading, latitude, LNAV longitude gap) and the observation phase several more.  Here:
+//   k = rint(x * 2/pi);  t = x - k*P1 (exact: fma, both multiples of ulp(P1)/2, |t| < 1);
+//   (r, rr) = t - k*P2 - k*P3 in double-double (TwoProd of k*P2 by FMA, TwoSum);
+//   fdlibm-form kernels sin(r + rr) = r - ((z*(rr/2 - v*S') - rr) - v*S1), v = z*r, and
+//   cos(r + rr) = w + (((1 - w) - z/2) + (z*z*C(z) - r*rr)), w = 1 - z/2, with minimax
+//   coefficients fitted by tools/fastmath/gen_coeffs.py (fit error <= 1.3e-18);
+//   quadrant k mod 4 swaps / negates.
+// Domain: |x| < 2^30 (the quadrant is (int)k; the reduction keeps ~2^-100 relative
+// accuracy there) -- every angle of the env path is below 10^4 rad.  inf / NaN give NaN
+// through the arithmetic.  No libm fallback: an out-of-line call made the compiler assume
+// the call ABI for the whole kernel (190 VGPRs, 1 KB scratch per lane), and an inlined
+// one doubled the code size of every call site.
+// sin_t, cos_t and sincos_t share the reduction and kernels, so a value evaluated through
+// any of them has the same bits.  Accuracy vs glibc (correctly rounded in practice,
+// what NumPy calls): tools/fastmath/ulp_check.cpp, tools/probe/fastmath_probe.hip.
+struct TrigRed { double r, rr; int q; };
+
+__host__ __device__ __forceinline__ TrigRed trig_reduce(double x) {
+  const double k = rint(x * kTwoOverPi);
+  const double t = fma(-k, kPio2Hi, x);
+  const double a = k * kPio2Mid;
+  const double al = fma(k, kPio2Mid, -a);
+  const double r0 = t - a;                          // TwoSum(t, -a): |t| < |a| near k*pi/2
+  const double bb = r0 - t;
+  const double e0 = (t - (r0 - bb)) + (-a - bb);
+  const double e = (e0 - al) - k * kPio2Lo;
+  TrigRed o;
+  o.r = r0 + e;                                     // renormalise (Fast2Sum, |r0| >= |e|)
+  o.rr = e - (o.r - r0);
+  o.q = (int)k & 3;
+  return o;
+}
+
+// The two roundings that dominate beyond fdlibm's: S1 as a double (up to ~0.2 ulp of
+// sin at |r| ~ pi/4: its low part goes into the tail) and z = r*r in cos's 1 - z/2 (up to
+// ~0.25 ulp: the exact error zl of r*r, by FMA, goes into the tail).
+__host__ __device__ __forceinline__ double ksin(double r, double rr, double z) {
+  const double v = z * r;
+  double p = kSinC[6];
+#pragma unroll
+  for (int k = 5; k >= 1; --k) p = fma(p, z, kSinC[k]);
+  return r - ((z * (0.5 * rr - v * p) - rr) - fma(v, kSinC0Lo, v * kSinC[0]));
+}
+
+__host__ __device__ __forceinline__ double kcos(double r, double rr, double z) {
+  double p = kCosC[5];
+#pragma unroll
+  for (int k = 4; k >= 0; --k) p = fma(p, z, kCosC[k]);
+  const double zl = fma(r, r, -z);                  // r*r = z + zl exactly
+  const double hz = 0.5 * z;
+  const double w = 1.0 - hz;
+  return w + ((((1.0 - w) - hz) - 0.5 * zl) + (z * (z * p) - r * rr));
+}
+
+__host__ __device__ __forceinline__ void sincos_t(double x, double* s, double* c) {
+  const TrigRed t = trig_reduce(x);
+  const double z = t.r * t.r;
+  const double ss = ksin(t.r, t.rr, z), cc = kcos(t.r, t.rr, z);
+  const double sq = (t.q & 1) ? cc : ss, cq = (t.q & 1) ? ss : cc;
+  *s = x == 0.0 ? x : ((t.q & 2) ? -sq : sq);        // sin(-0) = -0
+  *c = ((t.q + 1) & 2) ? -cq : cq;
+}
+
+__host__ __device__ __forceinline__ double sin_t(double x) {
+  const TrigRed t = trig_reduce(x);
+  const double z = t.r * t.r;
+  const double v = (t.q & 1) ? kcos(t.r, t.rr, z) : ksin(t.r, t.rr, z);
+  return x == 0.0 ? x : ((t.q & 2) ? -v : v);
+}
+
+__host__ __device__ __forceinline__ double cos_t(double x) {
+  const TrigRed t = trig_reduce(x);
+  const double z = t.r * t.r;
+  const double v = (t.q & 1) ? ksin(t.r, t.rr, z) : kcos(t.r, t.rr, z);
+  return ((t.q + 1) & 2) ? -v : v;
+}
+
+}  // namespace bsg

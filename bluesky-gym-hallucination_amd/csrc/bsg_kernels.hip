@@ -96,7 +96,7 @@ constexpr double WIND_ALTSTEP = 100.0 * FT;
 constexpr double WIND_ALTMAX = 45000.0 * FT;
 
 __device__ __forceinline__ double idw_weight(double lat, double lon, double latp, double lonp) {
-  const double cavelat = cos((0.5 * (lat + latp)) * kD2R);
+  const double cavelat = cos_t((0.5 * (lat + latp)) * kD2R);
   const double dy = (lat - latp) * kD2R;
   const double dx = cavelat * ((lon - lonp) * kD2R);
   return 1.0 / (1e-16 + dx * dx + dy * dy);
@@ -169,7 +169,7 @@ __device__ __forceinline__ double hdg_command_track(const WindDev& w, const AC& 
       double wn, we;
       wind_at(w, s.lat, s.lon, s.alt, &wn, &we);
       double sh, ch;
-      sincos(hdg * kD2R, &sh, &ch);
+      sincos_t(hdg * kD2R, &sh, &ch);
       const double tasnorth = s.tas * ch, taseast = s.tas * sh;
       return pymod(atan2(taseast + we, tasnorth + wn) * kR2D, 360.0);
     }
@@ -255,7 +255,7 @@ __device__ __forceinline__ void memo_init(Memo& m, const AC& s) {
   m.rad_bits = kNoKey; m.turnrad = 0;
   m.last_alt = s.alt;
   m.cas_tas_bits = kNoKey; m.cas_alt_bits = kNoKey;
-  sincos(s.lat * kD2R, &m.sinlat, &m.coslat);
+  sincos_t(s.lat * kD2R, &m.sinlat, &m.coslat);
 }
 
 // issued at kernel entry together with the state loads (one memory round trip)
@@ -323,7 +323,7 @@ __device__ __forceinline__ void memo_final_cas(Memo& m, AC& s) {
 __device__ __forceinline__ void memo_wp(Memo& m, const RouteRegs& rt, int k) {
   m.wp_k = k;
   rt.get(k, &m.wp_lat, &m.wp_lon, &m.wp_nq);
-  sincos(m.wp_lat * kD2R, &m.wp_sin, &m.wp_cos);
+  sincos_t(m.wp_lat * kD2R, &m.wp_sin, &m.wp_cos);
 }
 
 // ---- one BlueSky substep of one aircraft (Traffic.update, RESO OFF) ------------------
@@ -421,7 +421,7 @@ __device__ __forceinline__ void substep(AC& s, Memo& m, double dt, const RouteRe
     const double Vw = sqrt(vwn * vwn + vwe * vwe);
     const double winddir = atan2(vwe, vwn);
     const double drift = s.ap_trk * kD2R - winddir;
-    const double steer = asin(npmin(1.0, npmax(-1.0, Vw * sin(drift) / npmax(0.001, s.tas))));
+    const double steer = asin(npmin(1.0, npmax(-1.0, Vw * sin_t(drift) / npmax(0.001, s.tas))));
     hdg_cmd = pymod(s.ap_trk + steer * kR2D, 360.0);
   } else {
     hdg_cmd = pymod(s.ap_trk, 360.0);
@@ -479,7 +479,7 @@ __device__ __forceinline__ void substep(AC& s, Memo& m, double dt, const RouteRe
   if (!isfinite(s.vs)) s.vs = 0.0;
   // update_groundspeed + update_pos
   if (bits(s.hdg) != m.hdg_bits) {        // straight flight keeps its heading trig
-    sincos(s.hdg * kD2R, &m.shdg, &m.chdg);
+    sincos_t(s.hdg * kD2R, &m.shdg, &m.chdg);
     m.hdg_bits = bits(s.hdg);
   }
   const double shdg = m.shdg, chdg = m.chdg;
@@ -500,7 +500,7 @@ __device__ __forceinline__ void substep(AC& s, Memo& m, double dt, const RouteRe
   if (swaltsel) s.alt = divk(rint((s.alt + s.vs * dt) * 1e6), 1e6);   // a branch: level flight
   else s.alt = allow_h;                                            // skips the division
   s.lat = s.lat + divk(dt * gsnorth, Rearth) * kR2D;
-  sincos(s.lat * kD2R, &m.sinlat, &m.coslat);
+  sincos_t(s.lat * kD2R, &m.sinlat, &m.coslat);
   s.lon = s.lon + divk(dt * gseast / m.coslat, Rearth) * kR2D;
 }
 
@@ -530,13 +530,13 @@ __device__ __forceinline__ void stage(LT& L, int lane, const AC& s) {
   L.lat[lane] = s.lat; L.lon[lane] = s.lon; L.alt[lane] = s.alt; L.hdg[lane] = s.hdg;
   L.tas[lane] = s.tas; L.vs[lane] = s.vs;
   double st, ct;
-  sincos(s.hdg * kD2R, &st, &ct);
+  sincos_t(s.hdg * kD2R, &st, &ct);
   L.u[lane] = s.tas * st;
   L.v[lane] = s.tas * ct;
   if constexpr (LT::kWind) {
     L.gs[lane] = s.gs;
     double sk, ck;
-    sincos(s.trk * kD2R, &sk, &ck);
+    sincos_t(s.trk * kD2R, &sk, &ck);
     L.cu[lane] = s.gs * sk;
     L.cv[lane] = s.gs * ck;
   }
@@ -651,7 +651,7 @@ __device__ __forceinline__ CdOut cd_pair(const LT& L, int i, int k) {
   const double latk = L.lat[k], lonk = L.lon[k];
   const double dlat = (latk - lati) * kD2R;
   const double dlon = (pymod((lonk - loni) + 180.0, 360.0) - 180.0) * kD2R;
-  const double cavelat = cos(((lati + latk) * kD2R) * 0.5);
+  const double cavelat = cos_t(((lati + latk) * kD2R) * 0.5);
   const double dangle = sqrt(dlat * dlat + (dlon * dlon) * (cavelat * cavelat));
   const double dist = divk(6371000.0 * dangle, NM) * NM + 0.0;     // + 1e9*I, I = 0
   const double du = cd_u(L, k) - cd_u(L, i);
@@ -677,7 +677,7 @@ __device__ __forceinline__ CdOut cd_pair(const LT& L, int i, int k) {
   // undecided by the bounds: the exact StateBased arithmetic
   const double qdr = pymod(atan2(dlon * cavelat, dlat) * kR2D, 360.0);
   double sq, cq;
-  sincos(qdr * kD2R, &sq, &cq);
+  sincos_t(qdr * kD2R, &sq, &cq);
   const double dx = dist * sq;
   const double dy = dist * cq;
   const double tcpa = -(du * dx + dv * dy) / dv2 + 0.0;
@@ -757,8 +757,8 @@ __device__ __forceinline__ void creconfs_place(AC& s, double gsref, double dpsi,
   const double cpam = cpa * NM;
   const double pzr = RPZ;
   const double trk = trkref + dpsi * kD2R;
-  const double gsn = gsref * cos(trk), gse = gsref * sin(trk);
-  const double vreln = gsref * cos(trkref) - gsn, vrele = gsref * sin(trkref) - gse;
+  const double gsn = gsref * cos_t(trk), gse = gsref * sin_t(trk);
+  const double vreln = gsref * cos_t(trkref) - gsn, vrele = gsref * sin_t(trkref) - gse;
   const double vrel = sqrt(vreln * vreln + vrele * vrele);
   const double drelcpa = tlosh * vrel + (cpam > pzr ? 0.0 : sqrt(pzr * pzr - cpam * cpam));
   const double dist = sqrt(drelcpa * drelcpa + cpam * cpam);
@@ -989,7 +989,7 @@ __device__ __forceinline__ bool lane_obs(const LT& L, int base, int lane, double
   // kwikdist_matrix (merge_env.py:195) and kwikqdrdist (:203) forms
   const double dlat = (latj - lat0) * kD2R;
   const double dlon = (pymod((lonj - lon0) + 180.0, 360.0) - 180.0) * kD2R;
-  const double cavelat = cos(((lat0 + latj) * kD2R) * 0.5);
+  const double cavelat = cos_t(((lat0 + latj) * kD2R) * 0.5);
   const double dist = divk(6371000.0 * sqrt(dlat * dlat + dlon * dlon * cavelat * cavelat), NM);
   const double qdr = pymod(atan2(dlon * cavelat, dlat) * kR2D, 360.0);
   if constexpr (KIND == BSG_ENV_MERGE) {
@@ -997,7 +997,7 @@ __device__ __forceinline__ bool lane_obs(const LT& L, int base, int lane, double
     // ownship: drift = bound180(hdg - qdr to the waypoint) and its cos/sin (own_obs)
     const double ang = is_own ? bound180(hdg0 - qdr) : qdr;
     double sb, cb;
-    sincos(ang * kD2R, &sb, &cb);
+    sincos_t(ang * kD2R, &sb, &cb);
     if (is_own) {
       own->wdist = dist; own->drift = ang; own->sd = sb; own->cd = cb;
       *sortkey = __builtin_inf();
@@ -1010,13 +1010,13 @@ __device__ __forceinline__ bool lane_obs(const LT& L, int base, int lane, double
     const double vx_r = L.v[lane] - L.v[base], vy_r = L.u[lane] - L.u[base];
     const double track = atan2(vy_r, vx_r);
     double st, ct;
-    sincos(track, &st, &ct);
+    sincos_t(track, &st, &ct);
     o[0] = x_r; o[1] = y_r; o[2] = vx_r; o[3] = vy_r; o[4] = ct; o[5] = st; o[6] = dmat;
     *sortkey = dmat;
     return dist < 4;                                       // _check_intrusion :280-281
   } else if constexpr (KIND == BSG_ENV_SECTOR_CR) {
     // sector_cr_env.py:245-278: positions in the flat NM frame about CENTER, in metres
-    const double cc = cos(SC_CLAT * kD2R);
+    const double cc = cos_t(SC_CLAT * kD2R);
     const double x0 = (((lat0 - SC_CLAT) * 60) * 1.852) * 1000;
     const double y0 = ((((lon0 - SC_CLON) * 60) * cc) * 1.852) * 1000;
     const double xj = (((latj - SC_CLAT) * 60) * 1.852) * 1000;
@@ -1026,7 +1026,7 @@ __device__ __forceinline__ bool lane_obs(const LT& L, int base, int lane, double
     const double vx_r = L.v[lane] - L.v[base], vy_r = L.u[lane] - L.u[base];
     const double track = atan2(vy_r, vx_r);
     double st, ct;
-    sincos(track, &st, &ct);
+    sincos_t(track, &st, &ct);
     o[0] = dx; o[1] = dy; o[2] = vx_r; o[3] = vy_r; o[4] = ct; o[5] = st; o[6] = d;
     *sortkey = d;
     return dist < 5;                                       // _check_intrusion :329-338
@@ -1037,8 +1037,8 @@ __device__ __forceinline__ bool lane_obs(const LT& L, int base, int lane, double
     const double bearing = bound180(hdg0 - qdr);
     const double hd = hdg0 - L.hdg[lane];
     double sbr, cbr, shd, chd;
-    sincos(bearing * kD2R, &sbr, &cbr);
-    sincos(hd * kD2R, &shd, &chd);
+    sincos_t(bearing * kD2R, &sbr, &cbr);
+    sincos_t(hd * kD2R, &shd, &chd);
     o[0] = dist * 1.852;                                    // intruder_distance (km)
     o[1] = cbr;
     o[2] = sbr;
@@ -1115,7 +1115,7 @@ __device__ __forceinline__ void own_obs(const KParams& p, const LT& L, int lane,
     if (p.wind.augment) {
       double wn, we, sh, ch;
       wind_at(p.wind, lat, lon, L.alt[lane], &wn, &we);
-      sincos(L.hdg[lane] * kD2R, &sh, &ch);
+      sincos_t(L.hdg[lane] * kD2R, &sh, &ch);
       sc[5] = divk((wn * ch + we * sh), 50.0);
       sc[6] = divk((-wn * sh + we * ch), 50.0);
     }
@@ -1126,7 +1126,7 @@ __device__ __forceinline__ void own_obs(const KParams& p, const LT& L, int lane,
     kwikqdrdist(lat, lon, p.cfg.wpt_lat[w], p.cfg.wpt_lon[w], &wqdr, wdist);
     *drift = bound180(L.hdg[lane] - wqdr);
     double sd, cd;
-    sincos(*drift * kD2R, &sd, &cd);
+    sincos_t(*drift * kD2R, &sd, &cd);
     sc[0] = L.tas[lane]; sc[1] = cd; sc[2] = (double)ev.wpt_reach; sc[3] = sd; sc[4] = divk(*wdist, 250.0);
   } else if constexpr (KIND == BSG_ENV_SECTOR_CR) {
     // sector_cr_env.py:233-243
@@ -1134,7 +1134,7 @@ __device__ __forceinline__ void own_obs(const KParams& p, const LT& L, int lane,
     kwikqdrdist(lat, lon, ev.wpt_lat, ev.wpt_lon, &wqdr, &wd);
     *drift = bound180(L.hdg[lane] - wqdr);
     double sd, cd;
-    sincos(*drift * kD2R, &sd, &cd);
+    sincos_t(*drift * kD2R, &sd, &cd);
     sc[0] = divk((L.tas[lane] - 150), 6.0); sc[1] = cd; sc[2] = sd; sc[3] = 0.0; sc[4] = 0.0;
   } else if constexpr (KIND == BSG_ENV_STATIC_OBSTACLE) {
     // static_obstacle_env.py:231-246 (waypoint terms; obstacles in static_obs_write)
@@ -1143,7 +1143,7 @@ __device__ __forceinline__ void own_obs(const KParams& p, const LT& L, int lane,
     *wdist = wd * 1.852;
     *drift = bound180(L.hdg[lane] - wqdr);
     double sd, cd;
-    sincos(*drift * kD2R, &sd, &cd);
+    sincos_t(*drift * kD2R, &sd, &cd);
     sc[0] = divk(*wdist, 170.0); sc[1] = cd; sc[2] = sd; sc[3] = 0.0; sc[4] = 0.0;
   } else if constexpr (KIND == BSG_ENV_PLAN_WAYPOINT) {
     // plan_obs (five waypoints)
@@ -1154,7 +1154,7 @@ __device__ __forceinline__ void own_obs(const KParams& p, const LT& L, int lane,
     *wdist = wd * 1.852;                                   // km
     *drift = bound180(L.hdg[lane] - wqdr);
     double sd, cd;
-    sincos(*drift * kD2R, &sd, &cd);
+    sincos_t(*drift * kD2R, &sd, &cd);
     sc[0] = cd; sc[1] = sd; sc[2] = divk(*wdist, 150.0); sc[3] = 0.0; sc[4] = 0.0;
   } else {
     const double altitude = L.alt[lane], vz = L.vs[lane];
@@ -1222,7 +1222,7 @@ __device__ __forceinline__ void static_obs_write(const double* geo, double lat, 
     kwikqdrdist(lat, lon, g[0], g[1], &qdr, &d);
     const double bearing = bound180(hdg - qdr);
     double sb, cb;
-    sincos(bearing * kD2R, &sb, &cb);
+    sincos_t(bearing * kD2R, &sb, &cb);
     put(o, cb);                                         // cos_difference_restricted_area_pos
     put(SO_NOBST + 3 + o, divk((d * 1.852), 170.0));           // restricted_area_distance
     put(2 * SO_NOBST + 3 + o, divk(g[2], 50.0));               // restricted_area_radius
@@ -1242,7 +1242,7 @@ __device__ __forceinline__ void plan_obs(const double* geo, double lat, double l
     dkm[k] = d * 1.852;
     const double drift = bound180(hdg - qdr);
     double sd, cd;
-    sincos(drift * kD2R, &sd, &cd);
+    sincos_t(drift * kD2R, &sd, &cd);
     const double f = ((reach >> k) & 1) ? 0.0 : 1.0;
     po[k] = f * cd;                                  // cos_difference
     po[PW_NWPT + k] = f * sd;                        // sin_difference

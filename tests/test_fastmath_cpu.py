@@ -1,9 +1,9 @@
 """CPU checks of the kernel's fixed-exponent powers and constant atmospheres (no GPU).
 
-bsg_fastpow.h replaces the device libm pow of the atmosphere / CAS-TAS chain
+bsg_fastmath.h replaces the device libm pow of the atmosphere / CAS-TAS chain
 (oracle/bluesky_subset.py vatmos, vtas2cas, vcas2tas) by Chebyshev polynomials; the
 device/host bit-identity and the ulp statistics against glibc are measured by
-tools/probe/fastpow_probe.hip (profiles/r02/fastpow_probe.txt).  Here: the generated
+tools/probe/fastmath_probe.hip (profiles/r02/fastmath_probe.txt).  Here: the generated
 coefficients approximate the powers they claim to (exact binary64 exponents), and the
 two constant atmospheres hard-coded in bsg_device.h are the oracle's vatmos values.
 """
@@ -19,7 +19,7 @@ CSRC = os.path.join(os.path.dirname(__file__), "..", "bluesky-gym-hallucination_
 
 
 def _coeffs():
-    txt = open(os.path.join(CSRC, "bsg_fastpow_coeffs.h")).read()
+    txt = open(os.path.join(CSRC, "bsg_fastmath_coeffs.h")).read()
     out = {}
     for name in ("T", "35", "27"):
         x0 = float(re.search(rf"kPow{name}_X0 = ([^;]+);", txt).group(1))

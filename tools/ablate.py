@@ -37,6 +37,10 @@ for name, cfg, E, cd in [
     ("vert32_full_2048", config.vertical_config(num_intruders=31), 2048, True),
     ("descent_4096", config.descent_config(), 4096, False),
     ("horiz32_full_4096", config.horizontal_config(num_intruders=31), 4096, True),
+    ("merge32_full_512", config.merge_config(num_ac=32), 512, True),      # C4 shard at 8 GPUs
+    ("merge32_full_1024", config.merge_config(num_ac=32), 1024, True),    # C4 shard at 4 GPUs
+    ("merge32_full_2048", config.merge_config(num_ac=32), 2048, True),    # C4 shard at 2 GPUs
+    ("descent_512", config.descent_config(), 512, False),                 # C5 shard at 8 GPUs
     ("merge32_full_8192", config.merge_config(num_ac=32), 8192, True),
     ("merge32_full_16384", config.merge_config(num_ac=32), 16384, True),
 ]:

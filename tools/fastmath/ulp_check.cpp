@@ -1,5 +1,5 @@
-// Host accuracy check of bsg_fastpow.h (container-only dev tool, no GPU):
-//   hipcc -O2 -x hip --offload-arch=gfx950 tools/fastpow/ulp_check.cpp -o /tmp/ulp_check && /tmp/ulp_check
+// Host accuracy check of bsg_fastmath.h (container-only dev tool, no GPU):
+//   hipcc -O2 -x hip --offload-arch=gfx950 tools/fastmath/ulp_check.cpp -o /tmp/ulp_check && /tmp/ulp_check
 // The polynomials are FMA/mul/add chains, so the host evaluates them bit for bit as
 // gfx950 does (IEEE binary64, round to nearest).  For each power: N random arguments
 // uniform on its range plus a dense sweep; errors in ulps of the result against powl
@@ -10,7 +10,7 @@
 #include <cstring>
 #include <random>
 
-#include "../../bluesky-gym-hallucination_amd/csrc/bsg_fastpow.h"
+#include "../../bluesky-gym-hallucination_amd/csrc/bsg_fastmath.h"
 
 static double ulp_of(double x) { return std::nextafter(std::fabs(x), INFINITY) - std::fabs(x); }
 
@@ -72,7 +72,48 @@ static void div_check() {
   }
 }
 
+// sin / cos against glibc and the x87 extended sinl / cosl on the argument ranges the
+// kernel uses (headings and bearings in radians, latitudes, longitude gaps, wider), plus
+// every whole and half degree and the multiples of pi/2 as the kernel forms them
+static void trig_check() {
+  struct R { const char* name; double lo, hi; };
+  const R rs[] = {{"[-pi/2, pi/2] (latitudes)", -1.5707963267948966, 1.5707963267948966},
+                  {"[0, 2pi) (headings)", 0.0, 6.283185307179586},
+                  {"[-0.2, 0.2] (longitude gaps)", -0.2, 0.2},
+                  {"[-100, 100]", -100.0, 100.0}};
+  std::mt19937_64 rng(11);
+  for (const R& r : rs) {
+    Stat ss, sc;
+    std::uniform_real_distribution<double> U(r.lo, r.hi);
+    for (long i = 0; i < 4000000; ++i) {
+      const double x = U(rng);
+      double s, c;
+      bsg::sincos_t(x, &s, &c);
+      ss.add(s, std::sin(x), sinl((long double)x));
+      sc.add(c, std::cos(x), cosl((long double)x));
+      if (s != bsg::sin_t(x) || c != bsg::cos_t(x)) std::printf("  sin_t/cos_t differ from sincos_t at %.17g\n", x);
+    }
+    std::printf("sin %-28s max err vs sinl %.3f ulp, max |ours - glibc| %.3f ulp, identical to glibc %.3f%%\n",
+                r.name, ss.max_ref, ss.max_glibc, 100.0 * ss.same / ss.n);
+    std::printf("cos %-28s max err vs cosl %.3f ulp, max |ours - glibc| %.3f ulp, identical to glibc %.3f%%\n",
+                r.name, sc.max_ref, sc.max_glibc, 100.0 * sc.same / sc.n);
+  }
+  long bad = 0;
+  for (int d = -7200; d <= 7200; ++d) {       // every half degree in [-3600, 3600] deg
+    const double x = (d * 0.5) * (3.141592653589793238 / 180.0);
+    double s, c;
+    bsg::sincos_t(x, &s, &c);
+    const double gs = std::sin(x), gc = std::cos(x);
+    bad += std::fabs(s - gs) > ulp_of(gs) || std::fabs(c - gc) > ulp_of(gc);
+  }
+  std::printf("sin/cos at every half degree in [-3600, 3600]: %ld more than 1 ulp from glibc\n", bad);
+  double s, c;
+  bsg::sincos_t(-0.0, &s, &c);
+  std::printf("sincos_t(-0) = (%g, %g), signbit(sin) %d\n", s, c, (int)std::signbit(s));
+}
+
 int main() {
+  trig_check();
   div_check();
   const double cT = 4.256848030018761, c27 = 2.0 / 7.0;
   run("pow(x, 4.256848030018761)", bsg::kPowT_LO, bsg::kPowT_HI, (long double)cT, cT,

@@ -24,6 +24,6 @@ fi
 [ "${SKIP_BENCH:-0}" = 1 ] && exit 0
 run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit 1
 run bench 600 python bench.py || exit 1
-cp "$OUT/bench.log" "$OUT/bench.json"
+grep "^{" "$OUT/bench.log" > "$OUT/bench.json"
 [ "${SKIP_PROF:-0}" = 1 ] && exit 0
 run profile 900 bash tools/profile.sh "$TAG" || exit 1

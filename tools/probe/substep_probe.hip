@@ -1,0 +1,73 @@
+// Probe on gfx950: latency of the BlueSky substep (substep<false> of bsg_kernels.hip) for
+// one wave of real Merge aircraft (two envs, 64 lanes), one wave on the chip -- the
+// single-wave regime that bounds a C4 shard (512 envs/GPU) and the kernel's critical
+// path.  State comes from tools/probe/substep_probe.py (a DeviceBatch after 30 steps).
+//   hipcc -O3 -std=c++17 --offload-arch=gfx950 -ffp-contract=off -fno-fast-math \
+//         -mllvm -disable-machine-licm tools/probe/substep_probe.hip -o tools/probe/substep_probe
+#include "../../bluesky-gym-hallucination_amd/csrc/bsg_kernels.hip"
+
+#include <cstdio>
+#include <vector>
+
+constexpr int NF = 12;       // lat lon alt hdg tas cas vs ax ap_trk selspd selalt selvs, + nav
+constexpr int SMAX = 16;
+
+__global__ void probe(bsg::Route route, const double* st, int S, long long* cyc, double* out) {
+  using namespace bsg;
+  const int l = threadIdx.x;
+  AC s{};
+  double* f[NF] = {&s.lat, &s.lon, &s.alt, &s.hdg, &s.tas, &s.cas, &s.vs, &s.ax, &s.ap_trk,
+                   &s.selspd, &s.selalt, &s.selvs};
+  for (int k = 0; k < NF; ++k) *f[k] = st[k * 64 + l];
+  s.nav = (int)st[NF * 64 + l];
+  s.gs = s.tas; s.trk = s.hdg;
+  Memo m;
+  memo_init(m, s);
+  RouteRegs rt;
+  rt.load(route);
+  WindDev w{};
+  long long t[SMAX + 1];
+  t[0] = __builtin_amdgcn_s_memtime();
+  for (int it = 0; it < S; ++it) {
+    substep<false>(s, m, 5.0, rt, w);
+    t[it + 1] = __builtin_amdgcn_s_memtime();
+  }
+  if (l == 0)
+    for (int it = 0; it < S; ++it) cyc[it] = t[it + 1] - t[it];
+  for (int k = 0; k < NF; ++k) out[k * 64 + l] = *f[k];
+}
+
+int main(int argc, char** argv) {
+  if (argc < 2) { std::printf("usage: substep_probe state.bin\n"); return 2; }
+  FILE* fp = std::fopen(argv[1], "rb");
+  if (!fp) return 2;
+  std::vector<double> hdr(1 + 3 * BSG_MAX_ROUTE), st((NF + 1) * 64);
+  if (std::fread(hdr.data(), 8, hdr.size(), fp) != hdr.size() ||
+      std::fread(st.data(), 8, st.size(), fp) != st.size()) return 2;
+  std::fclose(fp);
+  bsg::Route route{};
+  route.len = (int)hdr[0];
+  for (int k = 0; k < BSG_MAX_ROUTE; ++k) {
+    route.lat[k] = hdr[1 + k]; route.lon[k] = hdr[1 + BSG_MAX_ROUTE + k];
+    route.next_qdr[k] = hdr[1 + 2 * BSG_MAX_ROUTE + k];
+  }
+  double *dst, *dout;
+  long long* dcyc;
+  if (hipMalloc(&dst, st.size() * 8) != hipSuccess || hipMalloc(&dout, NF * 64 * 8) != hipSuccess ||
+      hipMalloc(&dcyc, SMAX * 8) != hipSuccess) return 1;
+  (void)hipMemcpy(dst, st.data(), st.size() * 8, hipMemcpyHostToDevice);
+  const int S = 10;
+  std::vector<long long> best(S, 1LL << 62);
+  for (int rep = 0; rep < 7; ++rep) {
+    hipLaunchKernelGGL(probe, dim3(1), dim3(64), 0, 0, route, dst, S, dcyc, dout);
+    std::vector<long long> c(S);
+    (void)hipMemcpy(c.data(), dcyc, S * 8, hipMemcpyDeviceToHost);
+    for (int i = 0; i < S; ++i) best[i] = c[i] < best[i] ? c[i] : best[i];
+  }
+  long long tot = 0;
+  std::printf("substep cycles (one wave, min of 7):");
+  for (int i = 0; i < S; ++i) { std::printf(" %lld", best[i]); tot += best[i]; }
+  std::printf("\nfirst %lld  mean of the rest %.0f  total %lld\n", best[0],
+              (double)(tot - best[0]) / (S - 1), tot);
+  return 0;
+}

@@ -1,0 +1,33 @@
+"""Dump one wave of real Merge aircraft (envs 0-1 of a 512 x 32 DeviceBatch after 30
+steps) for tools/probe/substep_probe.hip and run the probe binaries given on the
+command line (GPU box):  python tools/probe/substep_probe.py tools/probe/substep_probe [...]"""
+import os
+import subprocess
+import sys
+
+sys.path[:0] = [os.getcwd(), os.path.join(os.getcwd(), "bluesky-gym-hallucination_amd")]
+import numpy as np
+import torch
+
+from bluesky_gym import config, core
+from bluesky_gym import _native as nat
+
+cfg = config.merge_config(num_ac=32)
+b = core.DeviceBatch(cfg, 512, compute_cd=True, seed=1234)
+b.reset()
+g = torch.Generator(device="cuda").manual_seed(3)
+for _ in range(30):
+    b.step(torch.rand((512, 2), dtype=torch.float64, device="cuda", generator=g) * 2 - 1)
+torch.cuda.synchronize()
+c = cfg.to_c(512, nat.AUTORESET_NEXT_STEP, True, 1234, 0, 0)
+M = nat.MAX_ROUTE
+hdr = [c.route_len] + list(c.route_lat) + list(c.route_lon) + list(c.route_next_qdr)
+fields = ("lat", "lon", "alt", "hdg", "tas", "cas", "vs", "ax", "ap_trk", "selspd", "selalt", "selvs")
+st = [b.state[f].cpu().numpy().reshape(-1)[:64] for f in fields]
+st.append(b.state["nav"].cpu().numpy().reshape(-1)[:64].astype(np.float64))
+os.makedirs("gpurun_out", exist_ok=True)
+path = "gpurun_out/substep_state.bin"
+np.concatenate([np.asarray(hdr, np.float64)] + st).astype(np.float64).tofile(path)
+for exe in sys.argv[1:]:
+    print("==", exe, flush=True)
+    subprocess.run(["timeout", "-k", "5", "60", exe, path], check=True)
