@@ -362,14 +362,16 @@ def bench_descent_sac(args):
         return el
 
     el_env = timed(lambda k: b.step(bank[k % 16]), args.steps)
+    graph = world == 1 and not args.no_graph
     pol = sac_torch.RLLoop(b, sac, learn=False)
     pol.obs.copy_(b.obs)
-    el_pol = timed(lambda k: pol.step(), args.steps)
+    if graph:
+        pol.capture()
+    el_pol = timed((lambda k: pol.replay()) if graph else (lambda k: pol.step()), args.steps)
     rl = sac_torch.RLLoop(b, sac, learn=True)
     rl.obs.copy_(b.obs)
     for _ in range(8):                                # fill the buffer past one batch
         rl.step()
-    graph = world == 1 and not args.no_graph
     if graph:
         rl.capture()
     el_rl = timed((lambda k: rl.replay()) if graph else (lambda k: rl.step()), args.steps)

@@ -4,6 +4,7 @@
 // lives in bsg_kernels.hip.  No C++ exception crosses the ABI.
 #include <hip/hip_runtime.h>
 
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -268,6 +269,12 @@ int32_t bsg_create(const bsg_config* cfg, bsg_ctx** out) {
     c->route.lat[k] = cfg->route_lat[k];
     c->route.lon[k] = cfg->route_lon[k];
     c->route.next_qdr[k] = cfg->route_next_qdr[k];
+    // geo.rwgs84 of the waypoint latitude (the LNAV distance bounds' centre)
+    const double lat = cfg->route_lat[k] * (3.141592653589793 / 180.0);
+    const double a = 6378137.0, b = 6356752.314245;
+    const double an = a * a * std::cos(lat), bn = b * b * std::sin(lat);
+    const double ad = a * std::cos(lat), bd = b * std::sin(lat);
+    c->route.rwgs[k] = std::sqrt((an * an + bn * bn) / (ad * ad + bd * bd));
   }
   if (const char* pad = std::getenv("BSG_LDS_PAD_BYTES")) c->lds_pad = (unsigned)std::atoi(pad);
   *out = c;

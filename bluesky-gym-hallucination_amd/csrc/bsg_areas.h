@@ -102,7 +102,7 @@ __device__ __forceinline__ double get_hdg(double lat1d, double lon1d, double lat
   const double dlon = lon2 - lon1;
   const double x = sin_t(dlon) * cos_t(lat2);
   const double y = cos_t(lat1) * sin_t(lat2) - sin_t(lat1) * cos_t(lat2) * cos_t(dlon);
-  return pymod(atan2(x, y) * kR2D + 360.0, 360.0);
+  return pymod360(atan2(x, y) * kR2D + 360.0);
 }
 
 // ---- StaticObstacleEnv-v0 ----------------------------------------------------------------

@@ -56,15 +56,19 @@ __device__ __forceinline__ uint64_t bits(double x) { return (uint64_t)__double_a
 
 __device__ __forceinline__ double sgn(double x) { return (double)((x > 0.0) - (x < 0.0)); }
 
-// np.remainder / Python float % (numpy npy_divmod): fmod, then move toward b's sign.
-__device__ __forceinline__ double pymod(double a, double b) {
-  // exact fast path for b > 0, |a| < b: fmod(a, b) == a, then the floor-mod sign fix
-  if (b > 0.0 && fabs(a) < b) return a > 0.0 ? a : (a < 0.0 ? a + b : 0.0);
-  double mod = fmod(a, b);
+// np.remainder(a, 360.0) (numpy npy_divmod: fmod, then the sign fix).  |a| < 360 is every
+// call but a rare one: there fmod(a, 360) = a exactly, and the result is a + 360 for
+// a < 0 (npy_divmod's one rounding) or a + 0.0 otherwise (the identity, with -0 -> +0 as
+// copysign(0, 360) gives).  Other |a| take the fmod path behind a branch.  (A branch-free
+// exact form via trunc/FMA measured slower: its compare/select chain sits on the LNAV
+// critical path, tools/probe/substep_probe.hip.)
+__host__ __device__ __forceinline__ double pymod360(double a) {
+  if (fabs(a) < 360.0) return a < 0.0 ? a + 360.0 : a + 0.0;
+  double mod = fmod(a, 360.0);
   if (mod != 0.0) {
-    if ((b < 0.0) != (mod < 0.0)) mod += b;
+    if (mod < 0.0) mod += 360.0;
   } else {
-    mod = copysign(0.0, b);
+    mod = 0.0;
   }
   return mod;
 }
@@ -73,7 +77,7 @@ __device__ __forceinline__ double pymod(double a, double b) {
 __device__ __forceinline__ double npmax(double a, double b) { return (a >= b || a != a) ? a : b; }
 __device__ __forceinline__ double npmin(double a, double b) { return (a <= b || a != a) ? a : b; }
 
-__device__ __forceinline__ double degto180(double a) { return pymod(a + 180.0, 360.0) - 180.0; }
+__device__ __forceinline__ double degto180(double a) { return pymod360(a + 180.0) - 180.0; }
 
 // functions.py:4-22 bound_angle_positive_negative_180 (single wrap)
 __device__ __forceinline__ double bound180(double a) {
@@ -86,10 +90,15 @@ struct Atmos { double p, rho, T; };
 __device__ __forceinline__ Atmos vatmos(double h) {
   Atmos a;
   a.T = npmax(288.15 - 0.0065 * h, TSTRAT);
-  double rhotrop = 1.225 * pow_trop(divk(a.T, 288.15));
-  double dhstrat = npmax(0.0, h - 11000.0);
-  // exp(-0.0) == 1 exactly: the troposphere skips the exp (a branch, not a select)
-  a.rho = dhstrat > 0.0 ? rhotrop * exp(divk(-dhstrat, 6341.552161)) : rhotrop * 1.0;
+  const double x = divk_nn(a.T, 288.15);            // T >= 216.65 > 0
+  const double dhstrat = npmax(0.0, h - 11000.0);
+  // one branch: the troposphere at h >= 0 (T/288.15 in the polynomial's range, and
+  // exp(-0.0) == 1 exactly) is every altitude the envs fly but the HMAX ceiling, whose
+  // atmosphere is a constant (vatmos_limit)
+  double rho = 1.225 * poly_trop(x);
+  if (!(in_trop(x) && dhstrat == 0.0))
+    rho = 1.225 * pow_trop(x) * (dhstrat > 0.0 ? exp(divk(-dhstrat, 6341.552161)) : 1.0);
+  a.rho = rho;
   a.p = a.rho * RGAS * a.T;
   return a;
 }
@@ -106,15 +115,33 @@ __device__ __forceinline__ Atmos vatmos_limit(double h) {
   return vatmos(h);
 }
 
+// vtas2cas / vcas2tas: both powers by polynomial with one range test for the pair (a
+// branch is ~80 cycles of latency even when not taken); outside, both by the libm.
 __device__ __forceinline__ double tas2cas_at(double tas, const Atmos& a) {
-  double qdyn = a.p * (pow_3p5(1.0 + a.rho * tas * tas / (7.0 * a.p)) - 1.0);
-  double cas = sqrt(7.0 * P0 / RHO0 * (pow_2o7(divk(qdyn, P0) + 1.0) - 1.0));
+  const double z = 1.0 + a.rho * tas * tas / (7.0 * a.p);
+  double qdyn = a.p * (poly_3p5(z) - 1.0);
+  double y = divk_nn(qdyn, P0) + 1.0;               // qdyn >= 0
+  double yp = poly_2o7(y);
+  if (!(in_3p5(z) && in_2o7(y))) {
+    qdyn = a.p * (pow(z, 3.5) - 1.0);
+    y = divk(qdyn, P0) + 1.0;
+    yp = pow(y, 2.0 / 7.0);
+  }
+  const double cas = sqrt(7.0 * P0 / RHO0 * (yp - 1.0));
   return tas < 0 ? -1 * cas : cas;
 }
 
 __device__ __forceinline__ double cas2tas_at(double cas, const Atmos& a) {
-  double qdyn = P0 * (pow_3p5(1.0 + divk(RHO0 * cas * cas, 7.0 * P0)) - 1.0);
-  double tas = sqrt(7.0 * a.p / a.rho * (pow_2o7(1.0 + qdyn / a.p) - 1.0));
+  const double z = 1.0 + divk_nn(RHO0 * cas * cas, 7.0 * P0);
+  double qdyn = P0 * (poly_3p5(z) - 1.0);
+  double y = 1.0 + qdyn / a.p;
+  double yp = poly_2o7(y);
+  if (!(in_3p5(z) && in_2o7(y))) {
+    qdyn = P0 * (pow(z, 3.5) - 1.0);
+    y = 1.0 + qdyn / a.p;
+    yp = pow(y, 2.0 / 7.0);
+  }
+  const double tas = sqrt(7.0 * a.p / a.rho * (yp - 1.0));
   return cas < 0 ? -1 * tas : tas;
 }
 
@@ -142,39 +169,39 @@ __device__ __forceinline__ void casormach_at(double spd, const Atmos& a, double*
 __device__ __forceinline__ void kwikqdrdist(double lata, double lona, double latb, double lonb,
                                             double* qdr, double* dist) {
   double dlat = (latb - lata) * kD2R;
-  double dlon = (pymod((lonb - lona) + 180.0, 360.0) - 180.0) * kD2R;
+  double dlon = (pymod360((lonb - lona) + 180.0) - 180.0) * kD2R;
   double cavelat = cos_t(((lata + latb) * kD2R) * 0.5);
   double dangle = sqrt(dlat * dlat + dlon * dlon * cavelat * cavelat);
-  *dist = divk(6371000.0 * dangle, NM);
-  *qdr = pymod(atan2(dlon * cavelat, dlat) * kR2D, 360.0);
+  *dist = divk_nn(6371000.0 * dangle, NM);
+  *qdr = pymod360(atan2(dlon * cavelat, dlat) * kR2D);
 }
 
 __device__ __forceinline__ double kwikdist(double lata, double lona, double latb, double lonb) {
   double dlat = (latb - lata) * kD2R;
-  double dlon = (pymod((lonb - lona) + 180.0, 360.0) - 180.0) * kD2R;
+  double dlon = (pymod360((lonb - lona) + 180.0) - 180.0) * kD2R;
   double cavelat = cos_t(((lata + latb) * kD2R) * 0.5);
   double dangle = sqrt(dlat * dlat + dlon * dlon * cavelat * cavelat);
-  return divk(6371000.0 * dangle, NM);
+  return divk_nn(6371000.0 * dangle, NM);
 }
 
 // kwikdist_matrix element (operation order of the matrix form, merge_env.py:195)
 __device__ __forceinline__ double kwikdist_mat(double lata, double lona, double latb, double lonb) {
   double dlat = (latb - lata) * kD2R;
-  double dlon = (pymod((lonb - lona) + 180.0, 360.0) - 180.0) * kD2R;
+  double dlon = (pymod360((lonb - lona) + 180.0) - 180.0) * kD2R;
   double cavelat = cos_t(((latb + lata) * kD2R) * 0.5);
   double dangle = sqrt(dlat * dlat + (dlon * dlon) * (cavelat * cavelat));
-  return divk(6371000.0 * dangle, NM);
+  return divk_nn(6371000.0 * dangle, NM);
 }
 
 // kwikqdrdist_matrix element (StateBased.detect), [i][j] = from a=i to b=j
 __device__ __forceinline__ void kwikqdrdist_mat(double lata, double lona, double latb, double lonb,
                                                 double* qdr, double* dist) {
   double dlat = (latb - lata) * kD2R;
-  double dlon = (pymod((lonb - lona) + 180.0, 360.0) - 180.0) * kD2R;
+  double dlon = (pymod360((lonb - lona) + 180.0) - 180.0) * kD2R;
   double cavelat = cos_t(((lata + latb) * kD2R) * 0.5);
   double dangle = sqrt(dlat * dlat + (dlon * dlon) * (cavelat * cavelat));
-  *dist = divk(6371000.0 * dangle, NM);
-  *qdr = pymod(atan2(dlon * cavelat, dlat) * kR2D, 360.0);
+  *dist = divk_nn(6371000.0 * dangle, NM);
+  *qdr = pymod360(atan2(dlon * cavelat, dlat) * kR2D);
 }
 
 __device__ __forceinline__ void kwikpos(double latd1, double lond1, double qdr, double dist,
@@ -184,7 +211,7 @@ __device__ __forceinline__ void kwikpos(double latd1, double lond1, double qdr, 
   double dlat = divk(dy, 60.0);
   double dlon = dx / npmax(0.01, 60.0 * cos_t(latd1 * kD2R));
   *lat2 = latd1 + dlat;
-  *lon2 = pymod((lond1 + dlon) + 180.0, 360.0) - 180.0;
+  *lon2 = pymod360((lond1 + dlon) + 180.0) - 180.0;
 }
 
 __device__ __forceinline__ double rwgs84(double latd) {
@@ -267,41 +294,33 @@ __device__ __forceinline__ double qdrdist_exact_nm(double latd1, double latd2, d
         npmax(0.000001, fabs(latd1) + fabs(latd2));
   }
   double d = r * acos(x);
-  return divk(d, NM);
+  return divk_nn(d, NM);                      // d >= 0
 }
 
-// Bounds [lo, hi] (metres) on the distance the exact path would yield, (d / NM) * NM with
-// d = r*acos(x), from x alone -- no transcendental.  r = rwgs84(mid-latitude) lies in
-// [b, a] on the same-hemisphere branch.  acos(1 - u) = 2 asin(sqrt(u/2)) >= sqrt(2u) for
-// u in [0, 2] (asin(y) >= y), <= sqrt(2u)(1 + 1e-4) for u <= 1e-3 (asin(y)/y <= 1 +
-// 1.01 y^2/6 at y <= 0.0224) and <= sqrt(2u) pi/2 beyond (asin convex on [0, 1]).
-// u = 1 - x is exact (Sterbenz) where it matters; the 1e-12 relative slack covers the
-// rounding of sqrt, r, acos and the /NM*NM round trip (each ~1e-16).  Returns false (use
-// the exact path) off the same-hemisphere branch and for x >= 1 (where acos(x) is 0 or
-// NaN in the exact path).
-__device__ __forceinline__ bool qdrdist_bounds(double latd1, double latd2, double x, double* lo,
-                                               double* hi) {
-  if (!(latd1 * latd2 >= 0.0)) return false;
+// Squared bounds [lo2, hi2] (m^2) on the distance the exact path would yield, (d/NM)*NM
+// with d = rwgs84(mid-latitude) * acos(x), from x and the waypoint's radius rw -- no
+// sqrt, acos, sincos or division (each a 100-300 cycle link of the LNAV chain):
+//   r:    |d rwgs84 / d phi| <= a - b < 21,500 m/rad, so r(mid) is within
+//         21,500 * |phi_mid - phi_wp| of r(wp) = rw (host value, +-1e-6 m for the device's
+//         rounding of rwgs84 and of rw);
+//   acos: acos(1 - u) = 2 asin(sqrt(u/2)) in [sqrt(2u), sqrt(2u) (1 + 0.085 u)] for
+//         u <= 0.02 (asin y <= y (1 + 0.1675 y^2) at y <= 0.1), u = 1 - x exact (Sterbenz);
+//   the 3e-12 relative slack covers acos's ulp error, the /NM*NM round trip and the
+//   rounding of these products (each ~1e-16).
+// false (decide exactly): different hemispheres (the other rwgs84 branch) or u outside
+// (0, 0.02] -- x >= 1 (acos 0 or NaN) or beyond ~90 km, where LNAV never asks.
+// (Straight-line: the bounds are computed whatever the validity, which is returned.)
+__device__ __forceinline__ bool qdrdist_bounds2(double latd1, double latd2, double x, double rw,
+                                                double* lo2, double* hi2) {
   const double u = 1.0 - x;
-  if (!(u > 0.0)) return false;
-  const double sq = sqrt(2.0 * u);
-  *lo = (6356752.314245 * sq) * (1.0 - 1e-12);
-  *hi = (6378137.0 * sq) * ((u <= 1e-3 ? 1.0001 : 1.5707963267948966) * (1.0 + 1e-12));
-  return true;
-}
-
-// Bounds [lo, hi] on tan(h) as the device libm computes it, 0 <= h <= 1.5 rad, without a
-// transcendental: every Taylor coefficient of tan is positive, so the partial sum
-// h + h^3/3 + 2h^5/15 + 17h^7/315 is a lower bound; pi^2 h / (pi^2 - 4h^2) is an upper
-// bound on (0, pi/2) (Becker-Stark).  The 1e-12 relative slack covers tan's ulp error
-// and the rounding of both expressions (each ~1e-16).  false: h outside [0, 1.5].
-__device__ __forceinline__ bool tan_bounds(double h, double* lo, double* hi) {
-  if (!(h >= 0.0 && h <= 1.5)) return false;
-  const double h2 = h * h;
-  const double pi2 = 9.869604401089358;    // pi^2 rounded: the slack absorbs its error
-  *lo = (h + h * h2 * (1.0 / 3.0 + h2 * (2.0 / 15.0 + h2 * (17.0 / 315.0)))) * (1.0 - 1e-12);
-  *hi = (pi2 * h / (pi2 - 4.0 * h2)) * (1.0 + 1e-12);
-  return true;
+  const bool ok = (latd1 * latd2 >= 0.0) && (u > 0.0 && u <= 0.02);
+  const double dr = 21500.0 * (0.5 * fabs(latd1 - latd2) * kD2R) + 1e-6;
+  const double rlo = rw - dr, rhi = rw + dr;
+  const double q = 2.0 * u;
+  const double f = 1.0 + 0.085 * u;
+  *lo2 = (rlo * rlo) * q * (1.0 - 3e-12);
+  *hi2 = (rhi * rhi) * q * (f * f) * (1.0 + 3e-12);
+  return ok;
 }
 
 // functions.py:24-42 get_point_at_distance (R = 6371 km)

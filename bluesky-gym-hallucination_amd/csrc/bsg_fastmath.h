@@ -27,6 +27,9 @@ namespace bsg {
 // the generator) with c2, c1, c0 carried as hi + lo.  Rounding c0..c2 and the last steps
 // in plain binary64 costs up to ~2.5 ulp where the result is small against c0 (pow_trop
 // near 0.75); this way the one rounding that remains is the final add (~0.5 ulp).
+// The plain-FMA part (degree DEG-3 in d, its error scaled by d^3) runs as two interleaved
+// Horner halves, p = P_a(d) * d^m + P_b(d): half the dependent FMA depth (the substep
+// chains are latency-bound at one or two waves per SIMD).
 template <int DEG>
 __host__ __device__ __forceinline__ double poly_dd(const double (&c)[DEG + 1],
                                                    const double (&clo)[3], double d) {
@@ -47,21 +50,37 @@ __host__ __device__ __forceinline__ double poly_dd(const double (&c)[DEG + 1],
   return uh + ul;
 }
 
+// The polynomials alone (no range test): callers test the range of a whole chain once and
+// redo it with the libm pow when any argument is outside -- a branch costs ~80 cycles of
+// latency whether taken or not (tools/probe/latency_probe.hip), one per power adds up.
+__host__ __device__ __forceinline__ double poly_trop(double x) {
+  return poly_dd<kPowT_DEG>(kPowT_C, kPowT_CLO, x - kPowT_X0);
+}
+__host__ __device__ __forceinline__ double poly_3p5(double z) {
+  return poly_dd<kPow35_DEG>(kPow35_C, kPow35_CLO, z - kPow35_X0);
+}
+__host__ __device__ __forceinline__ double poly_2o7(double y) {
+  return poly_dd<kPow27_DEG>(kPow27_C, kPow27_CLO, y - kPow27_X0);
+}
+__host__ __device__ __forceinline__ bool in_trop(double x) { return x >= kPowT_LO && x <= kPowT_HI; }
+__host__ __device__ __forceinline__ bool in_3p5(double z) { return z >= kPow35_LO && z <= kPow35_HI; }
+__host__ __device__ __forceinline__ bool in_2o7(double y) { return y >= kPow27_LO && y <= kPow27_HI; }
+
 // pow(x, 4.256848030018761), the troposphere density ratio of vatmos
 __host__ __device__ __forceinline__ double pow_trop(double x) {
-  if (x >= kPowT_LO && x <= kPowT_HI) return poly_dd<kPowT_DEG>(kPowT_C, kPowT_CLO, x - kPowT_X0);
+  if (in_trop(x)) return poly_trop(x);
   return pow(x, 4.256848030018761);
 }
 
 // pow(z, 3.5)
 __host__ __device__ __forceinline__ double pow_3p5(double z) {
-  if (z >= kPow35_LO && z <= kPow35_HI) return poly_dd<kPow35_DEG>(kPow35_C, kPow35_CLO, z - kPow35_X0);
+  if (in_3p5(z)) return poly_3p5(z);
   return pow(z, 3.5);
 }
 
 // pow(y, 2.0 / 7.0)
 __host__ __device__ __forceinline__ double pow_2o7(double y) {
-  if (y >= kPow27_LO && y <= kPow27_HI) return poly_dd<kPow27_DEG>(kPow27_C, kPow27_CLO, y - kPow27_X0);
+  if (in_2o7(y)) return poly_2o7(y);
   return pow(y, 2.0 / 7.0);
 }
 
@@ -84,6 +103,15 @@ __host__ __device__ __forceinline__ double div_r(double x, double y, double ry) 
 
 // divisor known at compile time: 1.0 / y folds to RN(1/y)
 __host__ __device__ __forceinline__ double divk(double x, double y) { return div_r(x, y, 1.0 / y); }
+
+// the same for a finite numerator whose zero, if any, is +0 (every physically non-negative
+// quantity: temperatures, squared speeds, dynamic pressures, distances): the guard's
+// compare/select pair is half the latency of the division itself
+__host__ __device__ __forceinline__ double divk_nn(double x, double y) {
+  const double ry = 1.0 / y;
+  const double q = x * ry;
+  return fma(fma(-q, y, x), ry, q);
+}
 
 // ---- sin / cos ------------------------------------------------------------------------
 // The device libm's sincos spends ~75 VALU on its small-argument path (3-part

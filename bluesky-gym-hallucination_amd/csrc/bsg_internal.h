@@ -14,6 +14,8 @@ enum { MODE_STEP = 0, MODE_RESET = 1 };
 struct Route {
   int len;
   double lat[BSG_MAX_ROUTE], lon[BSG_MAX_ROUTE], next_qdr[BSG_MAX_ROUTE];
+  double rwgs[BSG_MAX_ROUTE];   // WGS84 radius rwgs84(lat) of each waypoint (host libm; used
+                                // only inside rounding-slack bounds, bsg_device.h)
 };
 
 struct WindDev {

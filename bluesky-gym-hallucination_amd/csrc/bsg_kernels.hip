@@ -171,7 +171,7 @@ __device__ __forceinline__ double hdg_command_track(const WindDev& w, const AC& 
       double sh, ch;
       sincos_t(hdg * kD2R, &sh, &ch);
       const double tasnorth = s.tas * ch, taseast = s.tas * sh;
-      return pymod(atan2(taseast + we, tasnorth + wn) * kR2D, 360.0);
+      return pymod360(atan2(taseast + we, tasnorth + wn) * kR2D);
     }
   }
   return hdg;
@@ -184,18 +184,18 @@ __device__ __forceinline__ double hdg_command_track(const WindDev& w, const AC& 
 // waypoints (unused by the in-scope envs) are read from the kernarg segment.
 struct RouteRegs {
   int len;
-  double lat0, lon0, nq0, lat1, lon1, nq1;
+  double lat0, lon0, nq0, rw0, lat1, lon1, nq1, rw1;
   const Route* r;
   __device__ __forceinline__ void load(const Route& rr) {
     r = &rr;
     len = rr.len;
-    lat0 = rr.lat[0]; lon0 = rr.lon[0]; nq0 = rr.next_qdr[0];
-    lat1 = rr.lat[1]; lon1 = rr.lon[1]; nq1 = rr.next_qdr[1];
+    lat0 = rr.lat[0]; lon0 = rr.lon[0]; nq0 = rr.next_qdr[0]; rw0 = rr.rwgs[0];
+    lat1 = rr.lat[1]; lon1 = rr.lon[1]; nq1 = rr.next_qdr[1]; rw1 = rr.rwgs[1];
   }
-  __device__ __forceinline__ void get(int k, double* la, double* lo, double* q) const {
-    if (k == 0) { *la = lat0; *lo = lon0; *q = nq0; }
-    else if (k == 1) { *la = lat1; *lo = lon1; *q = nq1; }
-    else { *la = r->lat[k]; *lo = r->lon[k]; *q = r->next_qdr[k]; }
+  __device__ __forceinline__ void get(int k, double* la, double* lo, double* q, double* rw) const {
+    if (k == 0) { *la = lat0; *lo = lon0; *q = nq0; *rw = rw0; }
+    else if (k == 1) { *la = lat1; *lo = lon1; *q = nq1; *rw = rw1; }
+    else { *la = r->lat[k]; *lo = r->lon[k]; *q = r->next_qdr[k]; *rw = r->rwgs[k]; }
   }
 };
 
@@ -208,10 +208,8 @@ struct Memo {
   bool lim_gd;                         //   (and its flight phase: GD or airborne)
   double allow_tas;
   int wp_k;                        // cached waypoint (coords, next-leg bearing, trig)
-  double wp_lat, wp_lon, wp_nq, wp_cos, wp_sin;
+  double wp_lat, wp_lon, wp_nq, wp_cos, wp_sin, wp_rw;
   double coslat, sinlat;           // cos/sin(lat * D2R) of the current latitude
-  uint64_t tr_bits;                // key of turnrate = deg(g0*tan(bank)/max(tas, eps))
-  double turnrate;
   uint64_t hdg_bits;               // key of (shdg, chdg) = sincos(hdg * D2R)
   double shdg, chdg;
   uint64_t rad_bits;               // key of the LNAV turn radius tas^2/(g0*tan(bank))
@@ -242,15 +240,15 @@ __device__ __forceinline__ double key_as_double(uint64_t k) { return __longlong_
 
 __device__ __forceinline__ double allow_h_of(double selalt) { return selalt > HMAX ? HMAX : selalt; }
 
-// OpenAP flight phase GD (on the ground): its own speed envelope and axmax
-__device__ __forceinline__ bool ground_phase(double alt) { return divk(alt, FT) <= GD_ALT_FT; }
+// OpenAP flight phase GD (on the ground): its own speed envelope and axmax (a -inf
+// altitude, the one input divk_nn would read differently, is not an aircraft)
+__device__ __forceinline__ bool ground_phase(double alt) { return divk_nn(alt, FT) <= GD_ALT_FT; }
 
 __device__ __forceinline__ void memo_init(Memo& m, const AC& s) {
   m.alt_bits = kNoKey; m.spd_bits = kNoKey; m.spdalt_bits = kNoKey;
   m.lim_tas_bits = kNoKey; m.lim_h_bits = kNoKey; m.lim_gd = false;
   m.at = Atmos{0, 0, 0}; m.ap_tas = 0; m.allow_tas = 0;
-  m.wp_k = -1; m.wp_lat = 0; m.wp_lon = 0; m.wp_nq = 0; m.wp_cos = 0; m.wp_sin = 0;
-  m.tr_bits = kNoKey; m.turnrate = 0;
+  m.wp_k = -1; m.wp_lat = 0; m.wp_lon = 0; m.wp_nq = 0; m.wp_cos = 0; m.wp_sin = 0; m.wp_rw = 0;
   m.hdg_bits = kNoKey; m.shdg = 0; m.chdg = 0;
   m.rad_bits = kNoKey; m.turnrad = 0;
   m.last_alt = s.alt;
@@ -322,9 +320,15 @@ __device__ __forceinline__ void memo_final_cas(Memo& m, AC& s) {
 
 __device__ __forceinline__ void memo_wp(Memo& m, const RouteRegs& rt, int k) {
   m.wp_k = k;
-  rt.get(k, &m.wp_lat, &m.wp_lon, &m.wp_nq);
+  rt.get(k, &m.wp_lat, &m.wp_lon, &m.wp_nq, &m.wp_rw);
   sincos_t(m.wp_lat * kD2R, &m.wp_sin, &m.wp_cos);
 }
+
+// Diagnostic hook of tools/probe/substep_probe.hip (section timing of one substep);
+// expands to nothing in every library build.
+#ifndef BSG_SUBSTEP_MARK
+#define BSG_SUBSTEP_MARK(i) do { } while (0)
+#endif
 
 // ---- one BlueSky substep of one aircraft (Traffic.update, RESO OFF) ------------------
 // oracle/bluesky_subset.py: traffic_update.  WIND: a wind field is set (wrappers/wind.py).
@@ -338,11 +342,12 @@ __device__ __forceinline__ void substep(AC& s, Memo& m, double dt, const RouteRe
   // Autopilot.update -- LNAV direct-to + ActiveWaypoint.reached
   if (s.nav & 1) {
     int k = (s.nav >> 8) & 0xff;
-    if (k != m.wp_k) memo_wp(m, rt, k);
     // the waypoint distance only feeds `dist < turndist` (turndist <= turnrad while the
-    // leg change is <= 90 deg) and `dist/|gs| < 4 s`; beyond both it need not be exact
-    if (bits(s.tas) != m.rad_bits) {
-      m.turnrad = divk(s.tas * s.tas, npmax(0.01, TAN_BANKDEF) * G0);
+    // leg change is <= 90 deg) and `dist/|gs| < 4 s`; beyond both it need not be exact.
+    // One branch for both memo keys (a branch is ~80 cycles of latency, taken or not).
+    if (k != m.wp_k || bits(s.tas) != m.rad_bits) {
+      if (k != m.wp_k) memo_wp(m, rt, k);
+      m.turnrad = divk_nn(s.tas * s.tas, npmax(0.01, TAN_BANKDEF) * G0);
       m.rad_bits = bits(s.tas);
     }
     const double turnrad = m.turnrad;
@@ -350,47 +355,63 @@ __device__ __forceinline__ void substep(AC& s, Memo& m, double dt, const RouteRe
     double qdr, x;
     const bool far = qdr_x(s.lat, s.lon, m.coslat, m.sinlat, m.wp_lat, m.wp_lon, m.wp_cos,
                            m.wp_sin, far_m, &qdr, &x);
+    BSG_SUBSTEP_MARK(5);
     const double next_qdr = m.wp_nq < -900.0 ? qdr : m.wp_nq;
-    const double half = 0.5 * fabs(degto180(pymod(qdr, 360.0) - pymod(next_qdr, 360.0)));
+    const double half = 0.5 * fabs(degto180(pymod360(qdr) - pymod360(next_qdr)));
+    // far and half <= 45: dist > far_m > turnrad >= turndist and dist > 4|gs|: not reached.
+    // Otherwise ActiveWaypoint.reached needs only `dist < turndist` and `dist/g < 4`: each
+    // is decided from squared bounds on the distance the exact path would compute
+    // (qdrdist_bounds2: no sqrt / acos / sincos / division) and the WGS84 radius and acos
+    // are evaluated only when a bound straddles a threshold.  Every threshold is >= 0, so
+    // comparing squares compares the values; the 1e-14 factors cover the squares'
+    // rounding.  (Making this block straight-line for every lane -- selects instead of the
+    // branch -- measured ~170 cycles slower per substep: tools/probe/substep_probe.hip.)
+    const bool need = !far || half > 45.0;
     bool reached = false;
-    // far and half <= 45: dist > far_m > turnrad >= turndist and dist > 4|gs|: not reached
-    if (!far || half > 45.0) {
-      // ActiveWaypoint.reached needs only `dist < turndist` and `dist/g < 4`; decide each
-      // from bounds on the distance the exact path would compute (qdrdist_bounds) and
-      // evaluate the WGS84 radius and acos only when a bound straddles a threshold
+    if (need) {
       const double g = npmax(0.0001, fabs(gsv));
-      double lo = 0.0, hi = 0.0;
-      int rtn = -1, cw = -1;                 // reached_turn / close2wp: -1 = undecided
-      if (qdrdist_bounds(s.lat, m.wp_lat, x, &lo, &hi)) {
-        if (half <= 45.0 && lo > turnrad * 1.000001) {
-          rtn = 0;                           // tan(half) <= 1 -> turndist <= turnrad < dist
-        } else {
-          // turndist = |turnrad * tan(half)| bounded without the tan (tan_bounds); the
-          // exact tan only when the bounds overlap the distance's
-          double tl, th;
-          if (tan_bounds(half * kD2R, &tl, &th))
-            rtn = hi < turnrad * tl * (1.0 - 1e-15) ? 1 : (lo >= turnrad * th * (1.0 + 1e-15) ? 0 : -1);
-          if (rtn < 0) {
-            const double turndist = fabs(turnrad * tan(half * kD2R));
-            rtn = hi < turndist ? 1 : (lo >= turndist ? 0 : -1);
-          }
-        }
-        cw = hi < 4.0 * g * 0.999999 ? 1 : (lo > 4.0 * g * 1.000001 ? 0 : -1);
-      }
+      double lo2, hi2;
+      const bool bv = qdrdist_bounds2(s.lat, m.wp_lat, x, m.wp_rw, &lo2, &hi2);
+      const double trm = turnrad * 1.000001;
+      // turndist = |turnrad * tan(half)| bounded without the tan: the Taylor lower bound tl and
+      // the Becker-Stark upper bound pi^2 h / (pi^2 - 4 h^2), cross-multiplied (no division)
+      const double h = half * kD2R;
+      const double h2 = h * h;
+      const double tl = (h + h * h2 * (1.0 / 3.0 + h2 * (2.0 / 15.0 + h2 * (17.0 / 315.0)))) * (1.0 - 1e-12);
+      const double pi2 = 9.869604401089358;
+      const double den = pi2 - 4.0 * h2;                          // > 0 for h <= 1.5
+      const double tnum = turnrad * (pi2 * h) * (1.0 + 1e-12);      // turnrad * th * den
+      const double tlo = turnrad * tl;
+      const bool tb = h >= 0.0 && h <= 1.5;
+      int rtn = (half <= 45.0 && lo2 > trm * trm * (1.0 + 1e-14)) ? 0   // tan(half) <= 1 < dist/turnrad
+              : !tb ? -1
+              : hi2 < tlo * tlo * (1.0 - 1e-14) ? 1
+              : lo2 * (den * den) >= tnum * tnum * (1.0 + 1e-14) ? 0 : -1;
+      const double glo = 4.0 * g * 0.999999, ghi = 4.0 * g * 1.000001;
+      int cw = hi2 < glo * glo * (1.0 - 1e-14) ? 1 : (lo2 > ghi * ghi * (1.0 + 1e-14) ? 0 : -1);
+      if (!bv) { rtn = -1; cw = -1; }
       if (rtn < 0 || cw < 0) {
-        const double dist = qdrdist_exact_nm(s.lat, m.wp_lat, x) * NM;
-        if (half <= 45.0 && dist > turnrad * 1.000001) {
-          rtn = 0;
-        } else {
+        if (bv && rtn < 0) {                   // the exact tan against the distance bounds
           const double turndist = fabs(turnrad * tan(half * kD2R));
-          rtn = dist < turndist;
+          const double td2 = turndist * turndist;
+          rtn = hi2 < td2 * (1.0 - 1e-14) ? 1 : (lo2 >= td2 * (1.0 + 1e-14) ? 0 : -1);
         }
-        // dist/g < 4, decided without the division outside a 1e-6 band around 4*g
-        cw = dist < 4.0 * g * 0.999999 ? 1 : (dist > 4.0 * g * 1.000001 ? 0 : dist / g < 4.0);
+        if (rtn < 0 || cw < 0) {               // geo.qdrdist's distance itself
+          const double dist = qdrdist_exact_nm(s.lat, m.wp_lat, x) * NM;
+          if (half <= 45.0 && dist > turnrad * 1.000001) {
+            rtn = 0;
+          } else {
+            const double turndist = fabs(turnrad * tan(half * kD2R));
+            rtn = dist < turndist;
+          }
+          // dist/g < 4, decided without the division outside a 1e-6 band around 4*g
+          cw = dist < 4.0 * g * 0.999999 ? 1 : (dist > 4.0 * g * 1.000001 ? 0 : dist / g < 4.0);
+        }
       }
-      const bool tooclose = cw && (fabs(degto180(pymod(trkv, 360.0) - pymod(qdr, 360.0))) > 90.0);
-      reached = rtn || tooclose;
+      const bool tooclose = cw == 1 && (fabs(degto180(pymod360(trkv) - pymod360(qdr))) > 90.0);
+      reached = rtn == 1 || tooclose;
     }
+    BSG_SUBSTEP_MARK(6);
     if (reached) {
       if (k >= rt.len - 1) {
         s.nav &= ~1;                       // last waypoint: LNAV off, keep commanded track
@@ -404,15 +425,16 @@ __device__ __forceinline__ void substep(AC& s, Memo& m, double dt, const RouteRe
     }
     if (s.nav & 1) s.ap_trk = qdr;
   }
+  BSG_SUBSTEP_MARK(1);
   const double ap_vs = fabs(s.selvs) > 0.1 ? s.selvs : APVSDEF;
   const double ap_alt = s.selalt;
   const uint64_t ab = bits(s.alt);
   m.last_alt = s.alt;
-  if (bits(s.selspd) != m.spd_bits || ab != m.spdalt_bits) {
-    m.ap_tas = casormach2tas_at(s.selspd, memo_at(m, s.alt, ab));
-    m.spd_bits = bits(s.selspd);
-    m.spdalt_bits = ab;
-  }
+  // PerfModel.limits' keys (frozen A320 envelope; phase GD has its own speed range and axmax)
+  const bool gd = ground_phase(s.alt);
+  const double axmax = gd ? AXMAX_GD : AXMAX;
+  const double allow_h = ap_alt > HMAX ? HMAX : ap_alt;
+  const uint64_t hb = bits(allow_h);
   // aporasas
   const double vs_cmd0 = fabs(ap_vs);
   double hdg_cmd;
@@ -422,28 +444,33 @@ __device__ __forceinline__ void substep(AC& s, Memo& m, double dt, const RouteRe
     const double winddir = atan2(vwe, vwn);
     const double drift = s.ap_trk * kD2R - winddir;
     const double steer = asin(npmin(1.0, npmax(-1.0, Vw * sin_t(drift) / npmax(0.001, s.tas))));
-    hdg_cmd = pymod(s.ap_trk + steer * kR2D, 360.0);
+    hdg_cmd = pymod360(s.ap_trk + steer * kR2D);
   } else {
-    hdg_cmd = pymod(s.ap_trk, 360.0);
+    hdg_cmd = pymod360(s.ap_trk);
   }
-  // PerfModel.limits (frozen A320 envelope; phase GD has its own speed range and axmax)
-  const bool gd = ground_phase(s.alt);
-  const double axmax = gd ? AXMAX_GD : AXMAX;
-  const double allow_h = ap_alt > HMAX ? HMAX : ap_alt;
-  const uint64_t hb = bits(allow_h);
-  if (bits(m.ap_tas) != m.lim_tas_bits || hb != m.lim_h_bits || gd != m.lim_gd) {
-    const Atmos ah = (hb == ab) ? memo_at(m, s.alt, ab) : vatmos_limit(allow_h);
-    const double intent_cas = tas2cas_at(m.ap_tas, ah);
-    const double vmin = gd ? 0.0 : VMIN_CAS, vmax = gd ? VMAX_GD : VMAX_CAS;
-    double allow_cas = intent_cas < vmin ? vmin : intent_cas;
-    allow_cas = intent_cas > vmax ? vmax : allow_cas;
-    double allow_tas = cas2tas_at(allow_cas, ah);
-    const double snd_h = sound_at(ah);
-    if (allow_tas / snd_h > MMO) allow_tas = MMO * snd_h;
-    m.allow_tas = allow_tas;
-    m.lim_tas_bits = bits(m.ap_tas);
-    m.lim_h_bits = hb;
-    m.lim_gd = gd;
+  // the speed schedule: one branch for both memos (steady flight hits both)
+  const bool spd_miss = bits(s.selspd) != m.spd_bits || ab != m.spdalt_bits;
+  if (spd_miss || bits(m.ap_tas) != m.lim_tas_bits || hb != m.lim_h_bits || gd != m.lim_gd) {
+    if (spd_miss) {
+      m.ap_tas = casormach2tas_at(s.selspd, memo_at(m, s.alt, ab));
+      m.spd_bits = bits(s.selspd);
+      m.spdalt_bits = ab;
+    }
+    // PerfModel.limits
+    if (bits(m.ap_tas) != m.lim_tas_bits || hb != m.lim_h_bits || gd != m.lim_gd) {
+      const Atmos ah = (hb == ab) ? memo_at(m, s.alt, ab) : vatmos_limit(allow_h);
+      const double intent_cas = tas2cas_at(m.ap_tas, ah);
+      const double vmin = gd ? 0.0 : VMIN_CAS, vmax = gd ? VMAX_GD : VMAX_CAS;
+      double allow_cas = intent_cas < vmin ? vmin : intent_cas;
+      allow_cas = intent_cas > vmax ? vmax : allow_cas;
+      double allow_tas = cas2tas_at(allow_cas, ah);
+      const double snd_h = sound_at(ah);
+      if (allow_tas / snd_h > MMO) allow_tas = MMO * snd_h;
+      m.allow_tas = allow_tas;
+      m.lim_tas_bits = bits(m.ap_tas);
+      m.lim_h_bits = hb;
+      m.lim_gd = gd;
+    }
   }
   const double allow_tas = m.allow_tas;
   // s.ax / axmax with axmax in {0.5, 2}: multiplying by the exact reciprocal is the same
@@ -455,20 +482,18 @@ __device__ __forceinline__ void substep(AC& s, Memo& m, double dt, const RouteRe
   const bool need_ax = fabs(delta_spd) > fabs(dt * axmax);
   s.ax = (double)need_ax * sgn(delta_spd) * axmax;
   s.tas = need_ax ? s.tas + s.ax * dt : allow_tas;
-  const double delhdg = pymod(hdg_cmd - s.hdg + 180.0, 360.0) - 180.0;
+  BSG_SUBSTEP_MARK(2);
+  const double delhdg = pymod360(hdg_cmd - s.hdg + 180.0) - 180.0;
   // |delhdg| > |dt*turnrate| is false at delhdg == 0 whatever turnrate is: a straight
-  // flying aircraft needs no turn rate (and no division)
+  // flying aircraft needs no turn rate (whose division would sit on the tas -> heading ->
+  // position chain)
   bool swhdgsel = false;
   double turnrate = 0.0;
   if (delhdg != 0.0) {
-    if (bits(s.tas) != m.tr_bits) {
-      m.turnrate = (G0 * TAN_BANKDEF / npmax(s.tas, EPS_SPD)) * kR2D;
-      m.tr_bits = bits(s.tas);
-    }
-    turnrate = m.turnrate;
+    turnrate = (G0 * TAN_BANKDEF / npmax(s.tas, EPS_SPD)) * kR2D;
     swhdgsel = fabs(delhdg) > fabs(dt * turnrate);
   }
-  s.hdg = pymod(swhdgsel ? s.hdg + dt * turnrate * sgn(delhdg) : hdg_cmd, 360.0);
+  s.hdg = pymod360(swhdgsel ? s.hdg + dt * turnrate * sgn(delhdg) : hdg_cmd);
   const double delta_alt = allow_h - s.alt;
   const bool swaltsel = fabs(delta_alt) > npmax(10 * FT, fabs(2 * fabs(dt * s.vs)));
   const double target_vs = (double)swaltsel * sgn(delta_alt) * fabs(vs_cmd);
@@ -478,6 +503,7 @@ __device__ __forceinline__ void substep(AC& s, Memo& m, double dt, const RouteRe
   s.vs = need_az ? s.vs + az * dt : target_vs;
   if (!isfinite(s.vs)) s.vs = 0.0;
   // update_groundspeed + update_pos
+  BSG_SUBSTEP_MARK(3);
   if (bits(s.hdg) != m.hdg_bits) {        // straight flight keeps its heading trig
     sincos_t(s.hdg * kD2R, &m.shdg, &m.chdg);
     m.hdg_bits = bits(s.hdg);
@@ -491,7 +517,7 @@ __device__ __forceinline__ void substep(AC& s, Memo& m, double dt, const RouteRe
     gseast = gseast + vwe * (double)applywind;
     if (applywind) {
       s.gs = sqrt(gsnorth * gsnorth + gseast * gseast);
-      s.trk = pymod(atan2(gseast, gsnorth) * kR2D, 360.0);
+      s.trk = pymod360(atan2(gseast, gsnorth) * kR2D);
     } else {
       s.gs = s.tas;
       s.trk = s.hdg;
@@ -499,6 +525,7 @@ __device__ __forceinline__ void substep(AC& s, Memo& m, double dt, const RouteRe
   }
   if (swaltsel) s.alt = divk(rint((s.alt + s.vs * dt) * 1e6), 1e6);   // a branch: level flight
   else s.alt = allow_h;                                            // skips the division
+  BSG_SUBSTEP_MARK(4);
   s.lat = s.lat + divk(dt * gsnorth, Rearth) * kR2D;
   sincos_t(s.lat * kD2R, &m.sinlat, &m.coslat);
   s.lon = s.lon + divk(dt * gseast / m.coslat, Rearth) * kR2D;
@@ -650,10 +677,10 @@ __device__ __forceinline__ CdOut cd_pair(const LT& L, int i, int k) {
   const double lati = L.lat[i], loni = L.lon[i];
   const double latk = L.lat[k], lonk = L.lon[k];
   const double dlat = (latk - lati) * kD2R;
-  const double dlon = (pymod((lonk - loni) + 180.0, 360.0) - 180.0) * kD2R;
+  const double dlon = (pymod360((lonk - loni) + 180.0) - 180.0) * kD2R;
   const double cavelat = cos_t(((lati + latk) * kD2R) * 0.5);
   const double dangle = sqrt(dlat * dlat + (dlon * dlon) * (cavelat * cavelat));
-  const double dist = divk(6371000.0 * dangle, NM) * NM + 0.0;     // + 1e9*I, I = 0
+  const double dist = divk_nn(6371000.0 * dangle, NM) * NM + 0.0;     // + 1e9*I, I = 0
   const double du = cd_u(L, k) - cd_u(L, i);
   const double dv = cd_v(L, k) - cd_v(L, i);
   double dv2 = du * du + dv * dv;
@@ -675,7 +702,7 @@ __device__ __forceinline__ CdOut cd_pair(const LT& L, int i, int k) {
                           toutver, &r))
     return r;
   // undecided by the bounds: the exact StateBased arithmetic
-  const double qdr = pymod(atan2(dlon * cavelat, dlat) * kR2D, 360.0);
+  const double qdr = pymod360(atan2(dlon * cavelat, dlat) * kR2D);
   double sq, cq;
   sincos_t(qdr * kD2R, &sq, &cq);
   const double dx = dist * sq;
@@ -988,10 +1015,10 @@ __device__ __forceinline__ bool lane_obs(const LT& L, int base, int lane, double
   // shared kwik terms: lata + latb == latb + lata bitwise, so cavelat is common to the
   // kwikdist_matrix (merge_env.py:195) and kwikqdrdist (:203) forms
   const double dlat = (latj - lat0) * kD2R;
-  const double dlon = (pymod((lonj - lon0) + 180.0, 360.0) - 180.0) * kD2R;
+  const double dlon = (pymod360((lonj - lon0) + 180.0) - 180.0) * kD2R;
   const double cavelat = cos_t(((lat0 + latj) * kD2R) * 0.5);
-  const double dist = divk(6371000.0 * sqrt(dlat * dlat + dlon * dlon * cavelat * cavelat), NM);
-  const double qdr = pymod(atan2(dlon * cavelat, dlat) * kR2D, 360.0);
+  const double dist = divk_nn(6371000.0 * sqrt(dlat * dlat + dlon * dlon * cavelat * cavelat), NM);
+  const double qdr = pymod360(atan2(dlon * cavelat, dlat) * kR2D);
   if constexpr (KIND == BSG_ENV_MERGE) {
     // merge_env.py:195-218
     // ownship: drift = bound180(hdg - qdr to the waypoint) and its cos/sin (own_obs)
@@ -1003,7 +1030,7 @@ __device__ __forceinline__ bool lane_obs(const LT& L, int base, int lane, double
       *sortkey = __builtin_inf();
       return false;
     }
-    const double dmat = divk(6371000.0 * sqrt(dlat * dlat + (dlon * dlon) * (cavelat * cavelat)), NM);
+    const double dmat = divk_nn(6371000.0 * sqrt(dlat * dlat + (dlon * dlon) * (cavelat * cavelat)), NM);
     const double x_r = (dist * 1.852 * 1000) * cb;
     const double y_r = (dist * 1.852 * 1000) * sb;
     // vx = cos(hdg)*tas == v = tas*cos(hdg) bitwise (LDS staging)

@@ -8,7 +8,7 @@
 #include <cstdio>
 #include <vector>
 
-#include "../../bluesky-gym-hallucination_amd/csrc/bsg_fastmath.h"
+#include "../../bluesky-gym-hallucination_amd/csrc/bsg_device.h"
 
 constexpr int ITER = 2048;
 
@@ -39,6 +39,16 @@ PROBE(k_ocml_atan2, x = atan2(x, a) + b)
 PROBE(k_pow_ocml, x = pow(x * a + 1.0, 3.5) * b)
 PROBE(k_pow_3p5, x = bsg::pow_3p5(x * a + 1.0) * b)
 PROBE(k_cvt_f32, x = (double)(float)x + a)
+PROBE(k_select, x = (x > a) ? x * b : x + b)
+PROBE(k_branch, if (x > a) { x = x * b; } else { x = x + b; })
+PROBE(k_branch_skip, if (x < -1e30) { double sv, cv; sincos(x, &sv, &cv); x = sv * cv; } x = fma(x, a, b))
+PROBE(k_branch_skip2, if (x < -1e30) { double sv, cv; sincos(x, &sv, &cv); x = sv * cv; } x = fma(x, a, b);
+                      if (x < -1e31) { double sv, cv; sincos(x, &sv, &cv); x = sv + cv; } x = fma(x, a, b))
+PROBE(k_pymod360, x = bsg::pymod360(x * 360.0 + a) * (1.0 / 360.0))
+PROBE(k_branch_expect, if (__builtin_expect(x < -1e30, 0)) { double sv, cv; sincos(x, &sv, &cv); x = sv * cv; } x = fma(x, a, b))
+PROBE(k_branch_ballot, if (__builtin_amdgcn_ballot_w64(x < -1e30) != 0) { double sv, cv; sincos(x, &sv, &cv); x = sv * cv; } x = fma(x, a, b))
+PROBE(k_branch_any, if (__any(x < -1e30)) { if (x < -1e30) { double sv, cv; sincos(x, &sv, &cv); x = sv * cv; } } x = fma(x, a, b))
+PROBE(k_cmp_sel2, x = (x > a) ? ((x > b) ? x * a : x + a) : x + b)
 
 int main() {
   std::vector<double> h(66, 0.3);
@@ -56,7 +66,13 @@ int main() {
                   {"sqrt", k_sqrt}, {"rint", k_rint}, {"ocml sincos", k_ocml_sincos},
                   {"sincos_t", k_sincos_t}, {"ocml cos", k_ocml_cos}, {"cos_t", k_cos_t},
                   {"ocml atan2", k_ocml_atan2}, {"ocml pow(., 3.5)", k_pow_ocml},
-                  {"pow_3p5", k_pow_3p5}, {"f64->f32->f64", k_cvt_f32}};
+                  {"pow_3p5", k_pow_3p5}, {"f64->f32->f64", k_cvt_f32},
+                  {"select (cmp + cndmask)", k_select}, {"if/else uniform", k_branch},
+                  {"if (never, heavy) + fma", k_branch_skip}, {"2x (if (never) + fma)", k_branch_skip2},
+                  {"pymod360 (fast path)", k_pymod360},
+                  {"if (expect 0) + fma", k_branch_expect}, {"if (ballot) + fma", k_branch_ballot},
+                  {"if (__any) + fma", k_branch_any},
+                  {"two nested selects", k_cmp_sel2}};
   for (const K& k : ks) {
     long long best = 1LL << 62;
     for (int rep = 0; rep < 5; ++rep) {

@@ -4,10 +4,17 @@
 // path.  State comes from tools/probe/substep_probe.py (a DeviceBatch after 30 steps).
 //   hipcc -O3 -std=c++17 --offload-arch=gfx950 -ffp-contract=off -fno-fast-math \
 //         -mllvm -disable-machine-licm tools/probe/substep_probe.hip -o tools/probe/substep_probe
+// section marks inside substep (bsg_kernels.hip BSG_SUBSTEP_MARK): s_memtime per mark
+__device__ long long g_mark[8];
+#define BSG_SUBSTEP_MARK(i) do { g_mark[i] = __builtin_amdgcn_s_memtime(); } while (0)
 #include "../../bluesky-gym-hallucination_amd/csrc/bsg_kernels.hip"
 
 #include <cstdio>
 #include <vector>
+
+#ifndef PROBE_MODE
+#define PROBE_MODE 0
+#endif
 
 constexpr int NF = 12;       // lat lon alt hdg tas cas vs ax ap_trk selspd selalt selvs, + nav
 constexpr int SMAX = 16;
@@ -21,6 +28,12 @@ __global__ void probe(bsg::Route route, const double* st, int S, long long* cyc,
   for (int k = 0; k < NF; ++k) *f[k] = st[k * 64 + l];
   s.nav = (int)st[NF * 64 + l];
   s.gs = s.tas; s.trk = s.hdg;
+#if PROBE_MODE >= 1
+  s.nav = 0;                 // LNAV off: the substep without the waypoint bearing
+#endif
+#if PROBE_MODE >= 2
+  s.ap_trk = s.hdg;          // and no heading change: heading trig memo hits
+#endif
   Memo m;
   memo_init(m, s);
   RouteRegs rt;
@@ -28,10 +41,15 @@ __global__ void probe(bsg::Route route, const double* st, int S, long long* cyc,
   WindDev w{};
   long long t[SMAX + 1];
   t[0] = __builtin_amdgcn_s_memtime();
+  long long mk[SMAX][8];
   for (int it = 0; it < S; ++it) {
     substep<false>(s, m, 5.0, rt, w);
     t[it + 1] = __builtin_amdgcn_s_memtime();
+    for (int q = 0; q < 8; ++q) mk[it][q] = g_mark[q];
   }
+  if (l == 0)
+    for (int it = 0; it < S; ++it)
+      for (int q = 0; q < 8; ++q) cyc[SMAX + it * 8 + q] = mk[it][q] - t[it];
   if (l == 0)
     for (int it = 0; it < S; ++it) cyc[it] = t[it + 1] - t[it];
   for (int k = 0; k < NF; ++k) out[k * 64 + l] = *f[k];
@@ -54,7 +72,7 @@ int main(int argc, char** argv) {
   double *dst, *dout;
   long long* dcyc;
   if (hipMalloc(&dst, st.size() * 8) != hipSuccess || hipMalloc(&dout, NF * 64 * 8) != hipSuccess ||
-      hipMalloc(&dcyc, SMAX * 8) != hipSuccess) return 1;
+      hipMalloc(&dcyc, (SMAX + SMAX * 8) * 8) != hipSuccess) return 1;
   (void)hipMemcpy(dst, st.data(), st.size() * 8, hipMemcpyHostToDevice);
   const int S = 10;
   std::vector<long long> best(S, 1LL << 62);
@@ -63,6 +81,18 @@ int main(int argc, char** argv) {
     std::vector<long long> c(S);
     (void)hipMemcpy(c.data(), dcyc, S * 8, hipMemcpyDeviceToHost);
     for (int i = 0; i < S; ++i) best[i] = c[i] < best[i] ? c[i] : best[i];
+  }
+  {
+    std::vector<long long> c(SMAX + SMAX * 8);
+    (void)hipMemcpy(c.data(), dcyc, c.size() * 8, hipMemcpyDeviceToHost);
+    std::printf("section marks (cycles from substep start; 5 after qdr_x, 6 after the near-waypoint\n"
+                "block, 1 after LNAV, 2 after speed/limits, 3 after the turn, 4 after the heading trig):\n");
+    for (int it = 0; it < S; ++it) {
+      std::printf("  substep %d:", it);
+      const int order[6] = {5, 6, 1, 2, 3, 4};
+      for (int q : order) std::printf(" m%d=%lld", q, c[SMAX + it * 8 + q]);
+      std::printf("\n");
+    }
   }
   long long tot = 0;
   std::printf("substep cycles (one wave, min of 7):");
