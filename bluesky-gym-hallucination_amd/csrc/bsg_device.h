@@ -79,6 +79,22 @@ __device__ __forceinline__ double npmin(double a, double b) { return (a <= b || 
 
 __device__ __forceinline__ double degto180(double a) { return pymod360(a + 180.0) - 180.0; }
 
+// pymod360 where the caller proves the argument's range (or NaN), without the branch
+// (~150 -> 31 / 94 cycles of latency, tools/probe/latency_probe.hip):
+//  - pymod360_s: a in [-360, 360) -- e.g. atan2(..) * R2D, |a| <= 180 + 1 ulp: the fast
+//    path above as one select;
+//  - pymod360_r: a in [-360, 720) -- e.g. a difference of two [0, 360] angles + 180:
+//    a >= 360 has fmod(a, 360) = a - 360 exactly (Sterbenz: 360 <= a < 2 * 360).
+__device__ __forceinline__ double pymod360_s(double a) { return a < 0.0 ? a + 360.0 : a + 0.0; }
+__device__ __forceinline__ double pymod360_r(double a) {
+  const double lo = a + 360.0, hi = a - 360.0;
+  return a < 0.0 ? lo : (a >= 360.0 ? hi : a + 0.0);
+}
+// degto180(p - q) for p, q in [0, 360]: the argument p - q + 180 is in [-180, 540]
+__device__ __forceinline__ double degto180_pq(double p, double q) {
+  return pymod360_r((p - q) + 180.0) - 180.0;
+}
+
 // functions.py:4-22 bound_angle_positive_negative_180 (single wrap)
 __device__ __forceinline__ double bound180(double a) {
   return a > 180.0 ? -(360.0 - a) : (a < -180.0 ? 360.0 + a : a);
@@ -94,7 +110,7 @@ __device__ __forceinline__ Atmos vatmos(double h) {
   const double dhstrat = npmax(0.0, h - 11000.0);
   // one branch: the troposphere at h >= 0 (T/288.15 in the polynomial's range, and
   // exp(-0.0) == 1 exactly) is every altitude the envs fly but the HMAX ceiling, whose
-  // atmosphere is a constant (vatmos_limit)
+  // atmosphere is a constant (kAtmosHMAX_K)
   double rho = 1.225 * poly_trop(x);
   if (!(in_trop(x) && dhstrat == 0.0))
     rho = 1.225 * pow_trop(x) * (dhstrat > 0.0 ? exp(divk(-dhstrat, 6341.552161)) : 1.0);
@@ -109,11 +125,18 @@ __device__ __forceinline__ Atmos vatmos(double h) {
 constexpr Atmos kAtmosHMAX = {0x1.27c7249336b51p+14, 0x1.37b10b426ceafp-2, 0x1.b14cccccccccdp+7};
 constexpr Atmos kAtmosSL = {0x1.8bccff9dc0a57p+16, 0x1.399999999999ap+0, 0x1.2026666666666p+8};
 
-__device__ __forceinline__ Atmos vatmos_limit(double h) {
-  if (bits(h) == bits(HMAX)) return kAtmosHMAX;
-  if (h == 0.0) return kAtmosSL;
-  return vatmos(h);
-}
+// The same two atmospheres with what the CAS/TAS/Mach conversions of PerfModel.limits
+// divide by and its RN reciprocal (host-computed: RN(7p), RN(1/RN(7p)), RN(1/p),
+// RN(RN(7p)/rho), sqrt(GAMMA*RGAS*T) correctly rounded, RN(1/snd)), so that those
+// divisions are Markstein's 3-link form (~17 instead of ~74 cycles each on the chain;
+// tools/fastmath/ulp_check.cpp verifies each divisor against '/').
+struct AtmosK { Atmos a; double p7, r_p7, r_p, k7, snd, r_snd; };
+constexpr AtmosK kAtmosHMAX_K = {kAtmosHMAX, 0x1.02ce4000cfde7p+17, 0x1.fa7312a359f5cp-18,
+                                 0x1.bb24b04eeeb71p-15, 0x1.a92081eb7ed42p+18,
+                                 0x1.2711ca539cbf1p+8, 0x1.bc350c7fc3a97p-9};
+constexpr AtmosK kAtmosSL_K = {kAtmosSL, 0x1.5a535faa0890cp+19, 0x1.7a76ee408d549p-20,
+                               0x1.4b2810787baa0p-17, 0x1.1ab6ffb9d2bf5p+19,
+                               0x1.544b42cc9d77cp+8, 0x1.812c3ee51ffb9p-9};
 
 // vtas2cas / vcas2tas: both powers by polynomial with one range test for the pair (a
 // branch is ~80 cycles of latency even when not taken); outside, both by the libm.
@@ -147,6 +170,36 @@ __device__ __forceinline__ double cas2tas_at(double cas, const Atmos& a) {
 
 __device__ __forceinline__ double sound_at(const Atmos& a) { return sqrt(GAMMA * RGAS * a.T); }
 
+// tas2cas_at / cas2tas_at at a constant limit atmosphere (same operations, the divisions
+// by the precomputed divisors; numerators rho*tas^2 and qdyn are >= 0 or +0)
+__device__ __forceinline__ double tas2cas_k(double tas, const AtmosK& k) {
+  const double z = 1.0 + div_r_nn(k.a.rho * tas * tas, k.p7, k.r_p7);
+  double qdyn = k.a.p * (poly_3p5(z) - 1.0);
+  double y = divk_nn(qdyn, P0) + 1.0;
+  double yp = poly_2o7(y);
+  if (!(in_3p5(z) && in_2o7(y))) {
+    qdyn = k.a.p * (pow(z, 3.5) - 1.0);
+    y = divk(qdyn, P0) + 1.0;
+    yp = pow(y, 2.0 / 7.0);
+  }
+  const double cas = sqrt(7.0 * P0 / RHO0 * (yp - 1.0));
+  return tas < 0 ? -1 * cas : cas;
+}
+
+__device__ __forceinline__ double cas2tas_k(double cas, const AtmosK& k) {
+  const double z = 1.0 + divk_nn(RHO0 * cas * cas, 7.0 * P0);
+  double qdyn = P0 * (poly_3p5(z) - 1.0);
+  double y = 1.0 + div_r_nn(qdyn, k.a.p, k.r_p);
+  double yp = poly_2o7(y);
+  if (!(in_3p5(z) && in_2o7(y))) {
+    qdyn = P0 * (pow(z, 3.5) - 1.0);
+    y = 1.0 + qdyn / k.a.p;
+    yp = pow(y, 2.0 / 7.0);
+  }
+  const double tas = sqrt(k.k7 * (yp - 1.0));
+  return cas < 0 ? -1 * tas : tas;
+}
+
 // vcasormach2tas: |spd| < 2 -> Mach, else CAS
 __device__ __forceinline__ double casormach2tas_at(double spd, const Atmos& a) {
   return fabs(spd) < 2.0 ? spd * sound_at(a) : cas2tas_at(spd, a);
@@ -173,7 +226,7 @@ __device__ __forceinline__ void kwikqdrdist(double lata, double lona, double lat
   double cavelat = cos_t(((lata + latb) * kD2R) * 0.5);
   double dangle = sqrt(dlat * dlat + dlon * dlon * cavelat * cavelat);
   *dist = divk_nn(6371000.0 * dangle, NM);
-  *qdr = pymod360(atan2(dlon * cavelat, dlat) * kR2D);
+  *qdr = pymod360_s(atan2(dlon * cavelat, dlat) * kR2D);
 }
 
 __device__ __forceinline__ double kwikdist(double lata, double lona, double latb, double lonb) {
@@ -201,7 +254,7 @@ __device__ __forceinline__ void kwikqdrdist_mat(double lata, double lona, double
   double cavelat = cos_t(((lata + latb) * kD2R) * 0.5);
   double dangle = sqrt(dlat * dlat + (dlon * dlon) * (cavelat * cavelat));
   *dist = divk_nn(6371000.0 * dangle, NM);
-  *qdr = pymod360(atan2(dlon * cavelat, dlat) * kR2D);
+  *qdr = pymod360_s(atan2(dlon * cavelat, dlat) * kR2D);
 }
 
 __device__ __forceinline__ void kwikpos(double latd1, double lond1, double qdr, double dist,

@@ -107,11 +107,11 @@ __host__ __device__ __forceinline__ double divk(double x, double y) { return div
 // the same for a finite numerator whose zero, if any, is +0 (every physically non-negative
 // quantity: temperatures, squared speeds, dynamic pressures, distances): the guard's
 // compare/select pair is half the latency of the division itself
-__host__ __device__ __forceinline__ double divk_nn(double x, double y) {
-  const double ry = 1.0 / y;
+__host__ __device__ __forceinline__ double div_r_nn(double x, double y, double ry) {
   const double q = x * ry;
   return fma(fma(-q, y, x), ry, q);
 }
+__host__ __device__ __forceinline__ double divk_nn(double x, double y) { return div_r_nn(x, y, 1.0 / y); }
 
 // ---- sin / cos ------------------------------------------------------------------------
 // The device libm's sincos spends ~75 VALU on its small-argument path (3-part

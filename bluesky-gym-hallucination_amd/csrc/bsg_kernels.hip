@@ -171,7 +171,7 @@ __device__ __forceinline__ double hdg_command_track(const WindDev& w, const AC& 
       double sh, ch;
       sincos_t(hdg * kD2R, &sh, &ch);
       const double tasnorth = s.tas * ch, taseast = s.tas * sh;
-      return pymod360(atan2(taseast + we, tasnorth + wn) * kR2D);
+      return pymod360_s(atan2(taseast + we, tasnorth + wn) * kR2D);
     }
   }
   return hdg;
@@ -208,7 +208,7 @@ struct Memo {
   bool lim_gd;                         //   (and its flight phase: GD or airborne)
   double allow_tas;
   int wp_k;                        // cached waypoint (coords, next-leg bearing, trig)
-  double wp_lat, wp_lon, wp_nq, wp_cos, wp_sin, wp_rw;
+  double wp_lat, wp_lon, wp_nq, wp_cos, wp_sin, wp_rw, wp_pnq;   // wp_pnq = pymod360(wp_nq)
   double coslat, sinlat;           // cos/sin(lat * D2R) of the current latitude
   uint64_t hdg_bits;               // key of (shdg, chdg) = sincos(hdg * D2R)
   double shdg, chdg;
@@ -249,6 +249,7 @@ __device__ __forceinline__ void memo_init(Memo& m, const AC& s) {
   m.lim_tas_bits = kNoKey; m.lim_h_bits = kNoKey; m.lim_gd = false;
   m.at = Atmos{0, 0, 0}; m.ap_tas = 0; m.allow_tas = 0;
   m.wp_k = -1; m.wp_lat = 0; m.wp_lon = 0; m.wp_nq = 0; m.wp_cos = 0; m.wp_sin = 0; m.wp_rw = 0;
+  m.wp_pnq = 0;
   m.hdg_bits = kNoKey; m.shdg = 0; m.chdg = 0;
   m.rad_bits = kNoKey; m.turnrad = 0;
   m.last_alt = s.alt;
@@ -321,6 +322,7 @@ __device__ __forceinline__ void memo_final_cas(Memo& m, AC& s) {
 __device__ __forceinline__ void memo_wp(Memo& m, const RouteRegs& rt, int k) {
   m.wp_k = k;
   rt.get(k, &m.wp_lat, &m.wp_lon, &m.wp_nq, &m.wp_rw);
+  m.wp_pnq = pymod360(m.wp_nq);
   sincos_t(m.wp_lat * kD2R, &m.wp_sin, &m.wp_cos);
 }
 
@@ -356,8 +358,10 @@ __device__ __forceinline__ void substep(AC& s, Memo& m, double dt, const RouteRe
     const bool far = qdr_x(s.lat, s.lon, m.coslat, m.sinlat, m.wp_lat, m.wp_lon, m.wp_cos,
                            m.wp_sin, far_m, &qdr, &x);
     BSG_SUBSTEP_MARK(5);
-    const double next_qdr = m.wp_nq < -900.0 ? qdr : m.wp_nq;
-    const double half = 0.5 * fabs(degto180(pymod360(qdr) - pymod360(next_qdr)));
+    // pymod360 of the bearing (atan2 * R2D: one select) and of the leg's next bearing
+    // (memo_wp); half = 0.5 |degto180(.)| of their difference (two selects)
+    const double pq = pymod360_s(qdr);
+    const double half = 0.5 * fabs(degto180_pq(pq, m.wp_nq < -900.0 ? pq : m.wp_pnq));
     // far and half <= 45: dist > far_m > turnrad >= turndist and dist > 4|gs|: not reached.
     // Otherwise ActiveWaypoint.reached needs only `dist < turndist` and `dist/g < 4`: each
     // is decided from squared bounds on the distance the exact path would compute
@@ -408,7 +412,7 @@ __device__ __forceinline__ void substep(AC& s, Memo& m, double dt, const RouteRe
           cw = dist < 4.0 * g * 0.999999 ? 1 : (dist > 4.0 * g * 1.000001 ? 0 : dist / g < 4.0);
         }
       }
-      const bool tooclose = cw == 1 && (fabs(degto180(pymod360(trkv) - pymod360(qdr))) > 90.0);
+      const bool tooclose = cw == 1 && (fabs(degto180_pq(pymod360(trkv), pq)) > 90.0);
       reached = rtn == 1 || tooclose;
     }
     BSG_SUBSTEP_MARK(6);
@@ -458,14 +462,27 @@ __device__ __forceinline__ void substep(AC& s, Memo& m, double dt, const RouteRe
     }
     // PerfModel.limits
     if (bits(m.ap_tas) != m.lim_tas_bits || hb != m.lim_h_bits || gd != m.lim_gd) {
-      const Atmos ah = (hb == ab) ? memo_at(m, s.alt, ab) : vatmos_limit(allow_h);
-      const double intent_cas = tas2cas_at(m.ap_tas, ah);
       const double vmin = gd ? 0.0 : VMIN_CAS, vmax = gd ? VMAX_GD : VMAX_CAS;
-      double allow_cas = intent_cas < vmin ? vmin : intent_cas;
-      allow_cas = intent_cas > vmax ? vmax : allow_cas;
-      double allow_tas = cas2tas_at(allow_cas, ah);
-      const double snd_h = sound_at(ah);
-      if (allow_tas / snd_h > MMO) allow_tas = MMO * snd_h;
+      double allow_tas;
+      const bool khi = bits(allow_h) == bits(HMAX);
+      if (hb != ab && (khi || allow_h == 0.0)) {
+        // the Vertical/Descent commands (selalt 1e6 or 0): a constant atmosphere whose
+        // divisors have precomputed reciprocals
+        const AtmosK& k = khi ? kAtmosHMAX_K : kAtmosSL_K;
+        const double intent_cas = tas2cas_k(m.ap_tas, k);
+        double allow_cas = intent_cas < vmin ? vmin : intent_cas;
+        allow_cas = intent_cas > vmax ? vmax : allow_cas;
+        allow_tas = cas2tas_k(allow_cas, k);
+        if (div_r_nn(allow_tas, k.snd, k.r_snd) > MMO) allow_tas = MMO * k.snd;   // allow_tas >= 0
+      } else {
+        const Atmos ah = (hb == ab) ? memo_at(m, s.alt, ab) : vatmos(allow_h);
+        const double intent_cas = tas2cas_at(m.ap_tas, ah);
+        double allow_cas = intent_cas < vmin ? vmin : intent_cas;
+        allow_cas = intent_cas > vmax ? vmax : allow_cas;
+        allow_tas = cas2tas_at(allow_cas, ah);
+        const double snd_h = sound_at(ah);
+        if (allow_tas / snd_h > MMO) allow_tas = MMO * snd_h;
+      }
       m.allow_tas = allow_tas;
       m.lim_tas_bits = bits(m.ap_tas);
       m.lim_h_bits = hb;
@@ -517,7 +534,7 @@ __device__ __forceinline__ void substep(AC& s, Memo& m, double dt, const RouteRe
     gseast = gseast + vwe * (double)applywind;
     if (applywind) {
       s.gs = sqrt(gsnorth * gsnorth + gseast * gseast);
-      s.trk = pymod360(atan2(gseast, gsnorth) * kR2D);
+      s.trk = pymod360_s(atan2(gseast, gsnorth) * kR2D);
     } else {
       s.gs = s.tas;
       s.trk = s.hdg;
@@ -702,7 +719,7 @@ __device__ __forceinline__ CdOut cd_pair(const LT& L, int i, int k) {
                           toutver, &r))
     return r;
   // undecided by the bounds: the exact StateBased arithmetic
-  const double qdr = pymod360(atan2(dlon * cavelat, dlat) * kR2D);
+  const double qdr = pymod360_s(atan2(dlon * cavelat, dlat) * kR2D);
   double sq, cq;
   sincos_t(qdr * kD2R, &sq, &cq);
   const double dx = dist * sq;
@@ -1018,7 +1035,7 @@ __device__ __forceinline__ bool lane_obs(const LT& L, int base, int lane, double
   const double dlon = (pymod360((lonj - lon0) + 180.0) - 180.0) * kD2R;
   const double cavelat = cos_t(((lat0 + latj) * kD2R) * 0.5);
   const double dist = divk_nn(6371000.0 * sqrt(dlat * dlat + dlon * dlon * cavelat * cavelat), NM);
-  const double qdr = pymod360(atan2(dlon * cavelat, dlat) * kR2D);
+  const double qdr = pymod360_s(atan2(dlon * cavelat, dlat) * kR2D);
   if constexpr (KIND == BSG_ENV_MERGE) {
     // merge_env.py:195-218
     // ownship: drift = bound180(hdg - qdr to the waypoint) and its cos/sin (own_obs)

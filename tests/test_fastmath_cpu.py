@@ -57,3 +57,17 @@ def test_constant_atmospheres_are_the_oracle_vatmos():
         got = [float.fromhex(v.strip()) for v in lits]
         want = [float(v) for v in bs.vatmos(np.float64(h))]
         assert got == want, (name, got, want)
+
+
+def test_constant_atmosphere_divisors():
+    """kAtmos*_K: the divisors PerfModel.limits' conversions use at the two constant
+    atmospheres and their RN reciprocals (bsg_device.h AtmosK), as the host computes them."""
+    txt = open(os.path.join(CSRC, "bsg_device.h")).read()
+    for name, h in (("kAtmosHMAX_K", bs.HMAX), ("kAtmosSL_K", 0.0)):
+        body = re.search(rf"constexpr AtmosK {name} = \{{(\w+),([^}}]+)\}};", txt, re.S)
+        got = [float.fromhex(v.strip()) for v in body.group(2).split(",")]
+        p, rho, T = (float(v) for v in bs.vatmos(np.float64(h)))
+        p7 = 7.0 * p
+        snd = float(np.sqrt(1.4 * 287.05287 * T))
+        want = [p7, 1.0 / p7, 1.0 / p, p7 / rho, snd, 1.0 / snd]
+        assert got == want, (name, got, want)

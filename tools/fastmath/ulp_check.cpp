@@ -50,7 +50,10 @@ static void run(const char* name, double lo, double hi, long double c, double cd
 static void div_check() {
   const double ys[] = {288.15, 709275.0, 101325.0, 6371000.0, 1e6, 0.3048, 1852.0, 150.0, 250.0,
                        1000000.0, 3000.0, 200.0, 1000.0, 13000.0, 15000.0, 32.0, 66.0, 6.0, 170.0,
-                       75.0, 50.0, 5.0, 12.5, 6341.552161, 0.4663076581549986 * 9.80665};
+                       75.0, 50.0, 5.0, 12.5, 6341.552161, 0.4663076581549986 * 9.80665,
+                       // AtmosK (bsg_device.h): 7p, p, sound speed at HMAX and sea level
+                       0x1.02ce4000cfde7p+17, 0x1.27c7249336b51p+14, 0x1.2711ca539cbf1p+8,
+                       0x1.5a535faa0890cp+19, 0x1.8bccff9dc0a57p+16, 0x1.544b42cc9d77cp+8};
   std::mt19937_64 rng(7);
   for (double y : ys) {
     const double ry = 1.0 / y;
