@@ -315,22 +315,25 @@ __device__ __forceinline__ bool b_times_dphi_far(double latd1, double latd2, dou
 }
 
 // First half of geo.qdrdist for the LNAV loop: the bearing (exact, as qdrdist) and the
-// acos argument x of its distance.  Returns true when the distance is provably beyond
-// `far_m` (then the caller needs no more of it):
-//  - the meridian gap alone: great-circle >= r*|dphi|, r >= b (1e-6 relative margin);
-//  - the computed x itself: with t = far_m/b, x < 1 - t^2/2 <= cos(t) gives acos(x) > t,
-//    so d >= b*t = far_m (the 1e-12 margin covers acos's ulp error; the caller's
-//    thresholds sit >= 1 m inside far_m).  x is bit-identical to the argument the full
-//    path passes to acos.
-__device__ __forceinline__ bool qdr_x(double latd1, double lond1, double coslat1, double sinlat1,
+// acos argument x of its distance (bit-identical to the argument the full path passes to
+// acos).
+__device__ __forceinline__ void qdr_x(double latd1, double lond1, double coslat1, double sinlat1,
                                       double latd2, double lond2, double coslat2, double sinlat2,
-                                      double far_m, double* qdr, double* x) {
+                                      double* qdr, double* x) {
   double sdl, cdl;
   sincos_t(lond2 * kD2R - lond1 * kD2R, &sdl, &cdl);
   *qdr = atan2(sdl * coslat2, coslat1 * sinlat2 - sinlat1 * coslat2 * cdl) * kR2D;
   *x = coslat1 * coslat2 * cdl + sinlat1 * sinlat2;
+}
+
+// true when the distance qdrdist would compute from x is provably beyond far_m:
+//  - the meridian gap alone: great-circle >= r*|dphi|, r >= b (1e-6 relative margin);
+//  - x itself: with t = far_m/b, x < 1 - t^2/2 <= cos(t) gives acos(x) > t, so
+//    d >= b*t = far_m (the 1e-12 margin covers acos's ulp error; the caller's thresholds
+//    sit >= 1 m inside far_m).
+__device__ __forceinline__ bool far_of(double latd1, double latd2, double x, double far_m) {
   const double t = far_m * (1.0 / 6356752.314245);
-  return b_times_dphi_far(latd1, latd2, far_m) || *x < (1.0 - 0.5 * t * t) - 1e-12;
+  return b_times_dphi_far(latd1, latd2, far_m) || x < (1.0 - 0.5 * t * t) - 1e-12;
 }
 
 // Second half: the distance (NM) exactly as geo.qdrdist computes it from the same x.

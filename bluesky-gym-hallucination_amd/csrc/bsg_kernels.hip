@@ -353,23 +353,29 @@ __device__ __forceinline__ void substep(AC& s, Memo& m, double dt, const RouteRe
       m.rad_bits = bits(s.tas);
     }
     const double turnrad = m.turnrad;
-    const double far_m = npmax(turnrad, 4.0 * fabs(gsv)) * 1.000001 + 1.0;
     double qdr, x;
-    const bool far = qdr_x(s.lat, s.lon, m.coslat, m.sinlat, m.wp_lat, m.wp_lon, m.wp_cos,
-                           m.wp_sin, far_m, &qdr, &x);
+    qdr_x(s.lat, s.lon, m.coslat, m.sinlat, m.wp_lat, m.wp_lon, m.wp_cos, m.wp_sin, &qdr, &x);
     BSG_SUBSTEP_MARK(5);
     // pymod360 of the bearing (atan2 * R2D: one select) and of the leg's next bearing
     // (memo_wp); half = 0.5 |degto180(.)| of their difference (two selects)
     const double pq = pymod360_s(qdr);
     const double half = 0.5 * fabs(degto180_pq(pq, m.wp_nq < -900.0 ? pq : m.wp_pnq));
-    // far and half <= 45: dist > far_m > turnrad >= turndist and dist > 4|gs|: not reached.
-    // Otherwise ActiveWaypoint.reached needs only `dist < turndist` and `dist/g < 4`: each
-    // is decided from squared bounds on the distance the exact path would compute
-    // (qdrdist_bounds2: no sqrt / acos / sincos / division) and the WGS84 radius and acos
-    // are evaluated only when a bound straddles a threshold.  Every threshold is >= 0, so
-    // comparing squares compares the values; the 1e-14 factors cover the squares'
-    // rounding.  (Making this block straight-line for every lane -- selects instead of the
-    // branch -- measured ~170 cycles slower per substep: tools/probe/substep_probe.hip.)
+    const double h = half * kD2R;
+    // ActiveWaypoint.reached is `dist < turndist` or (`dist/g < 4` and the waypoint behind),
+    // turndist = |turnrad tan(half)|.  For half <= 45 deg, tan(h) <= 4h/pi (chord of the
+    // convex tan on [0, pi/4]), so beyond far_m = max(turnrad min(1, 4h/pi), 4|gs|) (with a
+    // 1e-6 relative + 1 m margin) the waypoint is not reached.  On a straight continuation
+    // (the last waypoint: half = 0) that radius is 4|gs| instead of the turn radius, so
+    // most substeps of a wave skip the block below.
+    const double far_m = npmax(turnrad * npmin(1.0, h * (4.0 / kPi)), 4.0 * fabs(gsv)) * 1.000001 + 1.0;
+    const bool far = far_of(s.lat, m.wp_lat, x, far_m);
+    // Otherwise the two comparisons are each decided from squared bounds on the distance
+    // the exact path would compute (qdrdist_bounds2: no sqrt / acos / sincos / division) and
+    // the WGS84 radius and acos are evaluated only when a bound straddles a threshold.
+    // Every threshold is >= 0, so comparing squares compares the values; the 1e-14 factors
+    // cover the squares' rounding.  (Making this block straight-line for every lane --
+    // selects instead of the branch -- measured ~170 cycles slower per substep:
+    // tools/probe/substep_probe.hip.)
     const bool need = !far || half > 45.0;
     bool reached = false;
     if (need) {
@@ -379,7 +385,6 @@ __device__ __forceinline__ void substep(AC& s, Memo& m, double dt, const RouteRe
       const double trm = turnrad * 1.000001;
       // turndist = |turnrad * tan(half)| bounded without the tan: the Taylor lower bound tl and
       // the Becker-Stark upper bound pi^2 h / (pi^2 - 4 h^2), cross-multiplied (no division)
-      const double h = half * kD2R;
       const double h2 = h * h;
       const double tl = (h + h * h2 * (1.0 / 3.0 + h2 * (2.0 / 15.0 + h2 * (17.0 / 315.0)))) * (1.0 - 1e-12);
       const double pi2 = 9.869604401089358;
@@ -424,7 +429,7 @@ __device__ __forceinline__ void substep(AC& s, Memo& m, double dt, const RouteRe
         s.nav = (k << 8) | 1;
         memo_wp(m, rt, k);
         qdr_x(s.lat, s.lon, m.coslat, m.sinlat, m.wp_lat, m.wp_lon, m.wp_cos, m.wp_sin,
-              0.0, &qdr, &x);              // only the bearing to the new waypoint is used
+              &qdr, &x);                   // only the bearing to the new waypoint is used
       }
     }
     if (s.nav & 1) s.ap_trk = qdr;
