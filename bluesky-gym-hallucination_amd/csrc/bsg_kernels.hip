@@ -639,8 +639,10 @@ __device__ __forceinline__ bool cd_candidate_f(float dlat, float dl, float x, fl
   const float xu = x + 2e-7f;
   const float c = fmaxf(1.0f - 0.5f * xu * xu - 1e-6f, 0.0f);
   const float y = dlon_lb * c;
-  const float a = 6371000.0f * __fsqrt_rn(dlat_lb * dlat_lb + y * y) * (1.0f - 1e-5f) - 20.0f;
-  const float hor = (9260.0f + 300.0f * (__fsqrt_rn(dv2) * (1.0f + 1e-5f) + 2e-3f)) * (1.0f + 1e-6f) + 2.0f;
+  // v_sqrt_f32 (<= 1 ulp, one instruction; __fsqrt_rn's correctly rounded refinement is
+  // ~10): its error is covered by the 2e-7 added to each relative margin
+  const float a = 6371000.0f * __builtin_amdgcn_sqrtf(dlat_lb * dlat_lb + y * y) * (1.0f - 1.02e-5f) - 20.0f;
+  const float hor = (9260.0f + 300.0f * (__builtin_amdgcn_sqrtf(dv2) * (1.0f + 1.02e-5f) + 2e-3f)) * (1.0f + 1e-6f) + 2.0f;
   return !(a > hor);
 }
 
@@ -1691,15 +1693,17 @@ __global__ __launch_bounds__(64) void step_kernel(KParams p) {
     __syncthreads();
     cand |= L.lm[lane];
     L.lm[lane] = 0ull;
+    // exclusive prefix sum of the per-lane counts (< 64) from one ballot per bit: each
+    // lane counts the set bits below it (mbcnt), no cross-lane data movement
     const int cnt = __popcll(cand);
-    int incl = cnt;
+    int pos = 0, total = 0;
 #pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-      const int t = __shfl_up(incl, off, 64);
-      if (lane >= off) incl += t;
+    for (int bit = 0; bit < 7; ++bit) {
+      const uint64_t bm = __ballot((cnt >> bit) & 1);
+      pos += (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32),
+                                            __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u)) << bit;
+      total += __popcll(bm) << bit;
     }
-    const int total = __shfl(incl, 63, 64);
-    int pos = incl - cnt;
     for (uint64_t c = cand; c; c &= c - 1) {
       const int k = __builtin_ctzll(c);
       cd_list[pos++] = (unsigned short)((lane << 6) | (base + k));

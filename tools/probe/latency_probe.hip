@@ -49,17 +49,33 @@ PROBE(k_branch_expect, if (__builtin_expect(x < -1e30, 0)) { double sv, cv; sinc
 PROBE(k_branch_ballot, if (__builtin_amdgcn_ballot_w64(x < -1e30) != 0) { double sv, cv; sincos(x, &sv, &cv); x = sv * cv; } x = fma(x, a, b))
 PROBE(k_branch_any, if (__any(x < -1e30)) { if (x < -1e30) { double sv, cv; sincos(x, &sv, &cv); x = sv * cv; } } x = fma(x, a, b))
 PROBE(k_cmp_sel2, x = (x > a) ? ((x > b) ? x * a : x + a) : x + b)
+PROBE(k_pymod360_s, x = bsg::pymod360_s(x * 360.0 - a) * (1.0 / 360.0))
+PROBE(k_pymod360_r, x = bsg::pymod360_r(x * 360.0 + a) * (1.0 / 360.0))
+// a wave-uniform flag computed before the loop (an SGPR): the branch needs no VALU result
+__global__ void k_branch_uniform(const double* in, double* out, long long* cyc) {
+  double x = in[threadIdx.x], a = in[64], b = in[65];
+  const bool u = __builtin_amdgcn_readfirstlane(in[66] > 0.5 ? 1 : 0) != 0;
+  const long long t0 = __builtin_amdgcn_s_memtime();
+  for (int i = 0; i < ITER; ++i) {
+    if (u) { double sv, cv; sincos(x, &sv, &cv); x = sv * cv; }
+    x = fma(x, a, b);
+  }
+  const long long t1 = __builtin_amdgcn_s_memtime();
+  out[threadIdx.x] = x;
+  if (threadIdx.x == 0) cyc[0] = t1 - t0;
+}
 
 int main() {
-  std::vector<double> h(66, 0.3);
+  std::vector<double> h(67, 0.3);
   h[64] = 0.999;
   h[65] = 1e-3;
+  h[66] = 0.0;
   double *din, *dout;
   long long* dc;
-  if (hipMalloc(&din, 66 * 8) != hipSuccess || hipMalloc(&dout, 64 * 8) != hipSuccess ||
+  if (hipMalloc(&din, 67 * 8) != hipSuccess || hipMalloc(&dout, 64 * 8) != hipSuccess ||
       hipMalloc(&dc, 8) != hipSuccess)
     return 1;
-  (void)hipMemcpy(din, h.data(), 66 * 8, hipMemcpyHostToDevice);
+  (void)hipMemcpy(din, h.data(), 67 * 8, hipMemcpyHostToDevice);
   struct K { const char* n; void (*f)(const double*, double*, long long*); };
   const K ks[] = {{"loop (x + 0)", k_empty}, {"fma f64", k_fma}, {"mul f64", k_mul},
                   {"add f64", k_add}, {"a / x (IEEE div)", k_div}, {"divk (Markstein)", k_divk},
@@ -72,7 +88,9 @@ int main() {
                   {"pymod360 (fast path)", k_pymod360},
                   {"if (expect 0) + fma", k_branch_expect}, {"if (ballot) + fma", k_branch_ballot},
                   {"if (__any) + fma", k_branch_any},
-                  {"two nested selects", k_cmp_sel2}};
+                  {"two nested selects", k_cmp_sel2},
+                  {"pymod360_s (1 select)", k_pymod360_s}, {"pymod360_r (2 selects)", k_pymod360_r},
+                  {"if (uniform SGPR) + fma", k_branch_uniform}};
   for (const K& k : ks) {
     long long best = 1LL << 62;
     for (int rep = 0; rep < 5; ++rep) {
