@@ -694,28 +694,19 @@ __device__ __forceinline__ bool cd_conflict_bounded(double dist, double dlat, do
   return false;
 }
 
-// exact StateBased terms of pair (i, k) (i != k), oracle operation order
-template <class LT>
-__device__ __forceinline__ CdOut cd_pair(const LT& L, int i, int k) {
+// exact StateBased terms of pair (i, k) (i != k), oracle operation order, from the terms
+// the two orders of a pair share bit for bit (cd_pair2): cavelat (lati + latk commutes),
+// du^2 + dv^2 (the two orders' du, dv are exact negatives), vrel and the horizon.
+// dlon is per order: pymod360((lonk - loni) + 180) - 180 is not odd in the last bit.
+__device__ __forceinline__ CdOut cd_order(double dlat, double dlon, double cavelat, double du,
+                                          double dv, double dv2, double vrel, double horizon,
+                                          double dalt, double dvs) {
   CdOut r{false, false, 0.0, 0.0, false};
-  const double lati = L.lat[i], loni = L.lon[i];
-  const double latk = L.lat[k], lonk = L.lon[k];
-  const double dlat = (latk - lati) * kD2R;
-  const double dlon = (pymod360((lonk - loni) + 180.0) - 180.0) * kD2R;
-  const double cavelat = cos_t(((lati + latk) * kD2R) * 0.5);
   const double dangle = sqrt(dlat * dlat + (dlon * dlon) * (cavelat * cavelat));
   const double dist = divk_nn(6371000.0 * dangle, NM) * NM + 0.0;     // + 1e9*I, I = 0
-  const double du = cd_u(L, k) - cd_u(L, i);
-  const double dv = cd_v(L, k) - cd_v(L, i);
-  double dv2 = du * du + dv * dv;
-  dv2 = fabs(dv2) < 1e-6 ? 1e-6 : dv2;
-  const double vrel = sqrt(dv2);
-  const double horizon = (RPZ + DTLOOKAHEAD * vrel) * (1.0 + 1e-9) + 1.0;
   if (dist > horizon) return r;
   r.inside = true;
   r.dist = dist;
-  const double dalt = L.alt[k] - L.alt[i] + 0.0;
-  double dvs = L.vs[k] - L.vs[i];
   dvs = fabs(dvs) < 1e-6 ? 1e-6 : dvs;
   const double tcrosshi = (dalt + HPZ) / -dvs;
   const double tcrosslo = (dalt - HPZ) / -dvs;
@@ -744,6 +735,29 @@ __device__ __forceinline__ CdOut cd_pair(const LT& L, int i, int k) {
   r.confl = swhor && (tin <= tout) && (tout > 0.0) && (tin < DTLOOKAHEAD);
   r.tcpa = tcpa;
   return r;
+}
+
+// both orders of the unordered pair {i, k}: rik = row i / column k, rki = row k / column i
+template <class LT>
+__device__ __forceinline__ void cd_pair2(const LT& L, int i, int k, CdOut* rik, CdOut* rki) {
+  const double lati = L.lat[i], loni = L.lon[i];
+  const double latk = L.lat[k], lonk = L.lon[k];
+  const double dlat = (latk - lati) * kD2R;
+  const double dlon_ik = (pymod360((lonk - loni) + 180.0) - 180.0) * kD2R;
+  const double dlon_ki = (pymod360((loni - lonk) + 180.0) - 180.0) * kD2R;
+  const double cavelat = cos_t(((lati + latk) * kD2R) * 0.5);
+  const double du = cd_u(L, k) - cd_u(L, i);
+  const double dv = cd_v(L, k) - cd_v(L, i);
+  double dv2 = du * du + dv * dv;
+  dv2 = fabs(dv2) < 1e-6 ? 1e-6 : dv2;
+  const double vrel = sqrt(dv2);
+  const double horizon = (RPZ + DTLOOKAHEAD * vrel) * (1.0 + 1e-9) + 1.0;
+  const double alti = L.alt[i], altk = L.alt[k], vsi = L.vs[i], vsk = L.vs[k];
+  *rik = cd_order(dlat, dlon_ik, cavelat, du, dv, dv2, vrel, horizon, altk - alti + 0.0, vsk - vsi);
+  // the (k, i) differences as that order computes them (equal to the negations but for
+  // the sign of a zero)
+  *rki = cd_order((lati - latk) * kD2R, dlon_ki, cavelat, cd_u(L, i) - cd_u(L, k),
+                  cd_v(L, i) - cd_v(L, k), dv2, vrel, horizon, alti - altk + 0.0, vsi - vsk);
 }
 
 template <int GS>
@@ -1658,19 +1672,17 @@ __global__ __launch_bounds__(64) void step_kernel(KParams p) {
     L.gmin[lane] = bits(__builtin_inf());
     // phase 1: candidate pairs (no transcendentals).  The bound is symmetric in (i, k)
     // bit for bit, so each unordered pair is tested once: lane j takes the ring offsets
-    // 1..nac/2 (16 per lane at N = 32, balanced) and ORs the mirrored bit into lane k's
-    // LDS word (L.lm, re-zeroed before phase 2).
-    __syncthreads();
-    uint64_t cand = 0;
+    // 1..nac/2 (16 per lane at N = 32, balanced).  (The LDS rows above are first touched
+    // by phase 2's atomics, after the work-list barrier.)
+    const int nac = ev.nac;
+    uint64_t mine = 0;                   // bit sft-1: pair (j, j + sft) is a candidate
     if (on) {
-      const int nac = ev.nac;
       const float4 pi = L.fpk[lane];
       const float flati = pi.x, floni = pi.y, fui = pi.z, fvi = pi.w;
       const float fali = fabsf(flati);
-      // loads and tests only (unrolled so the LDS reads of several offsets are in
-      // flight together); the mirrored bits go out afterwards
+      // loads and tests only (unrolled so the LDS reads of several offsets are in flight
+      // together)
       const int nsft = (nac & 1) ? nac / 2 : (j < nac / 2 ? nac / 2 : nac / 2 - 1);
-      uint64_t mine = 0;                 // bit sft-1: pair (j, j + sft) is a candidate
 #pragma unroll 4
       for (int sft = 1; sft <= nsft; ++sft) {
         int k = j + sft;
@@ -1683,19 +1695,11 @@ __global__ __launch_bounds__(64) void step_kernel(KParams p) {
         const float du = pk.z - fui, dv = pk.w - fvi;
         if (cd_candidate_f(dlat, dl, x, du * du + dv * dv)) mine |= 1ull << (sft - 1);
       }
-      for (uint64_t mm = mine; mm; mm &= mm - 1) {
-        int k = j + 1 + __builtin_ctzll(mm);
-        if (k >= nac) k -= nac;
-        cand |= 1ull << k;
-        atomicOr(&L.lm[base + k], 1ull << j);
-      }
     }
-    __syncthreads();
-    cand |= L.lm[lane];
-    L.lm[lane] = 0ull;
-    // exclusive prefix sum of the per-lane counts (< 64) from one ballot per bit: each
-    // lane counts the set bits below it (mbcnt), no cross-lane data movement
-    const int cnt = __popcll(cand);
+    // work list of the unordered candidate pairs: exclusive prefix sum of the per-lane
+    // counts (< 64) from one ballot per bit -- each lane counts the set bits below it
+    // (mbcnt), no cross-lane data movement
+    const int cnt = __popcll(mine);
     int pos = 0, total = 0;
 #pragma unroll
     for (int bit = 0; bit < 7; ++bit) {
@@ -1704,25 +1708,31 @@ __global__ __launch_bounds__(64) void step_kernel(KParams p) {
                                             __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u)) << bit;
       total += __popcll(bm) << bit;
     }
-    for (uint64_t c = cand; c; c &= c - 1) {
-      const int k = __builtin_ctzll(c);
+    for (uint64_t c = mine; c; c &= c - 1) {
+      int k = j + 1 + __builtin_ctzll(c);
+      if (k >= nac) k -= nac;
       cd_list[pos++] = (unsigned short)((lane << 6) | (base + k));
     }
     __syncthreads();
 #if defined(BSG_STAMPS) && BSG_STAMPS
     BSG_STAMP(4, stamp_clock() | ((unsigned long long)total << 48));
 #endif
-    // phase 2: dense exact StateBased over the surviving pairs
+    // phase 2: dense exact StateBased over the surviving pairs, both orders per lane
     for (int t = lane; t < total; t += 64) {
       const int pr = cd_list[t];
       const int li = pr >> 6, lk = pr & 63;
-      const CdOut r = cd_pair(L, li, lk);
-      if (r.inside) {
-        atomicMin(&L.gmin[li / GS], bits(r.dist));
-        const int kk = lk - (li / GS) * GS;
-        if (r.confl) atomicOr(&L.cm[li], 1ull << kk);
-        if (r.lossep) atomicOr(&L.lm[li], 1ull << kk);
-        if (r.confl && r.tcpa > 0.0) atomicMax(&L.tmax[li], bits(r.tcpa));
+      const int gb = (li / GS) * GS;
+      CdOut r[2];
+      cd_pair2(L, li, lk, &r[0], &r[1]);
+#pragma unroll
+      for (int o = 0; o < 2; ++o) {
+        const int row = o ? lk : li, col = (o ? li : lk) - gb;
+        if (r[o].inside) {
+          atomicMin(&L.gmin[li / GS], bits(r[o].dist));
+          if (r[o].confl) atomicOr(&L.cm[row], 1ull << col);
+          if (r[o].lossep) atomicOr(&L.lm[row], 1ull << col);
+          if (r[o].confl && r[o].tcpa > 0.0) atomicMax(&L.tmax[row], bits(r[o].tcpa));
+        }
       }
     }
     __syncthreads();
