@@ -210,6 +210,7 @@ struct Memo {
   int wp_k;                        // cached waypoint (coords, next-leg bearing, trig)
   double wp_lat, wp_lon, wp_nq, wp_cos, wp_sin, wp_rw, wp_pnq;   // wp_pnq = pymod360(wp_nq)
   double coslat, sinlat;           // cos/sin(lat * D2R) of the current latitude
+  double phdg;                     // pymod360(hdg), for LNAV's waypoint-behind test
   uint64_t hdg_bits;               // key of (shdg, chdg) = sincos(hdg * D2R)
   double shdg, chdg;
   uint64_t rad_bits;               // key of the LNAV turn radius tas^2/(g0*tan(bank))
@@ -251,6 +252,7 @@ __device__ __forceinline__ void memo_init(Memo& m, const AC& s) {
   m.wp_k = -1; m.wp_lat = 0; m.wp_lon = 0; m.wp_nq = 0; m.wp_cos = 0; m.wp_sin = 0; m.wp_rw = 0;
   m.wp_pnq = 0;
   m.hdg_bits = kNoKey; m.shdg = 0; m.chdg = 0;
+  m.phdg = pymod360(s.hdg);
   m.rad_bits = kNoKey; m.turnrad = 0;
   m.last_alt = s.alt;
   m.cas_tas_bits = kNoKey; m.cas_alt_bits = kNoKey;
@@ -392,14 +394,24 @@ __device__ __forceinline__ void substep(AC& s, Memo& m, double dt, const RouteRe
       const double tnum = turnrad * (pi2 * h) * (1.0 + 1e-12);      // turnrad * th * den
       const double tlo = turnrad * tl;
       const bool tb = h >= 0.0 && h <= 1.5;
-      int rtn = (half <= 45.0 && lo2 > trm * trm * (1.0 + 1e-14)) ? 0   // tan(half) <= 1 < dist/turnrad
-              : !tb ? -1
-              : hi2 < tlo * tlo * (1.0 - 1e-14) ? 1
-              : lo2 * (den * den) >= tnum * tnum * (1.0 + 1e-14) ? 0 : -1;
       const double glo = 4.0 * g * 0.999999, ghi = 4.0 * g * 1.000001;
-      int cw = hi2 < glo * glo * (1.0 - 1e-14) ? 1 : (lo2 > ghi * ghi * (1.0 + 1e-14) ? 0 : -1);
-      if (!bv) { rtn = -1; cw = -1; }
-      if (rtn < 0 || cw < 0) {
+      // the bound decisions as predicates (they combine as lane masks; nested int selects
+      // would each add a compare -> select latency):
+      //   r0a: tan(half) <= 1 < dist/turnrad -> not reached by the turn distance
+      //   r1 / r0b: dist below the Taylor / above the Becker-Stark turn distance
+      //   cw1 / cw0: dist/g below / above 4 outside the 1e-6 band
+      const bool r0a = half <= 45.0 && lo2 > trm * trm * (1.0 + 1e-14);
+      const bool r1 = hi2 < tlo * tlo * (1.0 - 1e-14);
+      const bool r0b = lo2 * (den * den) >= tnum * tnum * (1.0 + 1e-14);
+      const bool rtn1 = !r0a && tb && r1;
+      const bool rtn0 = r0a || (tb && !r1 && r0b);
+      const bool cw1 = hi2 < glo * glo * (1.0 - 1e-14);
+      const bool cw0 = !cw1 && lo2 > ghi * ghi * (1.0 + 1e-14);
+      const bool tc = fabs(degto180_pq(WIND ? pymod360(trkv) : m.phdg, pq)) > 90.0;   // waypoint behind
+      reached = rtn1 || (cw1 && tc);
+      if (!bv || !(rtn1 || rtn0) || !(cw1 || cw0)) {
+        int rtn = !bv ? -1 : (rtn1 ? 1 : (rtn0 ? 0 : -1));
+        int cw = !bv ? -1 : (cw1 ? 1 : (cw0 ? 0 : -1));
         if (bv && rtn < 0) {                   // the exact tan against the distance bounds
           const double turndist = fabs(turnrad * tan(half * kD2R));
           const double td2 = turndist * turndist;
@@ -416,9 +428,8 @@ __device__ __forceinline__ void substep(AC& s, Memo& m, double dt, const RouteRe
           // dist/g < 4, decided without the division outside a 1e-6 band around 4*g
           cw = dist < 4.0 * g * 0.999999 ? 1 : (dist > 4.0 * g * 1.000001 ? 0 : dist / g < 4.0);
         }
+        reached = rtn == 1 || (cw == 1 && tc);
       }
-      const bool tooclose = cw == 1 && (fabs(degto180_pq(pymod360(trkv), pq)) > 90.0);
-      reached = rtn == 1 || tooclose;
     }
     BSG_SUBSTEP_MARK(6);
     if (reached) {
@@ -516,6 +527,7 @@ __device__ __forceinline__ void substep(AC& s, Memo& m, double dt, const RouteRe
     swhdgsel = fabs(delhdg) > fabs(dt * turnrate);
   }
   s.hdg = pymod360(swhdgsel ? s.hdg + dt * turnrate * sgn(delhdg) : hdg_cmd);
+  m.phdg = s.hdg >= 360.0 ? s.hdg - 360.0 : s.hdg;   // pymod360 of a [0, 360] value
   const double delta_alt = allow_h - s.alt;
   const bool swaltsel = fabs(delta_alt) > npmax(10 * FT, fabs(2 * fabs(dt * s.vs)));
   const double target_vs = (double)swaltsel * sgn(delta_alt) * fabs(vs_cmd);
