@@ -143,6 +143,9 @@ def main():
                     help="merge: the BASELINE metric (default); descent-sac: BASELINE configs[4], "
                          "DescentEnv-v0 with the SAC learner in the loop")
     ap.add_argument("--no-graph", action="store_true", help="descent-sac: eager, no HIP graph")
+    ap.add_argument("--blas", default="cublas", choices=("default", "cublas", "cublaslt"),
+                    help="descent-sac: torch.backends.cuda.preferred_blas_library for the learner's "
+                         "GEMMs (cublas = rocBLAS/hipBLAS on ROCm, cublaslt = hipBLASLt)")
     args = ap.parse_args()
     if args.workload == "descent-sac":
         return bench_descent_sac(args)
@@ -327,6 +330,13 @@ def bench_descent_sac(args):
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
+    if args.blas != "default":
+        # the learner's GEMMs are batch-256 x 256-wide: hipBLASLt's default pick for them is a
+        # 256x256 macro tile, i.e. one or a few workgroups for the whole product
+        torch.backends.cuda.preferred_blas_library(args.blas)
+        if args.blas == "cublas":
+            # nn.Linear's addmm-with-bias otherwise still goes to hipBLASLt's bias epilogue
+            os.environ["DISABLE_ADDMM_CUDA_LT"] = "1"
     E = args.total_envs // world
     cfg = config.descent_config()
     b = core.DeviceBatch(cfg, E, autoreset=nat.AUTORESET_SAME_STEP, compute_cd=False,
@@ -399,7 +409,7 @@ def bench_descent_sac(args):
                        "envs_total": world * E, "envs_per_gpu": E,
                        "parallelism": f"env-shard x{world}" + (" + RCCL gradient all_reduce "
                                                                "(data-parallel SAC)" if world > 1 else ""),
-                       "hip_graph": graph},
+                       "hip_graph": graph, "blas": str(torch.backends.cuda.preferred_blas_library())},
             "env_only": {"value": total / el_env, "ms_per_step": el_env * 1e3 / args.steps},
             "env_policy": {"value": total / el_pol, "ms_per_step": el_pol * 1e3 / args.steps},
             "env_policy_learner": {"value": total / el_rl, "ms_per_step": el_rl * 1e3 / args.steps,

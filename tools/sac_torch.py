@@ -155,9 +155,12 @@ class SAC:
         self._allreduce([self.log_alpha])
         self.opt_al.step()
         with torch.no_grad():
-            for net, tgt in ((self.q1, self.q1t), (self.q2, self.q2t)):
-                for p, pt in zip(net.parameters(), tgt.parameters()):
-                    pt.mul_(1.0 - self.tau).add_(p, alpha=self.tau)
+            # SB3 polyak_update (target * (1 - tau), then + tau * param), as two multi-tensor
+            # kernels over all target parameters instead of two kernels per tensor
+            src = list(self.q1.parameters()) + list(self.q2.parameters())
+            tgt = list(self.q1t.parameters()) + list(self.q2t.parameters())
+            torch._foreach_mul_(tgt, 1.0 - self.tau)
+            torch._foreach_add_(tgt, src, alpha=self.tau)
         return lq.detach(), la.detach()
 
 
