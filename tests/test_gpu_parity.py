@@ -255,6 +255,8 @@ def _subset_compare(b, r, ids, N, kind, t, errs):
     for key, (a, z) in errs["slices"].items():
         errs["max"][key] = max(errs["max"].get(key, 0.0),
                                float(np.abs(o[:, a:z].astype(np.float64) - r["obs"][:, a:z]).max()))
+        errs.setdefault("ref", {})[key] = max(errs.get("ref", {}).get(key, 0.0),
+                                              float(np.abs(r["obs"][:, a:z]).max()))
     rw = b.reward.cpu().numpy()[ids].astype(np.float64)
     close(rw, r["reward"], f"reward t={t}")
     errs["max"]["(reward)"] = max(errs["max"].get("(reward)", 0.0), float(np.abs(rw - r["reward"]).max()))
@@ -283,9 +285,16 @@ def _obs_slices(b):
 
 
 def _report(errs, what):
+    """Print each obs key's max error and hold the normalised keys (|ref| <= 8, where an fp32
+    ulp is <= 1e-6) to north_star's flat 1e-5; raw-unit keys (airspeed in m/s, whose fp32
+    ulp is 1.5e-5 at 200 m/s) keep the 1e-5 + 1e-5 |ref| bar of close()."""
     print(f"\n{what}: per-key max |gpu - oracle| over the subset and all compared steps")
+    ref = errs.get("ref", {})
     for k, v in sorted(errs["max"].items()):
-        print(f"  {k:24s} {v:.3e}")
+        print(f"  {k:24s} {v:.3e}   max |ref| {ref.get(k, float('nan')):.3g}")
+    flat = {k: v for k, v in errs["max"].items() if k in ref and ref[k] <= 8.0}
+    bad = {k: v for k, v in flat.items() if v > 1e-5}
+    assert not bad, f"{what}: normalised keys above the flat 1e-5: {bad}"
 
 
 def test_merge_full_size_subset_parity(bg):
