@@ -213,8 +213,7 @@ struct Memo {
   double phdg;                     // pymod360(hdg), for LNAV's waypoint-behind test
   uint64_t hdg_bits;               // key of (shdg, chdg) = sincos(hdg * D2R)
   double shdg, chdg;
-  uint64_t rad_bits;               // key of the LNAV turn radius tas^2/(g0*tan(bank))
-  double turnrad;
+  double turnrad;                  // LNAV turn radius tas^2/(g0*tan(bank)) of the current tas
   double last_alt;                 // altitude at the start of the latest substep
   uint64_t cas_tas_bits, cas_alt_bits;  // key of the stored cas = vtas2cas(tas, alt)
 };
@@ -253,7 +252,7 @@ __device__ __forceinline__ void memo_init(Memo& m, const AC& s) {
   m.wp_pnq = 0;
   m.hdg_bits = kNoKey; m.shdg = 0; m.chdg = 0;
   m.phdg = pymod360(s.hdg);
-  m.rad_bits = kNoKey; m.turnrad = 0;
+  m.turnrad = 0;
   m.last_alt = s.alt;
   m.cas_tas_bits = kNoKey; m.cas_alt_bits = kNoKey;
   sincos_t(s.lat * kD2R, &m.sinlat, &m.coslat);
@@ -321,11 +320,22 @@ __device__ __forceinline__ void memo_final_cas(Memo& m, AC& s) {
   m.cas_alt_bits = lb;
 }
 
+__device__ __forceinline__ double turnrad_of(double tas) {
+  return divk_nn(tas * tas, npmax(0.01, TAN_BANKDEF) * G0);
+}
+
 __device__ __forceinline__ void memo_wp(Memo& m, const RouteRegs& rt, int k) {
   m.wp_k = k;
   rt.get(k, &m.wp_lat, &m.wp_lon, &m.wp_nq, &m.wp_rw);
   m.wp_pnq = pymod360(m.wp_nq);
   sincos_t(m.wp_lat * kD2R, &m.wp_sin, &m.wp_cos);
+}
+
+// the LNAV terms at the start of a launch: the active waypoint's (LNAV lanes) and the turn
+// radius of the loaded tas
+__device__ __forceinline__ void memo_lnav(Memo& m, const AC& s, const RouteRegs& rt) {
+  if (s.nav & 1) memo_wp(m, rt, (s.nav >> 8) & 0xff);
+  m.turnrad = turnrad_of(s.tas);
 }
 
 // Diagnostic hook of tools/probe/substep_probe.hip (section timing of one substep);
@@ -336,7 +346,9 @@ __device__ __forceinline__ void memo_wp(Memo& m, const RouteRegs& rt, int k) {
 
 // ---- one BlueSky substep of one aircraft (Traffic.update, RESO OFF) ------------------
 // oracle/bluesky_subset.py: traffic_update.  WIND: a wind field is set (wrappers/wind.py).
-template <bool WIND>
+// HMEMO: keep the heading's sin/cos across substeps keyed by its bits (kinds whose
+// aircraft fly constant headings); Merge's LNAV intruders change heading every substep.
+template <bool WIND, bool HMEMO = true>
 __device__ __forceinline__ void substep(AC& s, Memo& m, double dt, const RouteRegs& rt,
                                         const WindDev& w) {
   double vwn = 0.0, vwe = 0.0;
@@ -348,12 +360,9 @@ __device__ __forceinline__ void substep(AC& s, Memo& m, double dt, const RouteRe
     int k = (s.nav >> 8) & 0xff;
     // the waypoint distance only feeds `dist < turndist` (turndist <= turnrad while the
     // leg change is <= 90 deg) and `dist/|gs| < 4 s`; beyond both it need not be exact.
-    // One branch for both memo keys (a branch is ~80 cycles of latency, taken or not).
-    if (k != m.wp_k || bits(s.tas) != m.rad_bits) {
-      if (k != m.wp_k) memo_wp(m, rt, k);
-      m.turnrad = divk_nn(s.tas * s.tas, npmax(0.01, TAN_BANKDEF) * G0);
-      m.rad_bits = bits(s.tas);
-    }
+    // The waypoint terms (memo_wp) and the turn radius of the current tas are kept current
+    // where k and tas change (memo_lnav, the reached block, update_airspeed): no memo-key
+    // branch here (~85 cycles per substep even when never taken).
     const double turnrad = m.turnrad;
     double qdr, x;
     qdr_x(s.lat, s.lon, m.coslat, m.sinlat, m.wp_lat, m.wp_lon, m.wp_cos, m.wp_sin, &qdr, &x);
@@ -515,6 +524,7 @@ __device__ __forceinline__ void substep(AC& s, Memo& m, double dt, const RouteRe
   const bool need_ax = fabs(delta_spd) > fabs(dt * axmax);
   s.ax = (double)need_ax * sgn(delta_spd) * axmax;
   s.tas = need_ax ? s.tas + s.ax * dt : allow_tas;
+  m.turnrad = turnrad_of(s.tas);              // for the next substep's LNAV (off the chain)
   BSG_SUBSTEP_MARK(2);
   const double delhdg = pymod360(hdg_cmd - s.hdg + 180.0) - 180.0;
   // |delhdg| > |dt*turnrate| is false at delhdg == 0 whatever turnrate is: a straight
@@ -538,9 +548,15 @@ __device__ __forceinline__ void substep(AC& s, Memo& m, double dt, const RouteRe
   if (!isfinite(s.vs)) s.vs = 0.0;
   // update_groundspeed + update_pos
   BSG_SUBSTEP_MARK(3);
-  if (bits(s.hdg) != m.hdg_bits) {        // straight flight keeps its heading trig
+  if constexpr (HMEMO) {
+    if (bits(s.hdg) != m.hdg_bits) {      // straight flight keeps its heading trig
+      sincos_t(s.hdg * kD2R, &m.shdg, &m.chdg);
+      m.hdg_bits = bits(s.hdg);
+    }
+  } else {
+    // LNAV lanes re-aim at the waypoint's bearing every substep, so some lane of a wave
+    // always misses the memo: its branch would only add latency
     sincos_t(s.hdg * kD2R, &m.shdg, &m.chdg);
-    m.hdg_bits = bits(s.hdg);
   }
   const double shdg = m.shdg, chdg = m.chdg;
   double gsnorth = s.tas * chdg;
@@ -1494,13 +1510,14 @@ __device__ __forceinline__ void propagate(const KParams& p, int e, int j, size_t
     if (j == 0) { m.alt_bits = bits(oat[0]); m.at = Atmos{oat[1], oat[2], oat[3]}; }
     RouteRegs rt;
     rt.load(p.route);
+    memo_lnav(m, s, rt);
     const double dt = p.cfg.simdt;
     if constexpr (KIND == BSG_ENV_STATIC_OBSTACLE) {
       // static_obstacle_env.py:132-150: _get_reward after every substep, with the
       // waypoint distance and drift of the previous observation; stop when done
       const double* geo = b.env_geom + (size_t)e * SO_GEOM;
       for (int it = 0; it < S; ++it) {
-        substep<WIND>(s, m, dt, rt, p.wind);
+        substep<WIND, KIND != BSG_ENV_MERGE>(s, m, dt, rt, p.wind);
         int reach = 0;
         if (ev.aux[0] < 5 && ev.wpt_reach != 1) { ev.wpt_reach = 1; reach = 1; }
         const double dd = fabs(ev.aux[1] * kD2R);
@@ -1513,7 +1530,7 @@ __device__ __forceinline__ void propagate(const KParams& p, int e, int j, size_t
       }
     } else {
 #if defined(BSG_NO_PRIO_BALANCE) && BSG_NO_PRIO_BALANCE
-      for (int it = 0; it < S; ++it) substep<WIND>(s, m, dt, rt, p.wind);
+      for (int it = 0; it < S; ++it) substep<WIND, KIND != BSG_ENV_MERGE>(s, m, dt, rt, p.wind);
 #else
       // Balance the two waves that share a SIMD (4096 x 32 Merge: 2048 waves on 1024
       // SIMDs).  VALU issue goes by priority, then age, so the older wave (slot 0) used to
@@ -1531,7 +1548,7 @@ __device__ __forceinline__ void propagate(const KParams& p, int e, int j, size_t
       for (int it = 0; it < S; ++it) {
         if ((slot & 1) ? (it < sw) : (it >= sw)) __builtin_amdgcn_s_setprio(1);
         else __builtin_amdgcn_s_setprio(0);
-        substep<WIND>(s, m, dt, rt, p.wind);
+        substep<WIND, KIND != BSG_ENV_MERGE>(s, m, dt, rt, p.wind);
       }
       __builtin_amdgcn_s_setprio(0);
 #endif

@@ -15,6 +15,9 @@ __device__ long long g_mark[8];
 #ifndef PROBE_MODE
 #define PROBE_MODE 0
 #endif
+#ifndef PROBE_HMEMO
+#define PROBE_HMEMO false          // as the Merge kernel (LNAV intruders)
+#endif
 
 constexpr int NF = 12;       // lat lon alt hdg tas cas vs ax ap_trk selspd selalt selvs, + nav
 constexpr int SMAX = 16;
@@ -38,12 +41,13 @@ __global__ void probe(bsg::Route route, const double* st, int S, long long* cyc,
   memo_init(m, s);
   RouteRegs rt;
   rt.load(route);
+  memo_lnav(m, s, rt);
   WindDev w{};
   long long t[SMAX + 1];
   t[0] = __builtin_amdgcn_s_memtime();
   long long mk[SMAX][8];
   for (int it = 0; it < S; ++it) {
-    substep<false>(s, m, 5.0, rt, w);
+    substep<false, PROBE_HMEMO>(s, m, 5.0, rt, w);
     t[it + 1] = __builtin_amdgcn_s_memtime();
     for (int q = 0; q < 8; ++q) mk[it][q] = g_mark[q];
   }
