@@ -33,6 +33,8 @@
 //     the distance as well.  min_sep is defined over the pairs inside the horizon.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "bsg_areas.h"
 #include "bsg_device.h"
 #include "bsg_internal.h"
@@ -350,7 +352,7 @@ __device__ __forceinline__ void memo_lnav(Memo& m, const AC& s, const RouteRegs&
 // aircraft fly constant headings); Merge's LNAV intruders change heading every substep.
 template <bool WIND, bool HMEMO = true>
 __device__ __forceinline__ void substep(AC& s, Memo& m, double dt, const RouteRegs& rt,
-                                        const WindDev& w) {
+                                        const WindDev& w, bool fh = false) {
   double vwn = 0.0, vwe = 0.0;
   if constexpr (WIND) wind_at(w, s.lat, s.lon, s.alt, &vwn, &vwe);
   const double gsv = WIND ? s.gs : s.tas;     // without wind gs = tas and trk = hdg
@@ -388,8 +390,8 @@ __device__ __forceinline__ void substep(AC& s, Memo& m, double dt, const RouteRe
     // selects instead of the branch -- measured ~170 cycles slower per substep:
     // tools/probe/substep_probe.hip.)
     const bool need = !far || half > 45.0;
-    bool reached = false;
     if (need) {
+      bool reached = false;
       const double g = npmax(0.0001, fabs(gsv));
       double lo2, hi2;
       const bool bv = qdrdist_bounds2(s.lat, m.wp_lat, x, m.wp_rw, &lo2, &hi2);
@@ -439,19 +441,19 @@ __device__ __forceinline__ void substep(AC& s, Memo& m, double dt, const RouteRe
         }
         reached = rtn == 1 || (cw == 1 && tc);
       }
-    }
-    BSG_SUBSTEP_MARK(6);
-    if (reached) {
-      if (k >= rt.len - 1) {
-        s.nav &= ~1;                       // last waypoint: LNAV off, keep commanded track
-      } else {
-        ++k;
-        s.nav = (k << 8) | 1;
-        memo_wp(m, rt, k);
-        qdr_x(s.lat, s.lon, m.coslat, m.sinlat, m.wp_lat, m.wp_lon, m.wp_cos, m.wp_sin,
-              &qdr, &x);                   // only the bearing to the new waypoint is used
+      if (reached) {                       // (inside the block: no branch when no lane is near)
+        if (k >= rt.len - 1) {
+          s.nav &= ~1;                     // last waypoint: LNAV off, keep commanded track
+        } else {
+          ++k;
+          s.nav = (k << 8) | 1;
+          memo_wp(m, rt, k);
+          qdr_x(s.lat, s.lon, m.coslat, m.sinlat, m.wp_lat, m.wp_lon, m.wp_cos, m.wp_sin,
+                &qdr, &x);                 // only the bearing to the new waypoint is used
+        }
       }
     }
+    BSG_SUBSTEP_MARK(6);
     if (s.nav & 1) s.ap_trk = qdr;
   }
   BSG_SUBSTEP_MARK(1);
@@ -466,7 +468,7 @@ __device__ __forceinline__ void substep(AC& s, Memo& m, double dt, const RouteRe
   const uint64_t hb = bits(allow_h);
   // aporasas
   const double vs_cmd0 = fabs(ap_vs);
-  double hdg_cmd;
+  double hdg_cmd = 0.0;                     // !WIND: evaluated in the heading block below
   if constexpr (WIND) {
     // ActivePilot: heading that flies the commanded track through the wind
     const double Vw = sqrt(vwn * vwn + vwe * vwe);
@@ -474,8 +476,6 @@ __device__ __forceinline__ void substep(AC& s, Memo& m, double dt, const RouteRe
     const double drift = s.ap_trk * kD2R - winddir;
     const double steer = asin(npmin(1.0, npmax(-1.0, Vw * sin_t(drift) / npmax(0.001, s.tas))));
     hdg_cmd = pymod360(s.ap_trk + steer * kR2D);
-  } else {
-    hdg_cmd = pymod360(s.ap_trk);
   }
   // the speed schedule: one branch for both memos (steady flight hits both)
   const bool spd_miss = bits(s.selspd) != m.spd_bits || ab != m.spdalt_bits;
@@ -526,17 +526,30 @@ __device__ __forceinline__ void substep(AC& s, Memo& m, double dt, const RouteRe
   s.tas = need_ax ? s.tas + s.ax * dt : allow_tas;
   m.turnrad = turnrad_of(s.tas);              // for the next substep's LNAV (off the chain)
   BSG_SUBSTEP_MARK(2);
-  const double delhdg = pymod360(hdg_cmd - s.hdg + 180.0) - 180.0;
-  // |delhdg| > |dt*turnrate| is false at delhdg == 0 whatever turnrate is: a straight
-  // flying aircraft needs no turn rate (whose division would sit on the tas -> heading ->
-  // position chain)
-  bool swhdgsel = false;
-  double turnrate = 0.0;
-  if (delhdg != 0.0) {
-    turnrate = (G0 * TAN_BANKDEF / npmax(s.tas, EPS_SPD)) * kR2D;
-    swhdgsel = fabs(delhdg) > fabs(dt * turnrate);
-  }
-  s.hdg = pymod360(swhdgsel ? s.hdg + dt * turnrate * sgn(delhdg) : hdg_cmd);
+  // The heading update with its three pymod360.  fh (wave-uniform, propagate): every
+  // lane has |ap_trk| < 360 and hdg in [0, 360], so hdg_cmd = pymod360(ap_trk) is one
+  // select, and delhdg's and the new heading's arguments lie in [-180, 540] (two selects
+  // each; |dt * turnrate| < |delhdg| <= 180 when it is added) -- one uniform branch here
+  // instead of three ~150-cycle fmod branches.
+  auto turn = [&](auto fh_tag) {
+    constexpr bool F = decltype(fh_tag)::value;
+    if constexpr (!WIND) hdg_cmd = F ? pymod360_s(s.ap_trk) : pymod360(s.ap_trk);
+    const double da = hdg_cmd - s.hdg + 180.0;
+    const double delhdg = (F ? pymod360_r(da) : pymod360(da)) - 180.0;
+    // |delhdg| > |dt*turnrate| is false at delhdg == 0 whatever turnrate is: a straight
+    // flying aircraft needs no turn rate (whose division would sit on the tas -> heading
+    // -> position chain)
+    bool swhdgsel = false;
+    double turnrate = 0.0;
+    if (delhdg != 0.0) {
+      turnrate = (G0 * TAN_BANKDEF / npmax(s.tas, EPS_SPD)) * kR2D;
+      swhdgsel = fabs(delhdg) > fabs(dt * turnrate);
+    }
+    const double ha = swhdgsel ? s.hdg + dt * turnrate * sgn(delhdg) : hdg_cmd;
+    s.hdg = F ? pymod360_r(ha) : pymod360(ha);
+  };
+  if (!WIND && fh) turn(std::true_type{});
+  else turn(std::false_type{});
   m.phdg = s.hdg >= 360.0 ? s.hdg - 360.0 : s.hdg;   // pymod360 of a [0, 360] value
   const double delta_alt = allow_h - s.alt;
   const bool swaltsel = fabs(delta_alt) > npmax(10 * FT, fabs(2 * fabs(dt * s.vs)));
@@ -1512,12 +1525,18 @@ __device__ __forceinline__ void propagate(const KParams& p, int e, int j, size_t
     rt.load(p.route);
     memo_lnav(m, s, rt);
     const double dt = p.cfg.simdt;
+    // substep's fast heading block (fh): every stepping lane of the wave has |ap_trk| < 360
+    // and, for the first substep, hdg in [0, 360] (later substeps keep both: hdg becomes a
+    // pymod360 result, ap_trk a bearing).  A spawn heading (bearing - 180) fails the hdg
+    // test, so an env's first step after a reset runs one substep on the fmod path.
+    const bool trk_ok = !WIND && __ballot(!(fabs(s.ap_trk) < 360.0)) == 0;
+    const bool fh0 = trk_ok && __ballot(!(s.hdg >= 0.0 && s.hdg <= 360.0)) == 0;
     if constexpr (KIND == BSG_ENV_STATIC_OBSTACLE) {
       // static_obstacle_env.py:132-150: _get_reward after every substep, with the
       // waypoint distance and drift of the previous observation; stop when done
       const double* geo = b.env_geom + (size_t)e * SO_GEOM;
       for (int it = 0; it < S; ++it) {
-        substep<WIND, KIND != BSG_ENV_MERGE>(s, m, dt, rt, p.wind);
+        substep<WIND, KIND != BSG_ENV_MERGE>(s, m, dt, rt, p.wind, it == 0 ? fh0 : trk_ok);
         int reach = 0;
         if (ev.aux[0] < 5 && ev.wpt_reach != 1) { ev.wpt_reach = 1; reach = 1; }
         const double dd = fabs(ev.aux[1] * kD2R);
@@ -1530,7 +1549,8 @@ __device__ __forceinline__ void propagate(const KParams& p, int e, int j, size_t
       }
     } else {
 #if defined(BSG_NO_PRIO_BALANCE) && BSG_NO_PRIO_BALANCE
-      for (int it = 0; it < S; ++it) substep<WIND, KIND != BSG_ENV_MERGE>(s, m, dt, rt, p.wind);
+      for (int it = 0; it < S; ++it)
+        substep<WIND, KIND != BSG_ENV_MERGE>(s, m, dt, rt, p.wind, it == 0 ? fh0 : trk_ok);
 #else
       // Balance the two waves that share a SIMD (4096 x 32 Merge: 2048 waves on 1024
       // SIMDs).  VALU issue goes by priority, then age, so the older wave (slot 0) used to
@@ -1548,7 +1568,7 @@ __device__ __forceinline__ void propagate(const KParams& p, int e, int j, size_t
       for (int it = 0; it < S; ++it) {
         if ((slot & 1) ? (it < sw) : (it >= sw)) __builtin_amdgcn_s_setprio(1);
         else __builtin_amdgcn_s_setprio(0);
-        substep<WIND, KIND != BSG_ENV_MERGE>(s, m, dt, rt, p.wind);
+        substep<WIND, KIND != BSG_ENV_MERGE>(s, m, dt, rt, p.wind, it == 0 ? fh0 : trk_ok);
       }
       __builtin_amdgcn_s_setprio(0);
 #endif

@@ -42,12 +42,14 @@ __global__ void probe(bsg::Route route, const double* st, int S, long long* cyc,
   RouteRegs rt;
   rt.load(route);
   memo_lnav(m, s, rt);
+  const bool trk_ok = __ballot(!(fabs(s.ap_trk) < 360.0)) == 0;        // as propagate
+  const bool fh0 = trk_ok && __ballot(!(s.hdg >= 0.0 && s.hdg <= 360.0)) == 0;
   WindDev w{};
   long long t[SMAX + 1];
   t[0] = __builtin_amdgcn_s_memtime();
   long long mk[SMAX][8];
   for (int it = 0; it < S; ++it) {
-    substep<false, PROBE_HMEMO>(s, m, 5.0, rt, w);
+    substep<false, PROBE_HMEMO>(s, m, 5.0, rt, w, it == 0 ? fh0 : trk_ok);
     t[it + 1] = __builtin_amdgcn_s_memtime();
     for (int q = 0; q < 8; ++q) mk[it][q] = g_mark[q];
   }
