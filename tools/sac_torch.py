@@ -10,6 +10,8 @@ Linear-ReLU 256-256, squashed Gaussian with log_std clamped to [-20, 2], Adam lr
 batch 256, buffer 1e6, gamma 0.99, tau 0.005, entropy coefficient 'auto' (target
 entropy -dim(A)), train_freq 1 / gradient_steps 1 -- one gradient step per vector step.
 
+The twin critics are one TwinQ (weights stacked, one batched GEMM per layer for both).
+
 Per iteration: sample actions for every env (actor forward) -> one env step on the
 device (SAME_STEP autoreset, terminal obs from final_obs as SB3's VecEnv gives it) ->
 insert the E transitions into a device ring buffer -> one SAC update.  The whole
@@ -63,23 +65,60 @@ class Actor(nn.Module):
             self.log_std.weight.copy_(g("log_std.weight")); self.log_std.bias.copy_(g("log_std.bias"))
 
 
+class TwinQ(nn.Module):
+    """SB3's twin critics (two Linear-ReLU 256-256 MLPs over [obs, act], each initialised as
+    nn.Linear does) with their weights stacked on a leading axis of 2: every layer is one
+    batched GEMM for both critics (baddbmm) and every elementwise op, reduction and their
+    backward run once on [2, B, .] -- half the launches of two separate critics, which is
+    what a batch-256 update costs (a few microseconds per kernel).  forward -> [2, B]."""
+
+    def __init__(self, i, h=256):
+        super().__init__()
+        a, b = mlp(i, 1, h), mlp(i, 1, h)
+        w = lambda k: nn.Parameter(torch.stack([a[k].weight.detach().t(), b[k].weight.detach().t()]).contiguous())  # noqa: E731
+        c = lambda k: nn.Parameter(torch.stack([a[k].bias.detach(), b[k].bias.detach()])[:, None, :].contiguous())  # noqa: E731
+        self.w0, self.w1, self.w2 = w(0), w(2), w(4)
+        self.b0, self.b1, self.b2 = c(0), c(2), c(4)
+
+    def forward(self, x):
+        h = torch.relu(torch.baddbmm(self.b0, x.expand(2, *x.shape), self.w0))
+        h = torch.relu(torch.baddbmm(self.b1, h, self.w1))
+        return torch.baddbmm(self.b2, h, self.w2).squeeze(-1)
+
+
+class QView(nn.Module):
+    """Critic `idx` of a TwinQ as a module (forward -> [B, 1]); parameters() are the shared
+    stacked tensors (not registered here, so an optimizer over the TwinQ sees them once)."""
+
+    def __init__(self, twin, idx):
+        super().__init__()
+        object.__setattr__(self, "_twin", twin)
+        self.idx = idx
+
+    def forward(self, x):
+        return self._twin(x)[self.idx][:, None]
+
+    def parameters(self, recurse=True):
+        return self._twin.parameters(recurse)
+
+
 class SAC:
     def __init__(self, obs_dim, act_dim, device, *, lr=3e-4, batch=256, buffer=1_000_000,
                  gamma=0.99, tau=0.005, group=None, seed=0):
         torch.manual_seed(seed)
         self.dev = torch.device(device)
         self.actor = Actor(obs_dim, act_dim).to(self.dev)
-        self.q1, self.q2 = mlp(obs_dim + act_dim, 1).to(self.dev), mlp(obs_dim + act_dim, 1).to(self.dev)
-        self.q1t, self.q2t = mlp(obs_dim + act_dim, 1).to(self.dev), mlp(obs_dim + act_dim, 1).to(self.dev)
-        self.q1t.load_state_dict(self.q1.state_dict())
-        self.q2t.load_state_dict(self.q2.state_dict())
+        self.q = TwinQ(obs_dim + act_dim).to(self.dev)
+        self.qt = TwinQ(obs_dim + act_dim).to(self.dev)
+        self.qt.load_state_dict(self.q.state_dict())
+        self.q1, self.q2 = QView(self.q, 0), QView(self.q, 1)
         self.log_alpha = torch.zeros(1, device=self.dev, requires_grad=True)
         self.target_entropy = -float(act_dim)
         # fused Adam: one kernel per parameter group instead of a foreach chain per tensor
         # (the update is launch-bound: batch 256 through 256-wide MLPs)
         opt = dict(lr=lr, fused=True, capturable=True) if self.dev.type == "cuda" else dict(lr=lr)
         self.opt_a = torch.optim.Adam(self.actor.parameters(), **opt)
-        self.opt_q = torch.optim.Adam(list(self.q1.parameters()) + list(self.q2.parameters()), **opt)
+        self.opt_q = torch.optim.Adam(self.q.parameters(), **opt)
         self.opt_al = torch.optim.Adam([self.log_alpha], **opt)
         self.gamma, self.tau = gamma, tau
         self.group = group
@@ -88,11 +127,16 @@ class SAC:
         self.batch = max(1, batch // world)
         self.cap = buffer // world
         d = self.dev
-        self.buf_obs = torch.zeros((self.cap, obs_dim), device=d)
-        self.buf_next = torch.zeros((self.cap, obs_dim), device=d)
-        self.buf_act = torch.zeros((self.cap, act_dim), device=d)
-        self.buf_rew = torch.zeros((self.cap,), device=d)
-        self.buf_done = torch.zeros((self.cap,), device=d)
+        # one packed row per transition [obs | act | rew | next_obs | done]: an insert is one
+        # index_copy and a sample one gather (the named buffers are column views)
+        self.buf = torch.zeros((self.cap, 2 * obs_dim + act_dim + 2), device=d)
+        o0, o1 = 0, obs_dim
+        self.buf_obs = self.buf[:, o0:o1]
+        self.buf_act = self.buf[:, o1:o1 + act_dim]
+        self.buf_rew = self.buf[:, o1 + act_dim]
+        self.buf_next = self.buf[:, o1 + act_dim + 1:o1 + act_dim + 1 + obs_dim]
+        self.buf_done = self.buf[:, -1]
+        self.od, self.ad = obs_dim, act_dim
         self.pos = torch.zeros((), dtype=torch.long, device=d)
         self.size = torch.zeros((), dtype=torch.long, device=d)
 
@@ -100,19 +144,18 @@ class SAC:
     def insert(self, obs, act, rew, next_obs, term):
         n = obs.shape[0]
         idx = (self.pos + torch.arange(n, device=self.dev)) % self.cap
-        self.buf_obs.index_copy_(0, idx, obs)
-        self.buf_next.index_copy_(0, idx, next_obs)
-        self.buf_act.index_copy_(0, idx, act)
-        self.buf_rew.index_copy_(0, idx, rew)
-        self.buf_done.index_copy_(0, idx, term)
+        row = torch.cat([obs.to(self.buf.dtype), act.to(self.buf.dtype), rew.to(self.buf.dtype)[:, None],
+                         next_obs.to(self.buf.dtype), term.to(self.buf.dtype)[:, None]], -1)
+        self.buf.index_copy_(0, idx, row)
         self.pos.copy_((self.pos + n) % self.cap)
         self.size.copy_(torch.clamp(self.size + n, max=self.cap))
 
     def sample(self):
         u = torch.rand(self.batch, device=self.dev)
         idx = torch.clamp((u * self.size.float()).long(), max=self.cap - 1)
-        return (self.buf_obs[idx], self.buf_act[idx], self.buf_rew[idx], self.buf_next[idx],
-                self.buf_done[idx])
+        t = self.buf[idx]
+        od, ad = self.od, self.ad
+        return (t[:, :od], t[:, od:od + ad], t[:, od + ad], t[:, od + ad + 1:2 * od + ad + 1], t[:, -1])
 
     # -------------------------------------------------------------- SAC update
     def _allreduce(self, params):
@@ -131,20 +174,26 @@ class SAC:
     def update(self):
         o, a, r, o2, d = self.sample()
         alpha = self.log_alpha.exp().detach()
+        # the actor's two evaluations of the update (next obs for the target, obs for the
+        # actor loss) in one pass: its parameters do not change in between (its optimizer
+        # steps after both); the target half is detached
+        B = o.shape[0]
+        aa, ll = self.actor(torch.cat([o2, o]))
         with torch.no_grad():
-            a2, logp2 = self.actor(o2)
+            a2, logp2 = aa[:B].detach(), ll[:B].detach()
             x2 = torch.cat([o2, a2], -1)
-            qt = torch.min(self.q1t(x2), self.q2t(x2)).squeeze(-1) - alpha * logp2
+            qt = self.qt(x2).amin(0) - alpha * logp2
             y = r + self.gamma * (1.0 - d) * qt
         x = torch.cat([o, a], -1)
-        lq = F.mse_loss(self.q1(x).squeeze(-1), y) + F.mse_loss(self.q2(x).squeeze(-1), y)
+        # F.mse_loss(q1, y) + F.mse_loss(q2, y)
+        lq = (self.q(x) - y).pow(2).mean(-1).sum()
         self.opt_q.zero_grad(set_to_none=False)
         lq.backward()
-        self._allreduce(list(self.q1.parameters()) + list(self.q2.parameters()))
+        self._allreduce(list(self.q.parameters()))
         self.opt_q.step()
-        ap, logp = self.actor(o)
+        ap, logp = aa[B:], ll[B:]
         xp = torch.cat([o, ap], -1)
-        la = (alpha * logp - torch.min(self.q1(xp), self.q2(xp)).squeeze(-1)).mean()
+        la = (alpha * logp - self.q(xp).amin(0)).mean()
         self.opt_a.zero_grad(set_to_none=False)
         la.backward()
         self._allreduce(list(self.actor.parameters()))
@@ -157,8 +206,8 @@ class SAC:
         with torch.no_grad():
             # SB3 polyak_update (target * (1 - tau), then + tau * param), as two multi-tensor
             # kernels over all target parameters instead of two kernels per tensor
-            src = list(self.q1.parameters()) + list(self.q2.parameters())
-            tgt = list(self.q1t.parameters()) + list(self.q2t.parameters())
+            src = list(self.q.parameters())
+            tgt = list(self.qt.parameters())
             torch._foreach_mul_(tgt, 1.0 - self.tau)
             torch._foreach_add_(tgt, src, alpha=self.tau)
         return lq.detach(), la.detach()
