@@ -10,6 +10,7 @@ __device__ long long g_mark[8];
 #include "../../bluesky-gym-hallucination_amd/csrc/bsg_kernels.hip"
 
 #include <cstdio>
+#include <cstdlib>
 #include <vector>
 
 #ifndef PROBE_MODE
@@ -20,9 +21,9 @@ __device__ long long g_mark[8];
 #endif
 
 constexpr int NF = 12;       // lat lon alt hdg tas cas vs ax ap_trk selspd selalt selvs, + nav
-constexpr int SMAX = 16;
+constexpr int SMAX = 32;
 
-__global__ void probe(bsg::Route route, const double* st, int S, long long* cyc, double* out) {
+__global__ void probe(bsg::Route route, const double* st, int S, double dt, long long* cyc, double* out) {
   using namespace bsg;
   const int l = threadIdx.x;
   AC s{};
@@ -49,7 +50,7 @@ __global__ void probe(bsg::Route route, const double* st, int S, long long* cyc,
   t[0] = __builtin_amdgcn_s_memtime();
   long long mk[SMAX][8];
   for (int it = 0; it < S; ++it) {
-    substep<false, PROBE_HMEMO>(s, m, 5.0, rt, w, it == 0 ? fh0 : trk_ok);
+    substep<false, PROBE_HMEMO>(s, m, dt, rt, w, it == 0 ? fh0 : trk_ok);
     t[it + 1] = __builtin_amdgcn_s_memtime();
     for (int q = 0; q < 8; ++q) mk[it][q] = g_mark[q];
   }
@@ -62,7 +63,7 @@ __global__ void probe(bsg::Route route, const double* st, int S, long long* cyc,
 }
 
 int main(int argc, char** argv) {
-  if (argc < 2) { std::printf("usage: substep_probe state.bin\n"); return 2; }
+  if (argc < 2) { std::printf("usage: substep_probe state.bin [substeps] [dt]\n"); return 2; }
   FILE* fp = std::fopen(argv[1], "rb");
   if (!fp) return 2;
   std::vector<double> hdr(1 + 3 * BSG_MAX_ROUTE), st((NF + 1) * 64);
@@ -80,10 +81,12 @@ int main(int argc, char** argv) {
   if (hipMalloc(&dst, st.size() * 8) != hipSuccess || hipMalloc(&dout, NF * 64 * 8) != hipSuccess ||
       hipMalloc(&dcyc, (SMAX + SMAX * 8) * 8) != hipSuccess) return 1;
   (void)hipMemcpy(dst, st.data(), st.size() * 8, hipMemcpyHostToDevice);
-  const int S = 10;
+  const int S = argc > 2 ? std::atoi(argv[2]) : 10;        // substeps (<= SMAX)
+  const double dt = argc > 3 ? std::atof(argv[3]) : 5.0;    // simdt
+  if (S < 2 || S > SMAX) return 2;
   std::vector<long long> best(S, 1LL << 62);
   for (int rep = 0; rep < 7; ++rep) {
-    hipLaunchKernelGGL(probe, dim3(1), dim3(64), 0, 0, route, dst, S, dcyc, dout);
+    hipLaunchKernelGGL(probe, dim3(1), dim3(64), 0, 0, route, dst, S, dt, dcyc, dout);
     std::vector<long long> c(S);
     (void)hipMemcpy(c.data(), dcyc, S * 8, hipMemcpyDeviceToHost);
     for (int i = 0; i < S; ++i) best[i] = c[i] < best[i] ? c[i] : best[i];

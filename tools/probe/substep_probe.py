@@ -1,6 +1,9 @@
-"""Dump one wave of real Merge aircraft (envs 0-1 of a 512 x 32 DeviceBatch after 30
-steps) for tools/probe/substep_probe.hip and run the probe binaries given on the
-command line (GPU box):  python tools/probe/substep_probe.py tools/probe/substep_probe [...]"""
+"""Dump one wave of real aircraft for tools/probe/substep_probe.hip and run the probe
+binaries given on the command line (GPU box):
+  python tools/probe/substep_probe.py tools/probe/substep_probe [...]           Merge: envs 0-1 of a
+      512 x 32 DeviceBatch after 30 steps, 10 substeps of 5 s
+  python tools/probe/substep_probe.py --descent tools/probe/substep_probe_d [...]   Descent: envs
+      0-63 of a 512-env batch after 20 steps, 30 substeps of 1 s"""
 import os
 import subprocess
 import sys
@@ -12,12 +15,14 @@ import torch
 from bluesky_gym import config, core
 from bluesky_gym import _native as nat
 
-cfg = config.merge_config(num_ac=32)
-b = core.DeviceBatch(cfg, 512, compute_cd=True, seed=1234)
+descent = "--descent" in sys.argv
+args = [a for a in sys.argv[1:] if a != "--descent"]
+cfg = config.descent_config() if descent else config.merge_config(num_ac=32)
+b = core.DeviceBatch(cfg, 512, compute_cd=not descent, seed=1234)
 b.reset()
 g = torch.Generator(device="cuda").manual_seed(3)
-for _ in range(30):
-    b.step(torch.rand((512, 2), dtype=torch.float64, device="cuda", generator=g) * 2 - 1)
+for _ in range(20 if descent else 30):
+    b.step(torch.rand((512, b.act_dim), dtype=torch.float64, device="cuda", generator=g) * 2 - 1)
 torch.cuda.synchronize()
 c = cfg.to_c(512, nat.AUTORESET_NEXT_STEP, True, 1234, 0, 0)
 M = nat.MAX_ROUTE
@@ -28,6 +33,7 @@ st.append(b.state["nav"].cpu().numpy().reshape(-1)[:64].astype(np.float64))
 os.makedirs("gpurun_out", exist_ok=True)
 path = "gpurun_out/substep_state.bin"
 np.concatenate([np.asarray(hdr, np.float64)] + st).astype(np.float64).tofile(path)
-for exe in sys.argv[1:]:
+extra = ["30", "1.0"] if descent else []
+for exe in args:
     print("==", exe, flush=True)
-    subprocess.run(["timeout", "-k", "5", "60", exe, path], check=True)
+    subprocess.run(["timeout", "-k", "5", "60", exe, path] + extra, check=True)
