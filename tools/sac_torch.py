@@ -24,6 +24,7 @@ data-parallel SAC with the per-rank batch 256 / world.
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 import torch.nn as nn
@@ -116,7 +117,8 @@ class SAC:
         self.target_entropy = -float(act_dim)
         # fused Adam: one kernel per parameter group instead of a foreach chain per tensor
         # (the update is launch-bound: batch 256 through 256-wide MLPs)
-        opt = dict(lr=lr, fused=True, capturable=True) if self.dev.type == "cuda" else dict(lr=lr)
+        impl = os.environ.get("SAC_ADAM", "fused")          # fused | foreach (A/B)
+        opt = dict(lr=lr, capturable=True, **{impl: True}) if self.dev.type == "cuda" else dict(lr=lr)
         self.opt_a = torch.optim.Adam(self.actor.parameters(), **opt)
         self.opt_q = torch.optim.Adam(self.q.parameters(), **opt)
         self.opt_al = torch.optim.Adam([self.log_alpha], **opt)
@@ -187,19 +189,25 @@ class SAC:
         x = torch.cat([o, a], -1)
         # F.mse_loss(q1, y) + F.mse_loss(q2, y)
         lq = (self.q(x) - y).pow(2).mean(-1).sum()
-        self.opt_q.zero_grad(set_to_none=False)
+        self.opt_q.zero_grad(set_to_none=True)
         lq.backward()
         self._allreduce(list(self.q.parameters()))
         self.opt_q.step()
         ap, logp = aa[B:], ll[B:]
         xp = torch.cat([o, ap], -1)
+        # the critics only pass the actor loss's gradient through: SB3 lets it land on
+        # their .grad too (cleared before their next step); freezing them skips that work
+        for p_ in self.q.parameters():
+            p_.requires_grad_(False)
         la = (alpha * logp - self.q(xp).amin(0)).mean()
-        self.opt_a.zero_grad(set_to_none=False)
+        self.opt_a.zero_grad(set_to_none=True)
         la.backward()
+        for p_ in self.q.parameters():
+            p_.requires_grad_(True)
         self._allreduce(list(self.actor.parameters()))
         self.opt_a.step()
         lal = -(self.log_alpha * (logp.detach() + self.target_entropy)).mean()
-        self.opt_al.zero_grad(set_to_none=False)
+        self.opt_al.zero_grad(set_to_none=True)
         lal.backward()
         self._allreduce([self.log_alpha])
         self.opt_al.step()
