@@ -41,6 +41,9 @@ for name, cfg, E, cd in [
     ("merge32_full_1024", config.merge_config(num_ac=32), 1024, True),    # C4 shard at 4 GPUs
     ("merge32_full_2048", config.merge_config(num_ac=32), 2048, True),    # C4 shard at 2 GPUs
     ("descent_512", config.descent_config(), 512, False),                 # C5 shard at 8 GPUs
+    ("merge32_nocd_512", config.merge_config(num_ac=32), 512, False),
+    ("merge32_nocd_1024", config.merge_config(num_ac=32), 1024, False),
+    ("merge32_nocd_2048", config.merge_config(num_ac=32), 2048, False),
     ("merge32_full_8192", config.merge_config(num_ac=32), 8192, True),
     ("merge32_full_16384", config.merge_config(num_ac=32), 16384, True),
 ]:
