@@ -1582,21 +1582,26 @@ __device__ __forceinline__ void propagate(const KParams& p, int e, int j, size_t
   }
 }
 
-template <int KIND, int GS, bool WIND>
-__global__ __launch_bounds__(64) void step_kernel(KParams p) {
+// CDW: waves per workgroup.  Wave 0 owns the workgroup's 64/GS envs as always; waves 1..CDW-1
+// (small batches only, launch_kind_w) take no aircraft and only share the StateBased CD's
+// pair tests and exact pairs -- a C4 shard of 512-1024 envs leaves most SIMDs idle, and
+// the CD is a serial tail after the substeps of each wave.
+template <int KIND, int GS, bool WIND, int CDW = 1>
+__global__ __launch_bounds__(64 * CDW) void step_kernel(KParams p) {
 #if defined(BSG_STAMPS) && BSG_STAMPS
   BSG_STAMP(0, __builtin_amdgcn_s_memrealtime());
   BSG_STAMP(1, stamp_clock());
 #endif
   __shared__ Lds<WIND> L;
-  const int lane = threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  const int wv = CDW > 1 ? (int)(threadIdx.x >> 6) : 0;   // CD helper waves: wv > 0
   const int ws = (WIND && p.wind.augment) ? 2 : 0;   // obs carries wind_u / wind_v
   const int g = lane / GS;
   const int j = lane % GS;
   const int base = g * GS;
   const int e = blockIdx.x * (64 / GS) + g;
   const int N = p.N;
-  const bool env_ok = e < p.E;
+  const bool env_ok = wv == 0 && e < p.E;
   const bool ok = env_ok && j < N;
   const size_t a = (size_t)e * N + j;
   const Buffers& b = p.b;
@@ -1671,7 +1676,7 @@ __global__ __launch_bounds__(64) void step_kernel(KParams p) {
       reset_scalars<KIND>(ev, aux);
       if (ev.over) ev.flags |= BSG_FLAG_SPAWN_OVERFLOW;
     }
-    stage(L, lane, s);
+    if (wv == 0) stage(L, lane, s);
   }
   __syncthreads();
 #if defined(BSG_STAMPS) && BSG_STAMPS
@@ -1697,7 +1702,7 @@ __global__ __launch_bounds__(64) void step_kernel(KParams p) {
     if (kLaneObs && on && j > 0) intr = lane_obs<KIND>(L, base, lane, o, &sortkey);
   }
   if constexpr (kRanked) {
-    L.d[lane] = sortkey;
+    if (wv == 0) L.d[lane] = sortkey;
   }
   __syncthreads();
   int rank = 0x7fffffff;
@@ -1714,18 +1719,24 @@ __global__ __launch_bounds__(64) void step_kernel(KParams p) {
   uint64_t cmask = 0, lmask = 0;
   double tmax = 0.0, msep = __builtin_inf();
   if (kLaneObs && p.cfg.compute_cd) {
-    __shared__ unsigned short cd_list[64 * (GS > 1 ? GS - 1 : 1)];
+    constexpr int kList = 64 * (GS > 1 ? GS - 1 : 1);
+    __shared__ unsigned short cd_lists[CDW * kList];
+    unsigned short* cd_list = cd_lists + wv * kList;   // this wave's work list
+    if (wv == 0) {
     L.cm[lane] = 0ull;
     L.lm[lane] = 0ull;
     L.tmax[lane] = 0ull;                                   // bits of +0.0
     L.gmin[lane] = bits(__builtin_inf());
+    }
     // phase 1: candidate pairs (no transcendentals).  The bound is symmetric in (i, k)
     // bit for bit, so each unordered pair is tested once: lane j takes the ring offsets
     // 1..nac/2 (16 per lane at N = 32, balanced).  (The LDS rows above are first touched
     // by phase 2's atomics, after the work-list barrier.)
-    const int nac = ev.nac;
+    // helper waves test wave 0's aircraft (fixed count N: CDW > 1 only for Merge)
+    const int nac = CDW > 1 ? N : ev.nac;
+    const bool cd_on = CDW > 1 ? ((int)blockIdx.x * (64 / GS) + g < p.E && j < N) : on;
     uint64_t mine = 0;                   // bit sft-1: pair (j, j + sft) is a candidate
-    if (on) {
+    if (cd_on) {
       const float4 pi = L.fpk[lane];
       const float flati = pi.x, floni = pi.y, fui = pi.z, fvi = pi.w;
       const float fali = fabsf(flati);
@@ -1733,7 +1744,7 @@ __global__ __launch_bounds__(64) void step_kernel(KParams p) {
       // together)
       const int nsft = (nac & 1) ? nac / 2 : (j < nac / 2 ? nac / 2 : nac / 2 - 1);
 #pragma unroll 4
-      for (int sft = 1; sft <= nsft; ++sft) {
+      for (int sft = 1 + wv; sft <= nsft; sft += CDW) {
         int k = j + sft;
         if (k >= nac) k -= nac;
         const float4 pk = L.fpk[base + k];
@@ -2018,6 +2029,23 @@ static hipError_t launch_kind_w(const KParams& p, hipStream_t st) {
   const int grid = (p.E + epb - 1) / epb;
 #define BSG_CASE(G) \
   case G: hipLaunchKernelGGL((step_kernel<KIND, G, WIND>), dim3(grid), dim3(64), p.lds_pad, st, p); break;
+  if constexpr (KIND == BSG_ENV_MERGE && !WIND) {
+    // small batches (C4's per-GPU shards): CD helper waves while the workgroups, at 2..4
+    // waves each, still fit the 2 waves per SIMD the step kernel's VGPRs allow on 1,024
+    // SIMDs -- 512 envs x 32: 256 workgroups x 4 waves, 1,024 envs: 512 x 4, 2,048: 1,024 x 2
+    const int cdw = (!p.cfg.compute_cd || gs < 32) ? 1 : (grid <= 512 ? 4 : (grid <= 1024 ? 2 : 1));
+#define BSG_CASE_CD(G, W) \
+  case G: hipLaunchKernelGGL((step_kernel<KIND, G, WIND, W>), dim3(grid), dim3(64 * W), p.lds_pad, st, p); break;
+    if (cdw == 4) {
+      switch (gs) { BSG_CASE_CD(32, 4) BSG_CASE_CD(64, 4) default: return hipErrorInvalidValue; }
+      return hipGetLastError();
+    }
+    if (cdw == 2) {
+      switch (gs) { BSG_CASE_CD(32, 2) BSG_CASE_CD(64, 2) default: return hipErrorInvalidValue; }
+      return hipGetLastError();
+    }
+#undef BSG_CASE_CD
+  }
   if constexpr (KIND == BSG_ENV_DESCENT || KIND == BSG_ENV_STATIC_OBSTACLE ||
                 KIND == BSG_ENV_PLAN_WAYPOINT) {
     switch (gs) { BSG_CASE(1) default: return hipErrorInvalidValue; }        // one aircraft
