@@ -14,20 +14,62 @@ import numpy as np
 import torch
 
 from . import _native as nat
-from .vector import BlueSkyVectorEnv, DescentVectorEnv, MergeVectorEnv, VerticalCRVectorEnv
+from .vector import (BlueSkyVectorEnv, DescentVectorEnv, HorizontalCRVectorEnv, MergeVectorEnv,
+                     PlanWaypointVectorEnv, SectorCRVectorEnv, StaticObstacleVectorEnv,
+                     VerticalCRVectorEnv)
 
 try:  # pragma: no cover
     from stable_baselines3.common.vec_env import VecEnv as _SB3Base
 except ImportError:
     _SB3Base = object
 
-_VEC = {"MergeEnv-v0": MergeVectorEnv, "VerticalCREnv-v0": VerticalCRVectorEnv,
-        "DescentEnv-v0": DescentVectorEnv}
+VECTOR_ENVS = {"MergeEnv-v0": MergeVectorEnv, "VerticalCREnv-v0": VerticalCRVectorEnv,
+               "DescentEnv-v0": DescentVectorEnv, "HorizontalCREnv-v0": HorizontalCRVectorEnv,
+               "StaticObstacleEnv-v0": StaticObstacleVectorEnv,
+               "SectorCREnv-v0": SectorCRVectorEnv, "PlanWaypointEnv-v0": PlanWaypointVectorEnv}
+
+
+def episode_infos(venv: BlueSkyVectorEnv, dones, term, trunc):
+    """Per-env info dicts after a SAME_STEP launch: the running info of every env, and for
+    an env that finished (and was already respawned) its finished episode's info from
+    ep_info (merge_env.py:238-244; vertical_cr_env.py:203-211; descent_env.py:119-126)."""
+    b = venv.batch
+    kind = venv.kind_cfg.kind
+    cur = venv._infos(done=None)
+    cur.pop("conflicts", None)
+    keys = list(cur)
+    ep = b.ep_info.cpu().numpy() if dones.any() else None
+    infos = []
+    for i in range(venv.num_envs):
+        d = {k: cur[k][i].item() for k in keys}
+        if dones[i]:
+            d["total_reward"] = float(ep[i, 0])
+            if kind == nat.ENV_MERGE:
+                d["total_intrusions"] = int(ep[i, 1])
+                d["faf_reach"] = int(ep[i, 2])
+                d["average_drift"] = float(ep[i, 3])
+            elif kind == nat.ENV_VERTICAL_CR:
+                d["total_intrusions"] = int(ep[i, 1])
+                d["final_altitude"] = float(ep[i, 2])
+            elif kind in (nat.ENV_HORIZONTAL_CR, nat.ENV_SECTOR_CR):
+                d["total_intrusions"] = int(ep[i, 1])
+                d["average_drift"] = float(ep[i, 2])
+            elif kind == nat.ENV_STATIC_OBSTACLE:
+                d["waypoint_reached"] = int(ep[i, 1])
+                d["crashed"] = int(ep[i, 2])
+                d["average_drift"] = float(ep[i, 3])
+            elif kind == nat.ENV_PLAN_WAYPOINT:
+                d["waypoints_completed"] = int(ep[i, 2])
+            else:
+                d["final_altitude"] = float(ep[i, 2])
+            d["TimeLimit.truncated"] = bool(trunc[i] and not term[i])
+        infos.append(d)
+    return infos
 
 
 class SB3VecEnv(_SB3Base):
     def __init__(self, env_id: str, num_envs: int, *, seed=0, device=None, **env_kwargs):
-        self.venv: BlueSkyVectorEnv = _VEC[env_id](
+        self.venv: BlueSkyVectorEnv = VECTOR_ENVS[env_id](
             num_envs=num_envs, seed=seed, device=device, autoreset=nat.AUTORESET_SAME_STEP,
             **env_kwargs)
         self.num_envs = num_envs
@@ -35,7 +77,6 @@ class SB3VecEnv(_SB3Base):
         self.action_space = self.venv.single_action_space
         self.render_mode = None
         self._actions = None
-        self._kind = self.venv.kind_cfg.kind
 
     # ------------------------------------------------------------------ SB3 API
     def reset(self):
@@ -66,36 +107,7 @@ class SB3VecEnv(_SB3Base):
         return self.step_wait()
 
     def _infos(self, dones, term, trunc):
-        b = self.venv.batch
-        cur = self.venv._infos(done=None)
-        cur.pop("conflicts", None)
-        keys = list(cur)
-        ep = b.ep_info.cpu().numpy() if dones.any() else None
-        infos = []
-        for i in range(self.num_envs):
-            d = {k: cur[k][i].item() for k in keys}
-            if dones[i]:
-                # the finished episode's info (the env has already been reset)
-                d["total_reward"] = float(ep[i, 0])
-                if self._kind == nat.ENV_MERGE:
-                    d["total_intrusions"] = int(ep[i, 1])
-                    d["faf_reach"] = int(ep[i, 2])
-                    d["average_drift"] = float(ep[i, 3])
-                elif self._kind == nat.ENV_VERTICAL_CR:
-                    d["total_intrusions"] = int(ep[i, 1])
-                    d["final_altitude"] = float(ep[i, 2])
-                elif self._kind in (nat.ENV_HORIZONTAL_CR, nat.ENV_SECTOR_CR):
-                    d["total_intrusions"] = int(ep[i, 1])
-                    d["average_drift"] = float(ep[i, 2])
-                elif self._kind == nat.ENV_STATIC_OBSTACLE:
-                    d["waypoint_reached"] = int(ep[i, 1])
-                    d["crashed"] = int(ep[i, 2])
-                    d["average_drift"] = float(ep[i, 3])
-                else:
-                    d["final_altitude"] = float(ep[i, 2])
-                d["TimeLimit.truncated"] = bool(trunc[i] and not term[i])
-            infos.append(d)
-        return infos
+        return episode_infos(self.venv, dones, term, trunc)
 
     def close(self):
         self.venv.close()

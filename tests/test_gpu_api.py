@@ -112,6 +112,51 @@ def test_sb3_vecenv_terminal_observation_and_infos():
     env.close()
 
 
+@pytest.mark.parametrize("env_id,kw,A", [("MergeEnv-v0", dict(num_ac=32, max_episode_steps=12), 2),
+                                         ("DescentEnv-v0", dict(max_episode_steps=15), 1),
+                                         ("PlanWaypointEnv-v0", dict(max_episode_steps=15), 1)])
+def test_rllib_vector_env_matches_sb3_adapter(env_id, kw, A):
+    """RLlib's legacy VectorEnv contract on the device batch: vector_step reports a finished
+    env's terminal observation and reset_at(i) its next episode's first observation -- the
+    same values SB3's adapter reports as infos["terminal_observation"] and obs on the same
+    seed (both run SAME_STEP autoreset on one kernel); episode infos agree."""
+    from bluesky_gym.rllib import RLlibVectorEnv
+    from bluesky_gym.sb3 import SB3VecEnv
+    E = 128
+    rl = RLlibVectorEnv(env_id, E, seed=4, **kw)
+    sb = SB3VecEnv(env_id, E, seed=4, **kw)
+    obs_rl, infos = rl.vector_reset()
+    obs_sb = sb.reset()
+    keys = sorted(obs_sb)
+    assert len(obs_rl) == E and len(infos) == E
+    for i in (0, E - 1):
+        assert np.array_equal(flat(obs_rl[i], keys), flat({k: v[i] for k, v in obs_sb.items()}, keys))
+    rng = np.random.default_rng(6)
+    n_done = 0
+    for t in range(40):
+        a = rng.uniform(-1, 1, (E, A))
+        o_rl, r_rl, te, tr, inf_rl = rl.vector_step(a)
+        o_sb, r_sb, d_sb, inf_sb = sb.step(a)
+        assert np.array_equal(np.asarray(r_rl, np.float32), r_sb)
+        assert np.array_equal(np.asarray(te) | np.asarray(tr), d_sb)
+        for i in range(E):
+            if d_sb[i]:
+                n_done += 1
+                assert np.array_equal(flat(o_rl[i], keys), flat(inf_sb[i]["terminal_observation"], keys))
+                assert inf_rl[i]["total_reward"] == inf_sb[i]["total_reward"]
+                o_new, _ = rl.reset_at(i)
+                assert np.array_equal(flat(o_new, keys), flat({k: v[i] for k, v in o_sb.items()}, keys))
+            elif i % 17 == 0:
+                assert np.array_equal(flat(o_rl[i], keys), flat({k: v[i] for k, v in o_sb.items()}, keys))
+    assert n_done > 0
+    # an env that did not finish is reset by a masked reset launch
+    o5, _ = rl.reset_at(5)
+    assert all(np.all(np.isfinite(v)) for v in o5.values())
+    assert int(rl.venv.batch.envs["step_count"][5]) == 0
+    rl.close()
+    sb.close()
+
+
 def test_shards_equal_one_big_batch():
     """Global env ids (env_offset) make two 128-env shards identical to one 256 batch."""
     from bluesky_gym import config, core
