@@ -143,6 +143,8 @@ def main():
                     help="merge: the BASELINE metric (default); descent-sac: BASELINE configs[4], "
                          "DescentEnv-v0 with the SAC learner in the loop")
     ap.add_argument("--no-graph", action="store_true", help="descent-sac: eager, no HIP graph")
+    ap.add_argument("--torch-policy", action="store_true",
+                    help="descent-sac: sample actions with the torch actor instead of bsg_policy_sac")
     ap.add_argument("--blas", default="cublas", choices=("default", "cublas", "cublaslt"),
                     help="descent-sac: torch.backends.cuda.preferred_blas_library for the learner's "
                          "GEMMs (cublas = rocBLAS/hipBLAS on ROCm, cublaslt = hipBLASLt)")
@@ -308,7 +310,7 @@ def main():
 
 def bench_descent_sac(args):
     """BASELINE configs[4]: DescentEnv-v0 x 4096 envs (4096/N per rank) with the learner in
-    the loop (scripts/descent_env_sac.py:25-34: SB3 SAC, MultiInputPolicy, lr 3e-4, batch
+    the loop (scripts/descent_env_sac.py:25-34: SB3 SAC, MultiInputPolicy, lr 1e-3, batch
     256, buffer 1e6, train_freq 1, gradient_steps 1).  Three rates over the same envs:
     env only (U(-1,1) actions from HBM), env + policy (the reference's saved SAC actor,
     stochastic, forward on the kernel's fp32 obs rows), env + policy + one SAC update per
@@ -344,7 +346,7 @@ def bench_descent_sac(args):
     b.reset()
     W = dict(np.load(os.path.join(REPO, "tests", "golden", "sac_actors.npz")))
     sac = sac_torch.SAC(b.obs_dim, b.act_dim, dev, group=dist.group.WORLD if world > 1 else None,
-                        seed=rank)
+                        seed=rank, lr=1e-3)
     sac.actor.load_sb3(W, "descent")
     gen = torch.Generator(device=dev)
     gen.manual_seed(17 + rank)
@@ -373,12 +375,18 @@ def bench_descent_sac(args):
 
     el_env = timed(lambda k: b.step(bank[k % 16]), args.steps)
     graph = world == 1 and not args.no_graph
-    pol = sac_torch.RLLoop(b, sac, learn=False)
-    pol.obs.copy_(b.obs)
-    if graph:
-        pol.capture()
-    el_pol = timed((lambda k: pol.replay()) if graph else (lambda k: pol.step()), args.steps)
-    rl = sac_torch.RLLoop(b, sac, learn=True)
+    fused = not args.torch_policy
+
+    def policy_loop(fused_policy):
+        pol = sac_torch.RLLoop(b, sac, learn=False, fused_policy=fused_policy)
+        pol.obs.copy_(b.obs)
+        if graph:
+            pol.capture()
+        return timed((lambda k: pol.replay()) if graph else (lambda k: pol.step()), args.steps)
+
+    el_pol = policy_loop(fused)
+    el_pol_torch = policy_loop(False) if fused else el_pol
+    rl = sac_torch.RLLoop(b, sac, learn=True, fused_policy=fused)
     rl.obs.copy_(b.obs)
     for _ in range(8):                                # fill the buffer past one batch
         rl.step()
@@ -409,9 +417,13 @@ def bench_descent_sac(args):
                        "envs_total": world * E, "envs_per_gpu": E,
                        "parallelism": f"env-shard x{world}" + (" + RCCL gradient all_reduce "
                                                                "(data-parallel SAC)" if world > 1 else ""),
+                       "policy": "fused HIP actor (bsg_policy_sac)" if fused else "torch actor",
                        "hip_graph": graph, "blas": str(torch.backends.cuda.preferred_blas_library())},
             "env_only": {"value": total / el_env, "ms_per_step": el_env * 1e3 / args.steps},
-            "env_policy": {"value": total / el_pol, "ms_per_step": el_pol * 1e3 / args.steps},
+            "env_policy": {"value": total / el_pol, "ms_per_step": el_pol * 1e3 / args.steps,
+                           "policy": "fused HIP actor (bsg_policy_sac)" if fused else "torch actor"},
+            "env_policy_torch_actor": {"value": total / el_pol_torch,
+                                       "ms_per_step": el_pol_torch * 1e3 / args.steps},
             "env_policy_learner": {"value": total / el_rl, "ms_per_step": el_rl * 1e3 / args.steps,
                                    "critic_loss": float(lq), "actor_loss": float(la)},
         }

@@ -91,8 +91,15 @@ EXPORTED_SYMBOLS = (
     "bsg_abi_version", "bsg_last_error", "bsg_obs_dim", "bsg_action_dim", "bsg_spawn_width",
     "bsg_create", "bsg_destroy", "bsg_bind", "bsg_reset", "bsg_step", "bsg_set_timing",
     "bsg_step_timing", "bsg_set_stamps", "bsg_set_wind", "bsg_ctx_obs_dim", "bsg_geom_width",
-    "bsg_set_learner",
+    "bsg_set_learner", "bsg_policy_sac",
 )
+
+
+class BsgSacActor(C.Structure):
+    """include/bsg.h bsg_sac_actor: device pointers of an SB3 SAC actor's weights."""
+    _fields_ = [("obs_dim", C.c_int32), ("act_dim", C.c_int32), ("hidden", C.c_int32),
+                ("reserved", C.c_int32)] + [(n, C.c_void_p) for n in (
+                    "w0", "b0", "w1", "b1", "w_mu", "b_mu", "w_ls", "b_ls")]
 
 _lib = None
 
@@ -147,6 +154,9 @@ def load_library(path: str | None = None):
     lib.bsg_set_wind.argtypes = [C.c_void_p, C.POINTER(BsgWind)]
     lib.bsg_ctx_obs_dim.restype = C.c_int32
     lib.bsg_ctx_obs_dim.argtypes = [C.c_void_p]
+    lib.bsg_policy_sac.restype = C.c_int32
+    lib.bsg_policy_sac.argtypes = [C.POINTER(BsgSacActor), C.c_void_p, C.c_int32, C.c_int32,
+                                   C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
     if lib.bsg_abi_version() != ABI_VERSION:
         raise BsgError(f"libbsg ABI {lib.bsg_abi_version()} != expected {ABI_VERSION}")
     if path is None:

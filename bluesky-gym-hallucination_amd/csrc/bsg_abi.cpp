@@ -376,6 +376,31 @@ int32_t bsg_ctx_obs_dim(const bsg_ctx* c) {
   return c->obs_dim;
 }
 
+int32_t bsg_policy_sac(const bsg_sac_actor* w, const float* obs, int32_t num_envs,
+                       int32_t obs_stride, const float* eps, double* actions, float* log_prob,
+                       void* stream) {
+  if (!w) return fail(BSG_E_INVALID_ARG, "bsg_policy_sac: null actor%s%lld");
+  if (num_envs > 0 && (!obs || !actions)) return fail(BSG_E_INVALID_ARG, "bsg_policy_sac: null obs/actions%s%lld");
+  if (w->hidden != 256)
+    return fail(BSG_E_INVALID_ARG, "bsg_policy_sac: hidden must be 256%s (got %lld)", "", w->hidden);
+  if (w->obs_dim < 1 || w->obs_dim > 256)
+    return fail(BSG_E_INVALID_ARG, "bsg_policy_sac: obs_dim must be in [1, 256]%s (got %lld)", "", w->obs_dim);
+  if (w->act_dim < 1 || w->act_dim > 4)
+    return fail(BSG_E_INVALID_ARG, "bsg_policy_sac: act_dim must be in [1, 4]%s (got %lld)", "", w->act_dim);
+  if (num_envs < 0) return fail(BSG_E_INVALID_ARG, "bsg_policy_sac: num_envs < 0%s%lld");
+  if (obs_stride < w->obs_dim)
+    return fail(BSG_E_INVALID_ARG, "bsg_policy_sac: obs_stride < obs_dim%s (%lld)", "", obs_stride);
+  if (!w->w0 || !w->b0 || !w->w1 || !w->b1 || !w->w_mu || !w->b_mu || !w->w_ls || !w->b_ls)
+    return fail(BSG_E_INVALID_ARG, "bsg_policy_sac: null weight pointer%s%lld");
+  if (reinterpret_cast<uintptr_t>(w->w1) & 15)
+    return fail(BSG_E_INVALID_ARG, "bsg_policy_sac: w1 must be 16-byte aligned%s%lld");
+  if (num_envs == 0) return BSG_OK;
+  hipError_t e = bsg::launch_sac_actor(*w, obs, num_envs, obs_stride, eps, actions, log_prob,
+                                       static_cast<hipStream_t>(stream));
+  if (e != hipSuccess) return hip_fail(e, "bsg_policy_sac launch");
+  return BSG_OK;
+}
+
 int32_t bsg_set_stamps(bsg_ctx* c, void* buf) {
   if (!c) return fail(BSG_E_INVALID_ARG, "bsg_set_stamps: null ctx%s%lld");
 #if defined(BSG_STAMPS) && BSG_STAMPS

@@ -55,4 +55,8 @@ hipError_t launch_kind_4(const KParams& p, hipStream_t stream);
 hipError_t launch_kind_5(const KParams& p, hipStream_t stream);
 hipError_t launch_kind_6(const KParams& p, hipStream_t stream);
 
+// the fused SAC actor (bsg_policy.hip)
+hipError_t launch_sac_actor(const bsg_sac_actor& w, const float* obs, int E, int ostride,
+                            const float* eps, double* act, float* logp, hipStream_t stream);
+
 }  // namespace bsg

@@ -255,6 +255,33 @@ int32_t bsg_step_timing(bsg_ctx* ctx, double* total_ms, int32_t* launches);
  * writes them; otherwise returns BSG_E_UNSUPPORTED.  Never used on the measured path. */
 int32_t bsg_set_stamps(bsg_ctx* ctx, void* device_buf);
 
+/* Device policy: the weights of an SB3 SAC actor (MultiInputPolicy, net_arch [256, 256]:
+ * latent_pi.0, latent_pi.2, mu, log_std; nn.Linear layout [out, in], fp32, device memory;
+ * w1 16-byte aligned).  The caller owns them; a learner may update them in place. */
+typedef struct bsg_sac_actor {
+  int32_t obs_dim;           /* 1..256 */
+  int32_t act_dim;           /* 1..4 */
+  int32_t hidden;            /* must be 256 */
+  int32_t reserved;
+  const float *w0, *b0;      /* [hidden, obs_dim], [hidden] */
+  const float *w1, *b1;      /* [hidden, hidden], [hidden] */
+  const float *w_mu, *b_mu;  /* [act_dim, hidden], [act_dim] */
+  const float *w_ls, *b_ls;  /* [act_dim, hidden], [act_dim] */
+} bsg_sac_actor;
+
+/* Replaces: model.predict(obs, deterministic=True) (reference main.py:54,
+ * scripts/multi_processing_example.py:70) and the per-step action sampling of SB3 SAC's
+ * collect_rollouts (Actor.action_log_prob, stable_baselines3 2.x sac/policies.py; the
+ * library is not vendored in the reference) for a whole batch, as one kernel:
+ * a = tanh(mu + exp(clamp(log_std, -20, 2)) * eps) with eps: device fp32 [E, act_dim]
+ * standard normals (NULL = deterministic, a = tanh(mu)).  obs: device fp32 rows of
+ * `obs_stride` floats (the step kernel's obs, or learner rows).  actions: device f64
+ * [E, act_dim] (what bsg_step reads).  log_prob: optional device fp32 [E] (SB3's
+ * log_prob with the tanh correction).  Asynchronous on `stream`; capturable in a graph. */
+int32_t bsg_policy_sac(const bsg_sac_actor* actor, const float* obs, int32_t num_envs,
+                       int32_t obs_stride, const float* eps, double* actions, float* log_prob,
+                       void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -101,3 +101,29 @@ def test_empty_batch_and_bad_timing_interval_rejected():
     assert lib.bsg_create(C.byref(cfg), C.byref(ctx)) == -1
     assert b"num_envs" in lib.bsg_last_error()
     assert lib.bsg_set_timing(None, -1) == -1
+
+
+def test_policy_host_validation_without_gpu():
+    """The fused SAC actor's host layer: no CPU fallback, and the C entry point rejects bad
+    shapes before touching a device."""
+    import ctypes as C
+    import numpy as np
+    from bluesky_gym.policy import SACPolicy
+    with np.load(os.path.join(os.path.dirname(__file__), "golden", "sac_actors.npz")) as z:
+        W = {k.split("/", 1)[1]: z[k] for k in z.files if k.startswith("descent/") and "/log" not in k
+             and not k.endswith("obs_dim")}
+    with pytest.raises(nat.BsgError):
+        SACPolicy(W, "cpu")
+    lib = nat.load_library()
+    buf = (C.c_float * 70000)()
+    p = C.cast(buf, C.c_void_p).value
+    w = nat.BsgSacActor(4, 1, 128, 0, *([p] * 8))        # hidden must be 256
+    act = (C.c_double * 8)()
+    rc = lib.bsg_policy_sac(C.byref(w), p, 8, 4, None, C.cast(act, C.c_void_p), None, None)
+    assert rc == -1                                      # BSG_E_INVALID_ARG
+    assert b"hidden" in lib.bsg_last_error()
+    w = nat.BsgSacActor(4, 5, 256, 0, *([p] * 8))        # act_dim <= 4
+    assert lib.bsg_policy_sac(C.byref(w), p, 8, 4, None, C.cast(act, C.c_void_p), None, None) == -1
+    w = nat.BsgSacActor(4, 1, 256, 0, *([p] * 8))
+    assert lib.bsg_policy_sac(C.byref(w), p, 8, 3, None, C.cast(act, C.c_void_p), None, None) == -1
+    assert lib.bsg_policy_sac(C.byref(w), p, 0, 4, None, C.cast(act, C.c_void_p), None, None) == 0

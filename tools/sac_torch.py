@@ -6,7 +6,8 @@ stable-baselines3 is not installed here; this restates the part of SB3 2.x SAC t
 per environment step with the hyper-parameters of the reference's training script
 (scripts/descent_env_sac.py:25-34 -> SB3 defaults): MultiInputPolicy (the Dict obs
 flattened in sorted-key order = the kernel's flat rows), actor and twin critics
-Linear-ReLU 256-256, squashed Gaussian with log_std clamped to [-20, 2], Adam lr 3e-4,
+Linear-ReLU 256-256, squashed Gaussian with log_std clamped to [-20, 2], Adam (lr 1e-3 in
+the reference script, descent_env_sac.py:29),
 batch 256, buffer 1e6, gamma 0.99, tau 0.005, entropy coefficient 'auto' (target
 entropy -dim(A)), train_freq 1 / gradient_steps 1 -- one gradient step per vector step.
 
@@ -225,17 +226,28 @@ class RLLoop:
     """One RL iteration over a core.DeviceBatch in SAME_STEP mode (final_obs on) with
     the SAC above; step() runs it eagerly, capture() records it as one HIP graph."""
 
-    def __init__(self, batch, sac: SAC, learn=True):
+    def __init__(self, batch, sac: SAC, learn=True, fused_policy=False):
         self.b, self.sac, self.learn = batch, sac, learn
         self.obs = batch.obs.clone()
         self.act = torch.zeros((batch.E, batch.act_dim), dtype=torch.float64, device=batch.device)
         self.graph = None
+        # fused_policy: the action sample is one HIP kernel (bluesky_gym.policy.SACPolicy,
+        # bsg_policy_sac) reading the live actor's parameters, instead of ~25 torch kernels
+        self.pol = None
+        if fused_policy:
+            from bluesky_gym.policy import SACPolicy
+            self.pol = SACPolicy.from_module(sac.actor)
+            self.eps = torch.zeros((batch.E, batch.act_dim), dtype=torch.float32, device=batch.device)
 
     def step(self):
         b, s = self.b, self.sac
-        with torch.no_grad():
-            a, _ = s.actor(self.obs)
-        self.act.copy_(a)
+        if self.pol is not None:
+            torch.randn(self.eps.shape, device=self.eps.device, out=self.eps)
+            a = self.pol(self.obs, self.eps, out=self.act)
+        else:
+            with torch.no_grad():
+                a, _ = s.actor(self.obs)
+            self.act.copy_(a)
         b.step(self.act)
         done = (b.terminated | b.truncated).bool()
         if self.learn:
