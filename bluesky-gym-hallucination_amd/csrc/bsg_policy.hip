@@ -11,86 +11,107 @@
 // log_prob = sum_a [-eps^2/2 - log_std - log(2 pi)/2] - sum_a log(1 - a^2 + 1e-6).
 //
 // In torch that is ~25 kernels of 3-9 us each per vector step (the policy's whole cost at
-// 4096 envs is launch-bound, not arithmetic: 0.54 GFLOP).  Here: one workgroup of 256
-// threads per 16 envs; thread j owns hidden unit j for the workgroup's 16 rows, so each
+// 4096 envs is launch-bound, not arithmetic: 0.54 GFLOP).  Here: one workgroup of 512
+// threads per 16 envs; a thread owns a hidden unit for 8 of the workgroup's rows, so each
 // weight element is read once per workgroup (the 257 KB of weights stay in L2) and each
-// LDS activation read is a wave-wide broadcast.  fp32 FMA throughout (the MLP's dtype);
-// no MFMA: the batch-16 tile of a 256 x 256 layer is 1 M FMA per workgroup, below the
-// launch cost it replaces.
+// LDS activation read is a wave-wide broadcast.  fp32 throughout (the MLP's dtype): the
+// 256 x 256 layer on the matrix cores (f32-input MFMA, exact fp32 products, 16 x 16 tiles =
+// the workgroup's 16 rows), the small first layer and the heads on the VALU.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "bsg_internal.h"
 
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
 namespace {
 
 constexpr int H = 256;       // hidden width (SB3 default net_arch for SAC)
-constexpr int R = 16;        // env rows per workgroup
+constexpr int NT = 512;      // threads per workgroup: 8 waves, two per SIMD (hide the L2 latency of W1)
+constexpr int R = 16;        // env rows per workgroup (= the MFMA tile's 16 rows)
 constexpr int OMAX = 256;    // widest observation row handled
 constexpr int AMAX = 4;      // widest action
+constexpr int HS = H + 4;    // s_h row stride (16-B aligned rows, float4 reads spread over banks)
 constexpr int XS = OMAX + 1; // s_x row stride (the heads read 4 rows per wave: no bank aliasing)
 
-__global__ __launch_bounds__(H) void sac_actor_kernel(bsg_sac_actor w, const float* __restrict__ obs,
+__global__ __launch_bounds__(NT) void sac_actor_kernel(bsg_sac_actor w, const float* __restrict__ obs,
                                                      int E, int ostride, const float* __restrict__ eps,
                                                      double* __restrict__ act, float* __restrict__ logp) {
   __shared__ float s_x[R * XS];     // observation rows, then layer-1 activations
-  __shared__ float s_h[R * H];      // layer-0 activations
+  __shared__ float s_h[R * HS];     // layer-0 activations
   const int j = threadIdx.x;
   const int row0 = blockIdx.x * R;
   const int O = w.obs_dim, A = w.act_dim;
   const int nrow = min(R, E - row0);
 
   // stage the observation tile (rows past E read as 0; their outputs are never stored)
-  for (int i = j; i < R * O; i += H) {
+  for (int i = j; i < R * O; i += NT) {
     const int r = i / O, k = i - r * O;
     s_x[r * XS + k] = r < nrow ? obs[(size_t)(row0 + r) * ostride + k] : 0.0f;
   }
   __syncthreads();
 
-  float acc[R];
-  // layer 0: [R, O] x [O, H]
+  // layer 0: [R, O] x [O, H]; thread j owns hidden unit j % H for rows 8 (j / H) .. + 7
   {
-    const float b = w.b0[j];
+    constexpr int RH = R * H / NT;
+    const int col = j & (H - 1), rb = (j / H) * RH;
+    float acc[RH];
+    const float b = w.b0[col];
 #pragma unroll
-    for (int r = 0; r < R; ++r) acc[r] = b;
-    const float* wr = w.w0 + (size_t)j * O;
+    for (int r = 0; r < RH; ++r) acc[r] = b;
+    const float* wr = w.w0 + (size_t)col * O;
     for (int k = 0; k < O; ++k) {
       const float wk = wr[k];
 #pragma unroll
-      for (int r = 0; r < R; ++r) acc[r] = __builtin_fmaf(s_x[r * XS + k], wk, acc[r]);
+      for (int r = 0; r < RH; ++r) acc[r] = __builtin_fmaf(s_x[(rb + r) * XS + k], wk, acc[r]);
     }
 #pragma unroll
-    for (int r = 0; r < R; ++r) s_h[r * H + j] = fmaxf(acc[r], 0.0f);
+    for (int r = 0; r < RH; ++r) s_h[(rb + r) * HS + col] = fmaxf(acc[r], 0.0f);
   }
   __syncthreads();
-  // layer 1: [R, H] x [H, H]; weight row j (nn.Linear [out, in]) read as float4 along k
+  // layer 1: [R, H] x [H, H] on the matrix cores (v_mfma_f32_16x16x4_f32: exact fp32
+  // products, fp32 accumulation -- the VALU form of this loop was bound by the LDS broadcast
+  // of the activations, one ds_read_b128 per 4 FMAs).  Wave v owns the output columns
+  // [32v, 32v + 32) as two 16 x 16 tiles.  Lane l (m = l & 15, g = l >> 4) supplies
+  // A[m][k] = h0[m][k] and B[k][n] = W1[n][k] for n = 64v + 16t + m; over a 16-wide k block
+  // the lane's k slot g covers k0 + 4g .. k0 + 4g + 3 (one float4 of h0 from LDS, one float4
+  // of W1's row n from L2), consumed one component per MFMA -- a permutation of the k sum.
+  constexpr int TW = H / 16 / (NT / 64);   // tiles per wave
+  f32x4 c[TW];
   {
-    const float b = w.b1[j];
+    const int lane = j & 63, wv = j >> 6, m = lane & 15, g = lane >> 4;
 #pragma unroll
-    for (int r = 0; r < R; ++r) acc[r] = b;
-    const float4* wr = reinterpret_cast<const float4*>(w.w1 + (size_t)j * H);
+    for (int t = 0; t < TW; ++t) c[t] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    const float* wrow = w.w1 + (size_t)(16 * TW * wv + m) * H + 4 * g;
 #pragma unroll 4
-    for (int k4 = 0; k4 < H / 4; ++k4) {
-      const float4 wk = wr[k4];
+    for (int k0 = 0; k0 < H; k0 += 16) {
+      const float4 av = *reinterpret_cast<const float4*>(&s_h[m * HS + k0 + 4 * g]);
+      float4 bv[TW];
 #pragma unroll
-      for (int r = 0; r < R; ++r) {
-        const float4 x = *reinterpret_cast<const float4*>(&s_h[r * H + 4 * k4]);
-        float a = acc[r];
-        a = __builtin_fmaf(x.x, wk.x, a);
-        a = __builtin_fmaf(x.y, wk.y, a);
-        a = __builtin_fmaf(x.z, wk.z, a);
-        a = __builtin_fmaf(x.w, wk.w, a);
-        acc[r] = a;
+      for (int t = 0; t < TW; ++t) bv[t] = *reinterpret_cast<const float4*>(wrow + (size_t)16 * t * H + k0);
+#pragma unroll
+      for (int t = 0; t < TW; ++t) {
+        c[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.x, bv[t].x, c[t], 0, 0, 0);
+        c[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.y, bv[t].y, c[t], 0, 0, 0);
+        c[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.z, bv[t].z, c[t], 0, 0, 0);
+        c[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.w, bv[t].w, c[t], 0, 0, 0);
       }
     }
-  }
-  // s_x is free once layer 0 has read it (the barrier above): layer-1 activations go there
+    // D[row = 4g + i][col = m] of tile t is h1 before bias/ReLU; s_x is free once layer 0
+    // has read it (the barrier above)
 #pragma unroll
-  for (int r = 0; r < R; ++r) s_x[r * XS + j] = fmaxf(acc[r], 0.0f);
+    for (int t = 0; t < TW; ++t) {
+      const int n = 16 * TW * wv + 16 * t + m;
+      const float b = w.b1[n];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) s_x[(4 * g + i) * XS + n] = fmaxf(c[t][i] + b, 0.0f);
+    }
+  }
   __syncthreads();
 
-  // heads: thread (r = j / 16, q = j % 16) sums k = q, q + 16, ... for each of the 2A outputs,
+  // heads (the first 256 threads): thread (r = j / 16, q = j % 16) sums k = q, q + 16, ... for each of the 2A outputs,
   // then the 16 lanes of the row reduce by xor-shuffles (all within one wave)
+  if (j >= R * 16) return;
   const int r = j >> 4, q = j & 15;
   float out[2 * AMAX];
 #pragma unroll
@@ -131,7 +152,7 @@ namespace bsg {
 hipError_t launch_sac_actor(const bsg_sac_actor& w, const float* obs, int E, int ostride,
                             const float* eps, double* act, float* logp, hipStream_t stream) {
   const int grid = (E + R - 1) / R;
-  hipLaunchKernelGGL(sac_actor_kernel, dim3(grid), dim3(H), 0, stream, w, obs, E, ostride, eps,
+  hipLaunchKernelGGL(sac_actor_kernel, dim3(grid), dim3(NT), 0, stream, w, obs, E, ostride, eps,
                      act, logp);
   return hipGetLastError();
 }
