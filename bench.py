@@ -418,6 +418,8 @@ def bench_descent_sac(args):
                        "parallelism": f"env-shard x{world}" + (" + RCCL gradient all_reduce "
                                                                "(data-parallel SAC)" if world > 1 else ""),
                        "policy": "fused HIP actor (bsg_policy_sac)" if fused else "torch actor",
+                       "adam": "one launch per step (tools/sac_adam.hip)" if sac.hip_adam else
+                               "torch " + os.environ.get("SAC_ADAM", "fused"),
                        "hip_graph": graph, "blas": str(torch.backends.cuda.preferred_blas_library())},
             "env_only": {"value": total / el_env, "ms_per_step": el_env * 1e3 / args.steps},
             "env_policy": {"value": total / el_pol, "ms_per_step": el_pol * 1e3 / args.steps,
