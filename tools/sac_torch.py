@@ -24,6 +24,7 @@ data-parallel SAC with the per-rank batch 256 / world.
 """
 from __future__ import annotations
 
+import ctypes
 import math
 import os
 
@@ -32,6 +33,74 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 LOG_STD_MIN, LOG_STD_MAX = -20.0, 2.0
+_HERE = os.path.dirname(os.path.abspath(__file__))
+ADAM_LIB = os.path.join(_HERE, "_lib", "libsacadam.so")
+_MAXT = 16
+
+
+class _AdamTable(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_int32), ("start", ctypes.c_int32 * (_MAXT + 1)),
+                ("numel", ctypes.c_int64 * _MAXT), ("p", ctypes.c_void_p * _MAXT),
+                ("g", ctypes.c_void_p * _MAXT), ("m", ctypes.c_void_p * _MAXT),
+                ("v", ctypes.c_void_p * _MAXT)]
+
+
+class HipAdam:
+    """torch.optim.Adam (lr, betas (0.9, 0.999), eps 1e-8; no weight decay / amsgrad) over
+    several parameter groups, one launch of tools/sac_adam.hip per step() instead of one
+    torch fused-Adam launch per group at ~28 us each.  The step count t lives on the device
+    and is advanced by tick() (once per update: every group here steps once per update), so
+    the whole update can be captured in a HIP graph.  Gradients are read at step() time from
+    p.grad (set_to_none gradients included: the pointers are taken at launch/capture)."""
+
+    _lib = None
+
+    def __init__(self, params, lr, betas=(0.9, 0.999), eps=1e-8, step=None):
+        if HipAdam._lib is None:
+            if not os.path.exists(ADAM_LIB):
+                raise RuntimeError(f"{ADAM_LIB} missing: run __graft_entry__.build()")
+            lib = ctypes.CDLL(ADAM_LIB)
+            lib.sac_adam_step.restype = ctypes.c_int32
+            lib.sac_adam_step.argtypes = [ctypes.POINTER(_AdamTable), ctypes.c_void_p, ctypes.c_float,
+                                          ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_void_p]
+            HipAdam._lib = lib
+        self.params = list(params)
+        if len(self.params) > _MAXT:
+            raise ValueError("HipAdam: at most 16 tensors")
+        for p in self.params:
+            if p.dtype != torch.float32 or not p.is_contiguous() or p.device.type != "cuda":
+                raise ValueError("HipAdam: contiguous fp32 device parameters only")
+        self.m = [torch.zeros_like(p) for p in self.params]
+        self.v = [torch.zeros_like(p) for p in self.params]
+        self.lr, self.b1, self.b2, self.eps = float(lr), float(betas[0]), float(betas[1]), float(eps)
+        self.t = step if step is not None else torch.zeros((), dtype=torch.float32,
+                                                             device=self.params[0].device)
+
+    def tick(self):
+        self.t.add_(1.0)
+
+    def zero_grad(self, set_to_none=True):
+        for p in self.params:
+            p.grad = None
+
+    def step(self):
+        T = _AdamTable()
+        T.n = len(self.params)
+        acc = 0
+        T.start[0] = 0
+        for i, (p, m, v) in enumerate(zip(self.params, self.m, self.v)):
+            g = p.grad
+            if g is None or not g.is_contiguous():
+                raise RuntimeError("HipAdam: every parameter needs a contiguous gradient")
+            T.numel[i] = p.numel()
+            acc += (p.numel() + 255) // 256
+            T.start[i + 1] = acc
+            T.p[i], T.g[i], T.m[i], T.v[i] = p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr()
+        stream = ctypes.c_void_p(torch.cuda.current_stream(self.params[0].device).cuda_stream)
+        rc = self._lib.sac_adam_step(ctypes.byref(T), ctypes.c_void_p(self.t.data_ptr()), self.lr,
+                                     self.b1, self.b2, self.eps, stream)
+        if rc != 0:
+            raise RuntimeError(f"sac_adam_step failed ({rc})")
 
 
 def mlp(i, o, h=256):
@@ -118,11 +187,21 @@ class SAC:
         self.target_entropy = -float(act_dim)
         # fused Adam: one kernel per parameter group instead of a foreach chain per tensor
         # (the update is launch-bound: batch 256 through 256-wide MLPs)
-        impl = os.environ.get("SAC_ADAM", "fused")          # fused | foreach (A/B)
-        opt = dict(lr=lr, capturable=True, **{impl: True}) if self.dev.type == "cuda" else dict(lr=lr)
-        self.opt_a = torch.optim.Adam(self.actor.parameters(), **opt)
-        self.opt_q = torch.optim.Adam(self.q.parameters(), **opt)
-        self.opt_al = torch.optim.Adam([self.log_alpha], **opt)
+        # hip: tools/sac_adam.hip (one launch per step over every tensor of the groups that
+        # step together); fused | foreach: torch's Adam (A/B; the CPU tests use torch's)
+        impl = os.environ.get("SAC_ADAM", "hip" if self.dev.type == "cuda" else "torch")
+        self.hip_adam = impl == "hip"
+        if self.hip_adam:
+            t = torch.zeros((), dtype=torch.float32, device=self.dev)
+            self.opt_q = HipAdam(self.q.parameters(), lr, step=t)
+            # the actor and the entropy coefficient step back to back: one launch for both
+            self.opt_a = HipAdam(list(self.actor.parameters()) + [self.log_alpha], lr, step=t)
+            self.opt_al = None
+        else:
+            opt = dict(lr=lr, capturable=True, **{impl: True}) if self.dev.type == "cuda" else dict(lr=lr)
+            self.opt_a = torch.optim.Adam(self.actor.parameters(), **opt)
+            self.opt_q = torch.optim.Adam(self.q.parameters(), **opt)
+            self.opt_al = torch.optim.Adam([self.log_alpha], **opt)
         self.gamma, self.tau = gamma, tau
         self.group = group
         world = torch.distributed.get_world_size(group) if group is not None else 1
@@ -190,6 +269,8 @@ class SAC:
         x = torch.cat([o, a], -1)
         # F.mse_loss(q1, y) + F.mse_loss(q2, y)
         lq = (self.q(x) - y).pow(2).mean(-1).sum()
+        if self.hip_adam:
+            self.opt_q.tick()                     # shared step count: every group steps once
         self.opt_q.zero_grad(set_to_none=True)
         lq.backward()
         self._allreduce(list(self.q.parameters()))
@@ -206,12 +287,19 @@ class SAC:
         for p_ in self.q.parameters():
             p_.requires_grad_(True)
         self._allreduce(list(self.actor.parameters()))
-        self.opt_a.step()
+        if not self.hip_adam:
+            self.opt_a.step()
         lal = -(self.log_alpha * (logp.detach() + self.target_entropy)).mean()
-        self.opt_al.zero_grad(set_to_none=True)
+        if self.hip_adam:
+            self.log_alpha.grad = None
+        else:
+            self.opt_al.zero_grad(set_to_none=True)
         lal.backward()
         self._allreduce([self.log_alpha])
-        self.opt_al.step()
+        if self.hip_adam:
+            self.opt_a.step()                     # actor + log_alpha in one launch
+        else:
+            self.opt_al.step()
         with torch.no_grad():
             # SB3 polyak_update (target * (1 - tau), then + tau * param), as two multi-tensor
             # kernels over all target parameters instead of two kernels per tensor
