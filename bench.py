@@ -266,7 +266,8 @@ def main():
             "config": {
                 "workload": f"MergeEnv-v0 {world * E} envs x {N} aircraft ({E} per GPU), 10 substeps x DT 5 s, "
                             f"StateBased CD {'off' if args.no_cd else 'on'}, NEXT_STEP autoreset"
-                            + (", RCCL all_gather of [E, obs+3] fp32 per step" if gather else ""),
+                            + ((", RCCL" if backend == "nccl" else f", {backend}") + " all_gather of [E, obs+3] fp32 per step"
+                               if gather else ""),
                 "envs_total": world * E,
                 "envs_per_gpu": E,
                 "num_ac": N,
@@ -326,9 +327,13 @@ def bench_descent_sac(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    backend = os.environ.get("BENCH_BACKEND", "nccl")   # gloo: multi-rank rehearsal on one GPU
     if world > 1:
         torch.cuda.set_device(local % torch.cuda.device_count())
-        dist.init_process_group("nccl", device_id=torch.device("cuda", torch.cuda.current_device()))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", torch.cuda.current_device()))
+        else:
+            dist.init_process_group(backend)
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
@@ -415,8 +420,9 @@ def bench_descent_sac(args):
                                    f"DT 1 s, SAME_STEP autoreset + final_obs, SAC batch 256 "
                                    f"buffer 1e6 train_freq 1 gradient_steps 1",
                        "envs_total": world * E, "envs_per_gpu": E,
-                       "parallelism": f"env-shard x{world}" + (" + RCCL gradient all_reduce "
-                                                               "(data-parallel SAC)" if world > 1 else ""),
+                       "parallelism": f"env-shard x{world}" + (
+                           (" + RCCL" if backend == "nccl" else f" + {backend}") +
+                           " gradient all_reduce (data-parallel SAC)" if world > 1 else ""),
                        "policy": "fused HIP actor (bsg_policy_sac)" if fused else "torch actor",
                        "adam": "one launch per step (tools/sac_adam.hip)" if sac.hip_adam else
                                "torch " + os.environ.get("SAC_ADAM", "fused"),
