@@ -27,6 +27,23 @@ _KEYS = ("latent_pi.0.weight", "latent_pi.0.bias", "latent_pi.2.weight", "latent
          "mu.weight", "mu.bias", "log_std.weight", "log_std.bias")
 
 
+def load_sb3_actor(path) -> dict:
+    """The actor weights of a saved SB3 SAC model (``model.save(...)`` -> ``<name>.zip``):
+    ``policy.pth`` inside the archive, read with ``torch.load(weights_only=True)`` (tensors
+    only; nothing in the file is executed), keys ``actor.*`` with the prefix removed.  The
+    archive's pickled ``data`` member is never read."""
+    import io
+    import zipfile
+    with zipfile.ZipFile(path) as z:
+        with z.open("policy.pth") as f:
+            sd = torch.load(io.BytesIO(f.read()), map_location="cpu", weights_only=True)
+    w = {k[len("actor."):]: v for k, v in sd.items() if k.startswith("actor.")}
+    missing = [k for k in _KEYS if k not in w]
+    if missing:
+        raise KeyError(f"{path}: no SAC actor weights {missing} in policy.pth")
+    return {k: w[k] for k in _KEYS}
+
+
 class SACPolicy:
     """SAC actor (net_arch [256, 256]) on the device.
 
@@ -52,6 +69,12 @@ class SACPolicy:
         the reference's saved SAC actors, extracted weights-only)."""
         with np.load(path) as z:
             return cls({k: z[f"{tag}/{k}"] for k in _KEYS}, device)
+
+    @classmethod
+    def from_sb3_zip(cls, path, device="cuda"):
+        """The actor of a saved SB3 SAC model (the reference's ``model.save`` archives,
+        e.g. ``scripts/common/results/models_backup/*/model.zip``), weights only."""
+        return cls(load_sb3_actor(path), device)
 
     @classmethod
     def from_module(cls, actor):

@@ -127,3 +127,36 @@ def test_policy_host_validation_without_gpu():
     w = nat.BsgSacActor(4, 1, 256, 0, *([p] * 8))
     assert lib.bsg_policy_sac(C.byref(w), p, 8, 3, None, C.cast(act, C.c_void_p), None, None) == -1
     assert lib.bsg_policy_sac(C.byref(w), p, 0, 4, None, C.cast(act, C.c_void_p), None, None) == 0
+
+
+def test_load_sb3_actor_from_zip(tmp_path):
+    """SACPolicy.from_sb3_zip's loader: policy.pth inside an SB3 archive, weights only, actor.*
+    keys (a synthetic archive of the SB3 layout; critic keys and the pickled `data` member
+    are ignored)."""
+    import io
+    import zipfile
+    import numpy as np
+    import torch
+    from bluesky_gym.policy import load_sb3_actor
+    shapes = {"latent_pi.0.weight": (256, 4), "latent_pi.0.bias": (256,),
+              "latent_pi.2.weight": (256, 256), "latent_pi.2.bias": (256,),
+              "mu.weight": (1, 256), "mu.bias": (1,), "log_std.weight": (1, 256), "log_std.bias": (1,)}
+    g = torch.Generator().manual_seed(0)
+    sd = {f"actor.{k}": torch.randn(s, generator=g) for k, s in shapes.items()}
+    sd["critic.qf0.0.weight"] = torch.zeros(256, 5)
+    buf = io.BytesIO()
+    torch.save(sd, buf)
+    zp = tmp_path / "model.zip"
+    with zipfile.ZipFile(zp, "w") as z:
+        z.writestr("policy.pth", buf.getvalue())
+        z.writestr("data", b"not read")
+    w = load_sb3_actor(zp)
+    assert sorted(w) == sorted(shapes)
+    for k in shapes:
+        assert np.array_equal(np.asarray(w[k]), sd[f"actor.{k}"].numpy())
+    with zipfile.ZipFile(tmp_path / "bad.zip", "w") as z:
+        b2 = io.BytesIO()
+        torch.save({"critic.x": torch.zeros(1)}, b2)
+        z.writestr("policy.pth", b2.getvalue())
+    with pytest.raises(KeyError):
+        load_sb3_actor(tmp_path / "bad.zip")
