@@ -55,6 +55,8 @@ class SACPolicy:
         dev = torch.device(device)
         if dev.type != "cuda":
             raise nat.BsgError("SACPolicy runs on a HIP device (no CPU fallback)")
+        if dev.index is None:                     # "cuda" -> the current device, as tensors report it
+            dev = torch.device("cuda", torch.cuda.current_device())
         w = {k[len("actor."):] if k.startswith("actor.") else k: v for k, v in weights.items()}
         missing = [k for k in _KEYS if k not in w]
         if missing:

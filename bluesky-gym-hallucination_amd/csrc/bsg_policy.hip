@@ -73,7 +73,7 @@ __global__ __launch_bounds__(NT) void sac_actor_kernel(bsg_sac_actor w, const fl
   // products, fp32 accumulation -- the VALU form of this loop was bound by the LDS broadcast
   // of the activations, one ds_read_b128 per 4 FMAs).  Wave v owns the output columns
   // [32v, 32v + 32) as two 16 x 16 tiles.  Lane l (m = l & 15, g = l >> 4) supplies
-  // A[m][k] = h0[m][k] and B[k][n] = W1[n][k] for n = 64v + 16t + m; over a 16-wide k block
+  // A[m][k] = h0[m][k] and B[k][n] = W1[n][k] for n = 32v + 16t + m; over a 16-wide k block
   // the lane's k slot g covers k0 + 4g .. k0 + 4g + 3 (one float4 of h0 from LDS, one float4
   // of W1's row n from L2), consumed one component per MFMA -- a permutation of the k sum.
   constexpr int TW = H / 16 / (NT / 64);   // tiles per wave

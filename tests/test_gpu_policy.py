@@ -162,3 +162,5 @@ def test_policy_rejects_bad_shapes():
     with pytest.raises(ValueError):
         SACPolicy(bad, dev)
     pol(torch.zeros((0, 4), device=dev))                 # empty batch is a no-op
+    p2 = SACPolicy.from_npz(GOLD, "descent", "cuda")     # an index-less device string
+    assert p2(torch.zeros((8, 4), device=dev)).shape == (8, 1)
