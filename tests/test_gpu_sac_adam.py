@@ -58,3 +58,31 @@ def test_sac_update_hip_adam_matches_fused_adam(monkeypatch):
                     list(s.actor.parameters()) + list(s.q.parameters()) + [s.log_alpha]])
     for x, y in zip(*out):
         assert torch.allclose(x, y, rtol=1e-4, atol=1e-6), (x - y).abs().max().item()
+
+
+def test_replay_insert_kernel_matches_torch_insert():
+    """One-launch replay insert (tools/sac_adam.hip) against SAC.insert on the same
+    transitions: rows, ring wrap-around, pos and size bit-identical."""
+    from types import SimpleNamespace
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev).manual_seed(9)
+    E, O, A = 300, 4, 1
+    a_ = sac_torch.SAC(O, A, dev, seed=1, buffer=1000)
+    b_ = sac_torch.SAC(O, A, dev, seed=1, buffer=1000)
+    assert a_.hip_adam
+    for _ in range(7):                                   # 2100 rows: wraps the 1000-row ring twice
+        obs = torch.randn((E, O), generator=g, device=dev)
+        act = torch.rand((E, A), generator=g, device=dev, dtype=torch.float64) * 2 - 1
+        bt = SimpleNamespace(
+            reward=torch.randn((E,), generator=g, device=dev),
+            terminated=(torch.rand((E,), generator=g, device=dev) < 0.1).to(torch.uint8),
+            truncated=(torch.rand((E,), generator=g, device=dev) < 0.1).to(torch.uint8),
+            obs=torch.randn((E, O), generator=g, device=dev),
+            final_obs=torch.randn((E, O), generator=g, device=dev))
+        a_.insert_step(obs, act, bt)
+        done = (bt.terminated | bt.truncated).bool()
+        nxt = torch.where(done[:, None], bt.final_obs, bt.obs)
+        b_.insert(obs, act, bt.reward, nxt, bt.terminated.float())
+        torch.cuda.synchronize()
+        assert int(a_.pos) == int(b_.pos) and int(a_.size) == int(b_.size)
+        assert torch.equal(a_.buf, b_.buf)

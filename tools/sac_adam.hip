@@ -1,4 +1,6 @@
-// Adam step for the C5 learner (tools/sac_torch.py): every parameter tensor of one or more
+// Learner kernels of the C5 bench (tools/sac_torch.py).
+//
+// Adam step: every parameter tensor of one or more
 // optimizer groups in ONE launch, one element per thread.
 //
 // torch's fused Adam (multi_tensor_apply) gives each workgroup a 65,536-element chunk, so the
@@ -62,5 +64,74 @@ extern "C" int32_t sac_adam_step(const sac_adam_table* T, const float* step, flo
   if (T->start[0] != 0) return -1;
   hipLaunchKernelGGL(adam_kernel, dim3(T->start[T->n]), dim3(BLOCK), 0, (hipStream_t)stream, *T,
                      step, lr, b1, b2, eps);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+// ---------------------------------------------------------------------------------------
+// Replay insert for the C5 learner: the E transitions of one vector step written as packed
+// rows [obs | act | reward | next_obs | terminated] at ring positions (pos + e) % cap, in ONE
+// launch (the torch form is ~12 kernels: arange/add/remainder for the indices, the
+// terminated|truncated mask, torch.where for next_obs, casts, cat, index_copy, the pos/size
+// updates).  next_obs is the terminal observation (final_obs) for envs that ended this step
+// (terminated or truncated), as SB3's VecEnv hands it over; `terminated` alone is the done
+// flag (SB3 handle_timeout_termination).  pos / size (int64, device) are read by every
+// workgroup at its start and advanced by the last workgroup to finish (ticket counter), so
+// the launch is graph-capturable.  Pure copies and exact casts: bit-identical to the torch form.
+namespace {
+
+__global__ __launch_bounds__(256) void replay_insert_kernel(
+    float* __restrict__ buf, long long cap, int O, int A, const float* __restrict__ obs,
+    const double* __restrict__ act, const float* __restrict__ rew, const uint8_t* __restrict__ term,
+    const uint8_t* __restrict__ trunc, const float* __restrict__ next_obs,
+    const float* __restrict__ final_obs, int E, long long* pos, long long* size, unsigned* ticket) {
+  const int W = 2 * O + A + 2;
+  const long long p0 = __atomic_load_n(pos, __ATOMIC_RELAXED);
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < (long long)E * W) {
+    const int e = (int)(i / W), c = (int)(i - (long long)e * W);
+    float v;
+    if (c < O) {
+      v = obs[(size_t)e * O + c];
+    } else if (c < O + A) {
+      v = (float)act[(size_t)e * A + (c - O)];
+    } else if (c == O + A) {
+      v = rew[e];
+    } else if (c < 2 * O + A + 1) {
+      const int k = c - (O + A + 1);
+      v = (term[e] | trunc[e]) ? final_obs[(size_t)e * O + k] : next_obs[(size_t)e * O + k];
+    } else {
+      v = (float)term[e];
+    }
+    buf[(size_t)((p0 + e) % cap) * W + c] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();
+    const unsigned t = atomicAdd(ticket, 1u);
+    if (t == gridDim.x - 1) {                     // every workgroup has read pos
+      const long long s = __atomic_load_n(size, __ATOMIC_RELAXED) + E;
+      atomicExch(reinterpret_cast<unsigned long long*>(pos), (unsigned long long)((p0 + E) % cap));
+      atomicExch(reinterpret_cast<unsigned long long*>(size), (unsigned long long)(s < cap ? s : cap));
+      atomicExch(ticket, 0u);
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" int32_t sac_replay_insert(float* buf, long long cap, int32_t obs_dim, int32_t act_dim,
+                                     const float* obs, const double* act, const float* rew,
+                                     const uint8_t* term, const uint8_t* trunc,
+                                     const float* next_obs, const float* final_obs, int32_t E,
+                                     long long* pos, long long* size, unsigned* ticket,
+                                     void* stream) {
+  if (!buf || cap < 1 || obs_dim < 1 || act_dim < 1 || E < 1 || E > cap || !obs || !act || !rew ||
+      !term || !trunc || !next_obs || !final_obs || !pos || !size || !ticket)
+    return -1;
+  const long long n = (long long)E * (2 * obs_dim + act_dim + 2);
+  const int grid = (int)((n + 255) / 256);
+  hipLaunchKernelGGL(replay_insert_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, buf, cap,
+                     obs_dim, act_dim, obs, act, rew, term, trunc, next_obs, final_obs, E, pos, size,
+                     ticket);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }

@@ -63,6 +63,10 @@ class HipAdam:
             lib.sac_adam_step.restype = ctypes.c_int32
             lib.sac_adam_step.argtypes = [ctypes.POINTER(_AdamTable), ctypes.c_void_p, ctypes.c_float,
                                           ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_void_p]
+            lib.sac_replay_insert.restype = ctypes.c_int32
+            lib.sac_replay_insert.argtypes = ([ctypes.c_void_p, ctypes.c_longlong, ctypes.c_int32,
+                                               ctypes.c_int32] + [ctypes.c_void_p] * 7 +
+                                              [ctypes.c_int32] + [ctypes.c_void_p] * 4)
             HipAdam._lib = lib
         self.params = list(params)
         if len(self.params) > _MAXT:
@@ -232,6 +236,29 @@ class SAC:
         self.pos.copy_((self.pos + n) % self.cap)
         self.size.copy_(torch.clamp(self.size + n, max=self.cap))
 
+    def insert_step(self, obs, act, batch):
+        """The E transitions of one SAME_STEP vector step (obs before the step, fp64 actions,
+        the batch's reward / terminated / truncated / obs / final_obs) in one launch of
+        tools/sac_adam.hip's replay insert; the same rows and pos/size as insert() with
+        next_obs = final_obs where terminated | truncated and done = terminated."""
+        if not hasattr(self, "_ticket"):
+            self._ticket = torch.zeros((), dtype=torch.int32, device=self.dev)
+            HipAdam([torch.zeros(1, device=self.dev)], 0.0)      # loads the library
+        E = obs.shape[0]
+        for t, dt in ((obs, torch.float32), (act, torch.float64), (batch.reward, torch.float32),
+                      (batch.terminated, torch.uint8), (batch.truncated, torch.uint8),
+                      (batch.obs, torch.float32), (batch.final_obs, torch.float32)):
+            if t.dtype != dt or not t.is_contiguous() or t.shape[0] != E:
+                raise ValueError("insert_step: unexpected tensor layout")
+        ptr = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+        stream = ctypes.c_void_p(torch.cuda.current_stream(self.dev).cuda_stream)
+        rc = HipAdam._lib.sac_replay_insert(
+            ptr(self.buf), self.cap, self.od, self.ad, ptr(obs), ptr(act), ptr(batch.reward),
+            ptr(batch.terminated), ptr(batch.truncated), ptr(batch.obs), ptr(batch.final_obs), E,
+            ptr(self.pos), ptr(self.size), ptr(self._ticket), stream)
+        if rc != 0:
+            raise RuntimeError(f"sac_replay_insert failed ({rc})")
+
     def sample(self):
         u = torch.rand(self.batch, device=self.dev)
         idx = torch.clamp((u * self.size.float()).long(), max=self.cap - 1)
@@ -337,10 +364,13 @@ class RLLoop:
                 a, _ = s.actor(self.obs)
             self.act.copy_(a)
         b.step(self.act)
-        done = (b.terminated | b.truncated).bool()
         if self.learn:
-            nxt = torch.where(done[:, None], b.final_obs, b.obs)
-            s.insert(self.obs, a, b.reward, nxt, b.terminated.float())
+            if s.hip_adam:
+                s.insert_step(self.obs, self.act, b)       # one launch (tools/sac_adam.hip)
+            else:
+                done = (b.terminated | b.truncated).bool()
+                nxt = torch.where(done[:, None], b.final_obs, b.obs)
+                s.insert(self.obs, a, b.reward, nxt, b.terminated.float())
             s.update()
         self.obs.copy_(b.obs)
 
