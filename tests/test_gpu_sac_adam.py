@@ -86,3 +86,23 @@ def test_replay_insert_kernel_matches_torch_insert():
         torch.cuda.synchronize()
         assert int(a_.pos) == int(b_.pos) and int(a_.size) == int(b_.size)
         assert torch.equal(a_.buf, b_.buf)
+
+
+def test_replay_sample_kernel_matches_torch_gather():
+    """One-launch replay sample against the torch index arithmetic + gather on the same
+    uniforms: the same rows, bit for bit (a partly filled ring, so size < cap)."""
+    dev = torch.device("cuda", 0)
+    s = sac_torch.SAC(4, 1, dev, seed=1, buffer=5000)
+    g = torch.Generator(device=dev).manual_seed(4)
+    s.buf.copy_(torch.randn(s.buf.shape, generator=g, device=dev))
+    s.size.fill_(3777)
+    torch.manual_seed(123)
+    got = [x.clone() for x in s.sample()]
+    torch.manual_seed(123)
+    u = torch.rand(s.batch, device=dev)
+    idx = torch.clamp((u * s.size.float()).long(), max=s.cap - 1)
+    t = s.buf[idx]
+    od, ad = s.od, s.ad
+    ref = (t[:, :od], t[:, od:od + ad], t[:, od + ad], t[:, od + ad + 1:2 * od + ad + 1], t[:, -1])
+    for a, b in zip(got, ref):
+        assert torch.equal(a, b)

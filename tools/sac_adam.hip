@@ -135,3 +135,35 @@ extern "C" int32_t sac_replay_insert(float* buf, long long cap, int32_t obs_dim,
                      ticket);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
+
+// ---------------------------------------------------------------------------------------
+// Replay sample for the C5 learner: rows buf[min((int64)(u_b * (float)size), cap - 1)] for the
+// batch's uniforms u (torch.rand, fp32) gathered into a contiguous [B, W] tile in ONE launch
+// (the torch form: a size cast, mul, long cast, clamp and an index gather).  The index
+// arithmetic is the torch form's, operation for operation (fp32 product, truncation toward
+// zero, clamp), so the rows drawn are the same.
+namespace {
+
+__global__ __launch_bounds__(256) void replay_sample_kernel(const float* __restrict__ buf, long long cap,
+                                                           int W, const float* __restrict__ u, int B,
+                                                           const long long* __restrict__ size,
+                                                           float* __restrict__ out) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long long)B * W) return;
+  const int b = (int)(i / W), c = (int)(i - (long long)b * W);
+  long long idx = (long long)(u[b] * (float)size[0]);
+  if (idx > cap - 1) idx = cap - 1;
+  out[i] = buf[(size_t)idx * W + c];
+}
+
+}  // namespace
+
+extern "C" int32_t sac_replay_sample(const float* buf, long long cap, int32_t row_width,
+                                     const float* u, int32_t batch, const long long* size,
+                                     float* out, void* stream) {
+  if (!buf || cap < 1 || row_width < 1 || !u || batch < 1 || !size || !out) return -1;
+  const long long n = (long long)batch * row_width;
+  hipLaunchKernelGGL(replay_sample_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, buf, cap, row_width, u, batch, size, out);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}

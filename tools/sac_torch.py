@@ -67,6 +67,10 @@ class HipAdam:
             lib.sac_replay_insert.argtypes = ([ctypes.c_void_p, ctypes.c_longlong, ctypes.c_int32,
                                                ctypes.c_int32] + [ctypes.c_void_p] * 7 +
                                               [ctypes.c_int32] + [ctypes.c_void_p] * 4)
+            lib.sac_replay_sample.restype = ctypes.c_int32
+            lib.sac_replay_sample.argtypes = [ctypes.c_void_p, ctypes.c_longlong, ctypes.c_int32,
+                                              ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p,
+                                              ctypes.c_void_p, ctypes.c_void_p]
             HipAdam._lib = lib
         self.params = list(params)
         if len(self.params) > _MAXT:
@@ -261,8 +265,22 @@ class SAC:
 
     def sample(self):
         u = torch.rand(self.batch, device=self.dev)
-        idx = torch.clamp((u * self.size.float()).long(), max=self.cap - 1)
-        t = self.buf[idx]
+        if self.hip_adam:
+            # the gather below as one launch of tools/sac_adam.hip (same index arithmetic)
+            if not hasattr(self, "_rows"):
+                self._rows = torch.empty((self.batch, self.buf.shape[1]), device=self.dev)
+                HipAdam([torch.zeros(1, device=self.dev)], 0.0)  # loads the library
+            t = self._rows
+            rc = HipAdam._lib.sac_replay_sample(
+                ctypes.c_void_p(self.buf.data_ptr()), self.cap, self.buf.shape[1],
+                ctypes.c_void_p(u.data_ptr()), self.batch, ctypes.c_void_p(self.size.data_ptr()),
+                ctypes.c_void_p(t.data_ptr()),
+                ctypes.c_void_p(torch.cuda.current_stream(self.dev).cuda_stream))
+            if rc != 0:
+                raise RuntimeError(f"sac_replay_sample failed ({rc})")
+        else:
+            idx = torch.clamp((u * self.size.float()).long(), max=self.cap - 1)
+            t = self.buf[idx]
         od, ad = self.od, self.ad
         return (t[:, :od], t[:, od:od + ad], t[:, od + ad], t[:, od + ad + 1:2 * od + ad + 1], t[:, -1])
 
