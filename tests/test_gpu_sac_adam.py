@@ -106,3 +106,21 @@ def test_replay_sample_kernel_matches_torch_gather():
     ref = (t[:, :od], t[:, od:od + ad], t[:, od + ad], t[:, od + ad + 1:2 * od + ad + 1], t[:, -1])
     for a, b in zip(got, ref):
         assert torch.equal(a, b)
+
+
+def test_td_target_kernel_bit_identical():
+    """One-launch TD target against the torch expression of SAC.update on the same inputs."""
+    dev = torch.device("cuda", 0)
+    s = sac_torch.SAC(4, 1, dev, seed=1, buffer=5000)
+    g = torch.Generator(device=dev).manual_seed(8)
+    s.buf.copy_(torch.randn(s.buf.shape, generator=g, device=dev))
+    s.buf[:, -1] = (torch.rand(s.cap, generator=g, device=dev) < 0.2).float()
+    s.size.fill_(5000)
+    o, a, r, o2, d = s.sample()
+    B = s.batch
+    q2 = torch.randn((2, B), generator=g, device=dev) * 30
+    ll = torch.randn((2 * B,), generator=g, device=dev)
+    alpha = torch.rand((), generator=g, device=dev)
+    got = s._td_target(q2, ll, alpha).clone()
+    ref = r + s.gamma * (1.0 - d) * (q2.amin(0) - alpha * ll[:B])
+    assert torch.equal(got, ref), (got - ref).abs().max().item()

@@ -167,3 +167,36 @@ extern "C" int32_t sac_replay_sample(const float* buf, long long cap, int32_t ro
                      (hipStream_t)stream, buf, cap, row_width, u, batch, size, out);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
+
+// ---------------------------------------------------------------------------------------
+// SAC TD target for the C5 learner: y = r + gamma * (1 - d) * (min(q_t1, q_t2) - alpha * logp')
+// in ONE launch (the torch form is six: amin, mul, sub, rsub, mul, mul, add), operation for
+// operation in fp32 without contraction (this file builds with -ffp-contract=off), so y is
+// bit-identical.  r and d are columns of the sampled rows [B, W] (col_r, col_d).
+namespace {
+
+__global__ __launch_bounds__(256) void td_target_kernel(const float* __restrict__ q2, const float* __restrict__ logp2,
+                                                       const float* __restrict__ alpha,
+                                                       const float* __restrict__ rows, int W, int col_r,
+                                                       int col_d, float gamma, int B, float* __restrict__ y) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const float q = fminf(q2[b], q2[B + b]);
+  const float qt = q - alpha[0] * logp2[b];
+  const float d = rows[(size_t)b * W + col_d];
+  const float r = rows[(size_t)b * W + col_r];
+  y[b] = r + (gamma * (1.0f - d)) * qt;
+}
+
+}  // namespace
+
+extern "C" int32_t sac_td_target(const float* q2, const float* logp2, const float* alpha,
+                                 const float* rows, int32_t W, int32_t col_r, int32_t col_d,
+                                 float gamma, int32_t B, float* y, void* stream) {
+  if (!q2 || !logp2 || !alpha || !rows || !y || B < 1 || W < 1 || col_r < 0 || col_r >= W ||
+      col_d < 0 || col_d >= W)
+    return -1;
+  hipLaunchKernelGGL(td_target_kernel, dim3((B + 255) / 256), dim3(256), 0, (hipStream_t)stream, q2,
+                     logp2, alpha, rows, W, col_r, col_d, gamma, B, y);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}

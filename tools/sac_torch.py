@@ -71,6 +71,9 @@ class HipAdam:
             lib.sac_replay_sample.argtypes = [ctypes.c_void_p, ctypes.c_longlong, ctypes.c_int32,
                                               ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p,
                                               ctypes.c_void_p, ctypes.c_void_p]
+            lib.sac_td_target.restype = ctypes.c_int32
+            lib.sac_td_target.argtypes = ([ctypes.c_void_p] * 4 + [ctypes.c_int32] * 3 +
+                                          [ctypes.c_float, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p])
             HipAdam._lib = lib
         self.params = list(params)
         if len(self.params) > _MAXT:
@@ -284,6 +287,23 @@ class SAC:
         od, ad = self.od, self.ad
         return (t[:, :od], t[:, od:od + ad], t[:, od + ad], t[:, od + ad + 1:2 * od + ad + 1], t[:, -1])
 
+    def _td_target(self, q2, ll, alpha):
+        """r + gamma (1 - d) (min(q_t) - alpha logp') in one launch (tools/sac_adam.hip),
+        bit-identical to the torch expression; r, d from the sampled rows (self._rows), logp'
+        the first B entries of the actor pass's log-probs."""
+        B = self.batch
+        if not hasattr(self, "_y"):
+            self._y = torch.empty(B, device=self.dev)
+        q2 = q2.contiguous()
+        W = self._rows.shape[1]
+        rc = HipAdam._lib.sac_td_target(
+            ctypes.c_void_p(q2.data_ptr()), ctypes.c_void_p(ll.data_ptr()), ctypes.c_void_p(alpha.data_ptr()),
+            ctypes.c_void_p(self._rows.data_ptr()), W, self.od + self.ad, W - 1, self.gamma, B,
+            ctypes.c_void_p(self._y.data_ptr()), ctypes.c_void_p(torch.cuda.current_stream(self.dev).cuda_stream))
+        if rc != 0:
+            raise RuntimeError(f"sac_td_target failed ({rc})")
+        return self._y
+
     # -------------------------------------------------------------- SAC update
     def _allreduce(self, params):
         if self.world == 1:
@@ -309,8 +329,11 @@ class SAC:
         with torch.no_grad():
             a2, logp2 = aa[:B].detach(), ll[:B].detach()
             x2 = torch.cat([o2, a2], -1)
-            qt = self.qt(x2).amin(0) - alpha * logp2
-            y = r + self.gamma * (1.0 - d) * qt
+            if self.hip_adam:
+                y = self._td_target(self.qt(x2), ll, alpha)
+            else:
+                qt = self.qt(x2).amin(0) - alpha * logp2
+                y = r + self.gamma * (1.0 - d) * qt
         x = torch.cat([o, a], -1)
         # F.mse_loss(q1, y) + F.mse_loss(q2, y)
         lq = (self.q(x) - y).pow(2).mean(-1).sum()
