@@ -3,10 +3,11 @@ plain PyTorch reference of the same op (SB3 SAC Actor: Linear-ReLU 256-256, mu /
 heads, log_std clamped to [-20, 2], tanh squash, log-prob with the 1e-6 tanh correction),
 evaluated in float64 from the same fp32 weights and inputs.
 
-Tolerances: the kernel's actions are within max(2e-5, 2 x the error of torch's own fp32
-forward) of the float64 reference (both round fp32 256-term dot products; with N(0, 4)
-inputs far outside the actors' training range the pre-activations reach ~1e2 and fp32
-rounding reaches a few 1e-5 in either); log_prob 2e-3 absolute where 1 - a^2 > 1e-2
+Tolerances: the kernel's actions are within max(2e-5, 4 x the error of torch's own fp32
+forward) of the float64 reference (both round fp32 256-term dot products in different
+orders, so their worst rows over a batch differ by small factors; with N(0, 4) inputs far
+outside the actors' training range the pre-activations reach ~1e2 and fp32 rounding reaches
+a few 1e-5 in either); inputs are seeded; log_prob 2e-3 absolute where 1 - a^2 > 1e-2
 (log(1 - a^2) amplifies the action's rounding near +-1, where it is not compared)."""
 import os
 
@@ -44,7 +45,7 @@ def check_actions(act, W, obs, eps):
     ra = ref_actor(W, obs, eps)[0]
     terr = (ref_actor(W, obs, eps, torch.float32)[0].double() - ra).abs().max().item()
     err = (act - ra).abs().max().item()
-    assert err <= max(2e-5, 2 * terr), (err, terr)
+    assert err <= max(2e-5, 4 * terr), (err, terr)
 
 
 def weights(tag):
@@ -71,7 +72,7 @@ def test_policy_matches_torch_reference(tag, E, extra):
         terr = (ref_actor(W, obs, e, torch.float32)[0].double() - ra).abs().max().item()
         assert act.dtype == torch.float64 and act.shape == (E, A)
         err = (act - ra).abs().max().item()
-        assert err <= max(2e-5, 2 * terr), (tag, E, e is None, err, terr)
+        assert err <= max(2e-5, 4 * terr), (tag, E, e is None, err, terr)
         print(f"{tag} E={E} eps={e is not None}: kernel {err:.2e}, torch fp32 {terr:.2e}")
         ok = (1 - ra * ra).min(-1).values > 1e-2
         lerr = (lp.double() - rlp)[ok].abs().max().item() if ok.any() else 0.0
@@ -86,6 +87,7 @@ def test_policy_shares_live_module_weights_and_replays_in_graph():
     sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "tools"))
     import sac_torch
     dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
     actor = sac_torch.Actor(4, 1).to(dev)
     actor.load_sb3(np.load(GOLD), "descent")
     pol = SACPolicy.from_module(actor)

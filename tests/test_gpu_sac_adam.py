@@ -124,3 +124,21 @@ def test_td_target_kernel_bit_identical():
     got = s._td_target(q2, ll, alpha).clone()
     ref = r + s.gamma * (1.0 - d) * (q2.amin(0) - alpha * ll[:B])
     assert torch.equal(got, ref), (got - ref).abs().max().item()
+
+
+def test_twin_mse_gradient_bit_identical():
+    """TwinMSE (one forward, one backward launch) against (q - y).pow(2).mean(-1).sum():
+    gradient bit-identical, loss within fp32 reduction-order rounding."""
+    dev = torch.device("cuda", 0)
+    sac_torch.HipAdam([torch.zeros(1, device=dev)], 0.0)          # loads the library
+    g = torch.Generator(device=dev).manual_seed(2)
+    q0 = torch.randn((2, 256), generator=g, device=dev) * 20
+    y = torch.randn((256,), generator=g, device=dev) * 20
+    qa = q0.clone().requires_grad_(True)
+    qb = q0.clone().requires_grad_(True)
+    la = sac_torch.TwinMSE.apply(qa, y)
+    lb = (qb - y).pow(2).mean(-1).sum()
+    (la * 1.5).backward()
+    (lb * 1.5).backward()
+    assert torch.equal(qa.grad, qb.grad), (qa.grad - qb.grad).abs().max().item()
+    assert torch.allclose(la, lb, rtol=1e-5), (la.item(), lb.item())

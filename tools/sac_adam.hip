@@ -200,3 +200,58 @@ extern "C" int32_t sac_td_target(const float* q2, const float* logp2, const floa
                      logp2, alpha, rows, W, col_r, col_d, gamma, B, y);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
+
+// ---------------------------------------------------------------------------------------
+// Twin-critic MSE for the C5 learner: loss = sum_c mean_b (q[c, b] - y[b])^2 and the saved
+// difference q - y in ONE launch (one workgroup; B <= 1024), and its backward
+// dq = (g / B) * (2 (q - y)) in one more -- the operation order of torch's autograd for
+// (q - y).pow(2).mean(-1).sum() (MeanBackward divides the incoming gradient by B, PowBackward
+// multiplies by 2 (q - y)), so the gradient is bit-identical; the loss value itself comes
+// from a different reduction order (it is only reported).
+namespace {
+
+__global__ __launch_bounds__(1024) void twin_mse_fwd_kernel(const float* __restrict__ q,
+                                                            const float* __restrict__ y, int B,
+                                                            float* __restrict__ diff, float* __restrict__ loss) {
+  __shared__ float part[1024 / 64];
+  float acc = 0.0f;
+  for (int i = threadIdx.x; i < 2 * B; i += blockDim.x) {
+    const float d = q[i] - y[i % B];
+    diff[i] = d;
+    acc += d * d / (float)B;
+  }
+  for (int m = 32; m >= 1; m >>= 1) acc += __shfl_xor(acc, m, 64);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float s = 0.0f;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) s += part[w];
+    loss[0] = s;
+  }
+}
+
+__global__ __launch_bounds__(256) void twin_mse_bwd_kernel(const float* __restrict__ diff,
+                                                           const float* __restrict__ g, int B,
+                                                           float* __restrict__ dq) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= 2 * B) return;
+  dq[i] = (g[0] / (float)B) * (2.0f * diff[i]);
+}
+
+}  // namespace
+
+extern "C" int32_t sac_twin_mse_fwd(const float* q, const float* y, int32_t B, float* diff,
+                                    float* loss, void* stream) {
+  if (!q || !y || !diff || !loss || B < 1) return -1;
+  hipLaunchKernelGGL(twin_mse_fwd_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, q, y, B,
+                     diff, loss);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+extern "C" int32_t sac_twin_mse_bwd(const float* diff, const float* g, int32_t B, float* dq,
+                                    void* stream) {
+  if (!diff || !g || !dq || B < 1) return -1;
+  hipLaunchKernelGGL(twin_mse_bwd_kernel, dim3((2 * B + 255) / 256), dim3(256), 0,
+                     (hipStream_t)stream, diff, g, B, dq);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}

@@ -74,6 +74,12 @@ class HipAdam:
             lib.sac_td_target.restype = ctypes.c_int32
             lib.sac_td_target.argtypes = ([ctypes.c_void_p] * 4 + [ctypes.c_int32] * 3 +
                                           [ctypes.c_float, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p])
+            lib.sac_twin_mse_fwd.restype = ctypes.c_int32
+            lib.sac_twin_mse_fwd.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32,
+                                             ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+            lib.sac_twin_mse_bwd.restype = ctypes.c_int32
+            lib.sac_twin_mse_bwd.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32,
+                                             ctypes.c_void_p, ctypes.c_void_p]
             HipAdam._lib = lib
         self.params = list(params)
         if len(self.params) > _MAXT:
@@ -145,6 +151,36 @@ class Actor(nn.Module):
             self.latent[2].weight.copy_(g("latent_pi.2.weight")); self.latent[2].bias.copy_(g("latent_pi.2.bias"))
             self.mu.weight.copy_(g("mu.weight")); self.mu.bias.copy_(g("mu.bias"))
             self.log_std.weight.copy_(g("log_std.weight")); self.log_std.bias.copy_(g("log_std.bias"))
+
+
+class TwinMSE(torch.autograd.Function):
+    """(q - y).pow(2).mean(-1).sum() for q [2, B], y [B] (no grad) as one forward and one
+    backward launch of tools/sac_adam.hip; the gradient is bit-identical to torch's."""
+
+    @staticmethod
+    def forward(ctx, q, y):
+        q, y = q.contiguous(), y.contiguous()
+        B = y.shape[0]
+        diff = torch.empty_like(q)
+        loss = torch.empty((), device=q.device, dtype=q.dtype)
+        st = ctypes.c_void_p(torch.cuda.current_stream(q.device).cuda_stream)
+        if HipAdam._lib.sac_twin_mse_fwd(ctypes.c_void_p(q.data_ptr()), ctypes.c_void_p(y.data_ptr()), B,
+                                         ctypes.c_void_p(diff.data_ptr()), ctypes.c_void_p(loss.data_ptr()),
+                                         st) != 0:
+            raise RuntimeError("sac_twin_mse_fwd failed")
+        ctx.save_for_backward(diff)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        (diff,) = ctx.saved_tensors
+        g = g.contiguous()
+        dq = torch.empty_like(diff)
+        st = ctypes.c_void_p(torch.cuda.current_stream(diff.device).cuda_stream)
+        if HipAdam._lib.sac_twin_mse_bwd(ctypes.c_void_p(diff.data_ptr()), ctypes.c_void_p(g.data_ptr()),
+                                         diff.shape[1], ctypes.c_void_p(dq.data_ptr()), st) != 0:
+            raise RuntimeError("sac_twin_mse_bwd failed")
+        return dq, None
 
 
 class TwinQ(nn.Module):
@@ -336,7 +372,7 @@ class SAC:
                 y = r + self.gamma * (1.0 - d) * qt
         x = torch.cat([o, a], -1)
         # F.mse_loss(q1, y) + F.mse_loss(q2, y)
-        lq = (self.q(x) - y).pow(2).mean(-1).sum()
+        lq = TwinMSE.apply(self.q(x), y) if self.hip_adam else (self.q(x) - y).pow(2).mean(-1).sum()
         if self.hip_adam:
             self.opt_q.tick()                     # shared step count: every group steps once
         self.opt_q.zero_grad(set_to_none=True)
