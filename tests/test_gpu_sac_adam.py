@@ -142,3 +142,24 @@ def test_twin_mse_gradient_bit_identical():
     (lb * 1.5).backward()
     assert torch.equal(qa.grad, qb.grad), (qa.grad - qb.grad).abs().max().item()
     assert torch.allclose(la, lb, rtol=1e-5), (la.item(), lb.item())
+
+
+def test_actor_loss_gradient_bit_identical():
+    """ActorLoss (one forward, one backward launch) against (alpha * logp - q.amin(0)).mean():
+    gradients bit-identical (a tie included), loss within fp32 reduction-order rounding."""
+    dev = torch.device("cuda", 0)
+    sac_torch.HipAdam([torch.zeros(1, device=dev)], 0.0)          # loads the library
+    g = torch.Generator(device=dev).manual_seed(6)
+    q0 = torch.randn((2, 256), generator=g, device=dev) * 20
+    q0[1, 7] = q0[0, 7]                                             # a tie: amin splits evenly
+    l0 = torch.randn((256,), generator=g, device=dev)
+    alpha = torch.rand((), generator=g, device=dev)
+    qa, qb = q0.clone().requires_grad_(True), q0.clone().requires_grad_(True)
+    la_, lb_ = l0.clone().requires_grad_(True), l0.clone().requires_grad_(True)
+    a = sac_torch.ActorLoss.apply(qa, la_, alpha)
+    b = (alpha * lb_ - qb.amin(0)).mean()
+    (a * 0.7).backward()
+    (b * 0.7).backward()
+    assert torch.equal(qa.grad, qb.grad), (qa.grad - qb.grad).abs().max().item()
+    assert torch.equal(la_.grad, lb_.grad), (la_.grad - lb_.grad).abs().max().item()
+    assert torch.allclose(a, b, rtol=1e-5, atol=1e-6), (a.item(), b.item())

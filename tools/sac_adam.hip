@@ -255,3 +255,67 @@ extern "C" int32_t sac_twin_mse_bwd(const float* diff, const float* g, int32_t B
                      (hipStream_t)stream, diff, g, B, dq);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
+
+// ---------------------------------------------------------------------------------------
+// SAC actor loss for the C5 learner: loss = mean_b(alpha * logp[b] - min(q[0, b], q[1, b])) in
+// one launch (one workgroup; B <= 1024), backward in one more: dlogp = (g / B) * alpha and
+// dq[c, b] = -(g / B) on the smaller critic (split evenly on a tie), autograd's operation
+// order for (alpha * logp - q.amin(0)).mean() (MeanBackward's g / B, MulBackward's * alpha,
+// SubBackward's negation, AminBackward's even split).  The loss value comes from a different
+// reduction order (reported only).
+namespace {
+
+__global__ __launch_bounds__(1024) void actor_loss_fwd_kernel(const float* __restrict__ q,
+                                                              const float* __restrict__ logp,
+                                                              const float* __restrict__ alpha, int B,
+                                                              float* __restrict__ loss) {
+  __shared__ float part[1024 / 64];
+  float acc = 0.0f;
+  const float al = alpha[0];
+  for (int b = threadIdx.x; b < B; b += blockDim.x) acc += (al * logp[b] - fminf(q[b], q[B + b])) / (float)B;
+  for (int m = 32; m >= 1; m >>= 1) acc += __shfl_xor(acc, m, 64);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float s = 0.0f;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) s += part[w];
+    loss[0] = s;
+  }
+}
+
+__global__ __launch_bounds__(256) void actor_loss_bwd_kernel(const float* __restrict__ q,
+                                                             const float* __restrict__ alpha,
+                                                             const float* __restrict__ g, int B,
+                                                             float* __restrict__ dq, float* __restrict__ dlogp) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const float gb = g[0] / (float)B;
+  dlogp[b] = gb * alpha[0];
+  const float q0 = q[b], q1 = q[B + b], mn = fminf(q0, q1);
+  const float ng = -gb;
+  if (q0 == q1) {
+    dq[b] = ng / 2.0f;
+    dq[B + b] = ng / 2.0f;
+  } else {
+    dq[b] = q0 == mn ? ng : 0.0f;
+    dq[B + b] = q1 == mn ? ng : 0.0f;
+  }
+}
+
+}  // namespace
+
+extern "C" int32_t sac_actor_loss_fwd(const float* q, const float* logp, const float* alpha, int32_t B,
+                                      float* loss, void* stream) {
+  if (!q || !logp || !alpha || !loss || B < 1) return -1;
+  hipLaunchKernelGGL(actor_loss_fwd_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, q, logp,
+                     alpha, B, loss);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+extern "C" int32_t sac_actor_loss_bwd(const float* q, const float* alpha, const float* g, int32_t B,
+                                      float* dq, float* dlogp, void* stream) {
+  if (!q || !alpha || !g || !dq || !dlogp || B < 1) return -1;
+  hipLaunchKernelGGL(actor_loss_bwd_kernel, dim3((B + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+                     q, alpha, g, B, dq, dlogp);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}

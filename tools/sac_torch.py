@@ -80,6 +80,10 @@ class HipAdam:
             lib.sac_twin_mse_bwd.restype = ctypes.c_int32
             lib.sac_twin_mse_bwd.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32,
                                              ctypes.c_void_p, ctypes.c_void_p]
+            lib.sac_actor_loss_fwd.restype = ctypes.c_int32
+            lib.sac_actor_loss_fwd.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_int32] + [ctypes.c_void_p] * 2
+            lib.sac_actor_loss_bwd.restype = ctypes.c_int32
+            lib.sac_actor_loss_bwd.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_int32] + [ctypes.c_void_p] * 3
             HipAdam._lib = lib
         self.params = list(params)
         if len(self.params) > _MAXT:
@@ -181,6 +185,38 @@ class TwinMSE(torch.autograd.Function):
                                          diff.shape[1], ctypes.c_void_p(dq.data_ptr()), st) != 0:
             raise RuntimeError("sac_twin_mse_bwd failed")
         return dq, None
+
+
+class ActorLoss(torch.autograd.Function):
+    """(alpha * logp - q.amin(0)).mean() for q [2, B], logp [B], alpha a detached 0-dim
+    tensor, as one forward and one backward launch of tools/sac_adam.hip."""
+
+    @staticmethod
+    def forward(ctx, q, logp, alpha):
+        q, logp = q.contiguous(), logp.contiguous()
+        B = logp.shape[0]
+        loss = torch.empty((), device=q.device, dtype=q.dtype)
+        st = ctypes.c_void_p(torch.cuda.current_stream(q.device).cuda_stream)
+        if HipAdam._lib.sac_actor_loss_fwd(ctypes.c_void_p(q.data_ptr()), ctypes.c_void_p(logp.data_ptr()),
+                                           ctypes.c_void_p(alpha.data_ptr()), B,
+                                           ctypes.c_void_p(loss.data_ptr()), st) != 0:
+            raise RuntimeError("sac_actor_loss_fwd failed")
+        ctx.save_for_backward(q, alpha)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        q, alpha = ctx.saved_tensors
+        g = g.contiguous()
+        B = q.shape[1]
+        dq = torch.empty_like(q)
+        dlogp = torch.empty((B,), device=q.device, dtype=q.dtype)
+        st = ctypes.c_void_p(torch.cuda.current_stream(q.device).cuda_stream)
+        if HipAdam._lib.sac_actor_loss_bwd(ctypes.c_void_p(q.data_ptr()), ctypes.c_void_p(alpha.data_ptr()),
+                                           ctypes.c_void_p(g.data_ptr()), B, ctypes.c_void_p(dq.data_ptr()),
+                                           ctypes.c_void_p(dlogp.data_ptr()), st) != 0:
+            raise RuntimeError("sac_actor_loss_bwd failed")
+        return dq, dlogp, None
 
 
 class TwinQ(nn.Module):
@@ -385,7 +421,8 @@ class SAC:
         # their .grad too (cleared before their next step); freezing them skips that work
         for p_ in self.q.parameters():
             p_.requires_grad_(False)
-        la = (alpha * logp - self.q(xp).amin(0)).mean()
+        la = ActorLoss.apply(self.q(xp), logp, alpha) if self.hip_adam else \
+            (alpha * logp - self.q(xp).amin(0)).mean()
         self.opt_a.zero_grad(set_to_none=True)
         la.backward()
         for p_ in self.q.parameters():
