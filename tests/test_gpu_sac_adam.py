@@ -3,6 +3,7 @@ torch.optim.Adam, and of a whole SAC update with it against the same update with
 fused Adam (same seed, same replay samples).  Tolerance: 1e-5 relative + 1e-7 absolute per
 parameter after 10 steps (fp32; the two evaluate the same formula in a different operation
 order), 1e-4 after 10 SAC updates (the differences feed back through the losses)."""
+import math
 import os
 import sys
 
@@ -36,9 +37,11 @@ def test_hip_adam_matches_torch_adam():
         assert torch.allclose(x, y, rtol=1e-5, atol=1e-7), (x - y).abs().max().item()
 
 
-def test_sac_update_hip_adam_matches_fused_adam(monkeypatch):
+@pytest.mark.parametrize("fused_dist", ["0"])
+def test_sac_update_hip_adam_matches_fused_adam(monkeypatch, fused_dist):
     dev = torch.device("cuda", 0)
     out = []
+    monkeypatch.setenv("SAC_FUSED_DIST", fused_dist)
     for impl in ("hip", "fused"):
         monkeypatch.setenv("SAC_ADAM", impl)
         s = sac_torch.SAC(4, 1, dev, seed=7, lr=1e-3, buffer=4096)
@@ -163,3 +166,35 @@ def test_actor_loss_gradient_bit_identical():
     assert torch.equal(qa.grad, qb.grad), (qa.grad - qb.grad).abs().max().item()
     assert torch.equal(la_.grad, lb_.grad), (la_.grad - lb_.grad).abs().max().item()
     assert torch.allclose(a, b, rtol=1e-5, atol=1e-6), (a.item(), b.item())
+
+
+def test_squashed_gaussian_matches_autograd():
+    """SquashedGaussian (one forward, one backward launch) against Actor.forward's torch form
+    on the same (mu, raw log_std, eps), incl. clamped log_std entries: outputs within 2 ulp-ish
+    (1e-6 relative), gradients within 1e-5 relative (different association)."""
+    dev = torch.device("cuda", 0)
+    sac_torch.HipAdam([torch.zeros(1, device=dev)], 0.0)          # loads the library
+    g = torch.Generator(device=dev).manual_seed(12)
+    for A in (1, 2):
+        mu0 = torch.randn((512, A), generator=g, device=dev) * 2
+        ls0 = torch.randn((512, A), generator=g, device=dev) * 3
+        ls0[0, 0], ls0[1, 0] = 5.0, -25.0                           # outside the clamp
+        eps = torch.randn((512, A), generator=g, device=dev)
+        wa = torch.randn((512, A), generator=g, device=dev)
+        wl = torch.randn((512,), generator=g, device=dev)
+        m1, l1 = mu0.clone().requires_grad_(True), ls0.clone().requires_grad_(True)
+        m2, l2 = mu0.clone().requires_grad_(True), ls0.clone().requires_grad_(True)
+        a1, lp1 = sac_torch.SquashedGaussian.apply(m1, l1, eps)
+        ls = torch.clamp(l2, -20.0, 2.0)
+        std = ls.exp()
+        u = m2 + std * eps
+        a2 = torch.tanh(u)
+        lp2 = (-0.5 * ((u - m2) / std) ** 2 - ls - 0.5 * math.log(2 * math.pi)).sum(-1)
+        lp2 = lp2 - torch.log(1 - a2 * a2 + 1e-6).sum(-1)
+        assert torch.allclose(a1, a2, rtol=1e-6, atol=1e-7)
+        assert torch.allclose(lp1, lp2, rtol=1e-5, atol=1e-4)
+        ((a1 * wa).sum() + (lp1 * wl).sum()).backward()
+        ((a2 * wa).sum() + (lp2 * wl).sum()).backward()
+        assert torch.allclose(m1.grad, m2.grad, rtol=1e-4, atol=1e-4), (m1.grad - m2.grad).abs().max().item()
+        assert torch.allclose(l1.grad, l2.grad, rtol=1e-4, atol=1e-4), (l1.grad - l2.grad).abs().max().item()
+        assert l1.grad[0, 0] == 0 and l1.grad[1, 0] == 0

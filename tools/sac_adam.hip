@@ -319,3 +319,80 @@ extern "C" int32_t sac_actor_loss_bwd(const float* q, const float* alpha, const 
                      q, alpha, g, B, dq, dlogp);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
+
+// ---------------------------------------------------------------------------------------
+// SB3's squashed diagonal Gaussian for the C5 learner's actor pass, one launch forward and
+// one backward (the torch form is ~13 elementwise kernels forward and as many backward):
+//   ls = clamp(ls_raw, -20, 2); std = exp(ls); u = mu + std * eps; a = tanh(u);
+//   logp = sum_j [-((u - mu) / std)^2 / 2 - ls - log(2 pi) / 2] - sum_j log(1 - a^2 + 1e-6)
+// backward from (ga, gl): with z = (u - mu) / std,
+//   g_u = ga (1 - a^2) + gl (-z / std + 2a (1 - a^2) / (1 - a^2 + 1e-6))
+//   g_mu = g_u + gl z / std;  g_std = g_u eps + gl z^2 / std;  g_ls = g_std std - gl,
+//   passed to ls_raw inside the clamp's closed range (torch's clamp backward).
+// One thread per row (A <= 4).  Within fp32 rounding of torch's autograd (different
+// association), checked by tests/test_gpu_sac_adam.py.
+namespace {
+
+__global__ __launch_bounds__(256) void sq_gauss_fwd_kernel(const float* __restrict__ mu, const float* __restrict__ lsr,
+                                                          const float* __restrict__ eps, int N, int A,
+                                                          float* __restrict__ a_out, float* __restrict__ logp) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= N) return;
+  float s1 = 0.0f, s2 = 0.0f;
+  for (int j = 0; j < A; ++j) {
+    const int i = r * A + j;
+    const float ls = fminf(fmaxf(lsr[i], -20.0f), 2.0f);
+    const float sd = expf(ls);
+    const float u = mu[i] + sd * eps[i];
+    const float a = tanhf(u);
+    a_out[i] = a;
+    const float z = (u - mu[i]) / sd;
+    s1 += -0.5f * (z * z) - ls - 0.91893853320467274f;
+    s2 += logf(1.0f - a * a + 1e-6f);
+  }
+  logp[r] = s1 - s2;
+}
+
+__global__ __launch_bounds__(256) void sq_gauss_bwd_kernel(const float* __restrict__ mu, const float* __restrict__ lsr,
+                                                          const float* __restrict__ eps, const float* __restrict__ a_out,
+                                                          const float* __restrict__ ga, const float* __restrict__ gl,
+                                                          int N, int A, float* __restrict__ gmu,
+                                                          float* __restrict__ glsr) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= N) return;
+  const float g = gl ? gl[r] : 0.0f;
+  for (int j = 0; j < A; ++j) {
+    const int i = r * A + j;
+    const float x = lsr[i];
+    const float ls = fminf(fmaxf(x, -20.0f), 2.0f);
+    const float sd = expf(ls);
+    const float u = mu[i] + sd * eps[i];
+    const float z = (u - mu[i]) / sd;
+    const float a = a_out[i];
+    const float da = 1.0f - a * a;
+    const float gu = (ga ? ga[i] : 0.0f) * da + g * (-z / sd + (2.0f * a / (da + 1e-6f)) * da);
+    gmu[i] = gu + g * z / sd;
+    const float gsd = gu * eps[i] + g * (z * z) / sd;
+    const float gls = gsd * sd - g;
+    glsr[i] = (x >= -20.0f && x <= 2.0f) ? gls : 0.0f;
+  }
+}
+
+}  // namespace
+
+extern "C" int32_t sac_sq_gauss_fwd(const float* mu, const float* lsr, const float* eps, int32_t N,
+                                    int32_t A, float* a_out, float* logp, void* stream) {
+  if (!mu || !lsr || !eps || !a_out || !logp || N < 1 || A < 1 || A > 4) return -1;
+  hipLaunchKernelGGL(sq_gauss_fwd_kernel, dim3((N + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+                     mu, lsr, eps, N, A, a_out, logp);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+extern "C" int32_t sac_sq_gauss_bwd(const float* mu, const float* lsr, const float* eps,
+                                    const float* a_out, const float* ga, const float* gl, int32_t N,
+                                    int32_t A, float* gmu, float* glsr, void* stream) {
+  if (!mu || !lsr || !eps || !a_out || !gmu || !glsr || N < 1 || A < 1 || A > 4) return -1;
+  hipLaunchKernelGGL(sq_gauss_bwd_kernel, dim3((N + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+                     mu, lsr, eps, a_out, ga, gl, N, A, gmu, glsr);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}

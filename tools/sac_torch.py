@@ -84,6 +84,10 @@ class HipAdam:
             lib.sac_actor_loss_fwd.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_int32] + [ctypes.c_void_p] * 2
             lib.sac_actor_loss_bwd.restype = ctypes.c_int32
             lib.sac_actor_loss_bwd.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_int32] + [ctypes.c_void_p] * 3
+            lib.sac_sq_gauss_fwd.restype = ctypes.c_int32
+            lib.sac_sq_gauss_fwd.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_int32] * 2 + [ctypes.c_void_p] * 3
+            lib.sac_sq_gauss_bwd.restype = ctypes.c_int32
+            lib.sac_sq_gauss_bwd.argtypes = [ctypes.c_void_p] * 6 + [ctypes.c_int32] * 2 + [ctypes.c_void_p] * 3
             HipAdam._lib = lib
         self.params = list(params)
         if len(self.params) > _MAXT:
@@ -128,6 +132,39 @@ def mlp(i, o, h=256):
     return nn.Sequential(nn.Linear(i, h), nn.ReLU(), nn.Linear(h, h), nn.ReLU(), nn.Linear(h, o))
 
 
+class SquashedGaussian(torch.autograd.Function):
+    """(tanh(u), log_prob) of SB3's squashed Gaussian from (mu, raw log_std, eps) as one
+    forward and one backward launch of tools/sac_adam.hip (Actor.forward's torch form is
+    ~13 kernels each way)."""
+
+    @staticmethod
+    def forward(ctx, mu, lsr, eps):
+        mu, lsr, eps = mu.contiguous(), lsr.contiguous(), eps.contiguous()
+        N, A = mu.shape
+        a = torch.empty_like(mu)
+        lp = torch.empty((N,), device=mu.device, dtype=mu.dtype)
+        st = ctypes.c_void_p(torch.cuda.current_stream(mu.device).cuda_stream)
+        p = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+        if HipAdam._lib.sac_sq_gauss_fwd(p(mu), p(lsr), p(eps), N, A, p(a), p(lp), st) != 0:
+            raise RuntimeError("sac_sq_gauss_fwd failed")
+        ctx.save_for_backward(mu, lsr, eps, a)
+        return a, lp
+
+    @staticmethod
+    def backward(ctx, ga, gl):
+        mu, lsr, eps, a = ctx.saved_tensors
+        N, A = mu.shape
+        gmu, glsr = torch.empty_like(mu), torch.empty_like(lsr)
+        ga = ga.contiguous() if ga is not None else None
+        gl = gl.contiguous() if gl is not None else None
+        st = ctypes.c_void_p(torch.cuda.current_stream(mu.device).cuda_stream)
+        p = lambda t: None if t is None else ctypes.c_void_p(t.data_ptr())  # noqa: E731
+        if HipAdam._lib.sac_sq_gauss_bwd(p(mu), p(lsr), p(eps), p(a), p(ga), p(gl), N, A, p(gmu),
+                                         p(glsr), st) != 0:
+            raise RuntimeError("sac_sq_gauss_bwd failed")
+        return gmu, glsr, None
+
+
 class Actor(nn.Module):
     def __init__(self, obs_dim, act_dim, h=256):
         super().__init__()
@@ -135,10 +172,15 @@ class Actor(nn.Module):
         self.mu = nn.Linear(h, act_dim)
         self.log_std = nn.Linear(h, act_dim)
 
+    fused_dist = False       # SquashedGaussian launches (set by SAC on the HIP path)
+
     def forward(self, obs):
         """(tanh-squashed sample, log-prob) of the SB3 squashed diagonal Gaussian."""
         h = self.latent(obs)
         mu = self.mu(h)
+        if self.fused_dist:
+            lsr = self.log_std(h)
+            return SquashedGaussian.apply(mu, lsr, torch.randn_like(mu))
         log_std = torch.clamp(self.log_std(h), LOG_STD_MIN, LOG_STD_MAX)
         std = log_std.exp()
         u = mu + std * torch.randn_like(mu)
@@ -274,6 +316,7 @@ class SAC:
         # step together); fused | foreach: torch's Adam (A/B; the CPU tests use torch's)
         impl = os.environ.get("SAC_ADAM", "hip" if self.dev.type == "cuda" else "torch")
         self.hip_adam = impl == "hip"
+        self.actor.fused_dist = self.hip_adam and os.environ.get("SAC_FUSED_DIST", "0") == "1"
         if self.hip_adam:
             t = torch.zeros((), dtype=torch.float32, device=self.dev)
             self.opt_q = HipAdam(self.q.parameters(), lr, step=t)
