@@ -1,5 +1,5 @@
 """The SAC learner of bench.py --workload descent-sac (tools/sac_torch.py) on the CPU:
-the reference's saved actor loads into it and reproduces tests/sac_policy.py's actor,
+the reference's saved actor loads into it and reproduces tests/ref_policy.py's actor,
 the replay ring buffer wraps, updates run and change the networks, and the
 data-parallel gradient all-reduce of two gloo ranks equals one learner on the union
 batch (world-size-2 rehearsal of the multi-GPU learner)."""
@@ -13,7 +13,7 @@ import torch
 
 sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "tools"))
 import sac_torch  # noqa: E402
-import sac_policy as sp  # noqa: E402
+import ref_policy as sp  # noqa: E402
 
 
 def test_actor_loads_reference_weights():
