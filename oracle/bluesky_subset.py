@@ -56,7 +56,8 @@ Tstrat = 216.65         # K
 # Frozen A320 envelope and autopilot defaults (docs/BLUESKY_SUBSET_SPEC.md §A.3).  The
 # speed / vertical-speed limits and the ground-phase envelope are FITTED to the reference's
 # own SAC training logs (scripts/common/results/logs_backup/*_SAC.csv) by rolling out its
-# saved actors (tests/golden/sac_actors.npz; tests/test_sac_logs.py):
+# saved actors (tests/golden/sac_actors.npz; tests/test_ref_logs.py; the
+# held-out DDPG/PPO actors reject the binding VSMAX, see there):
 #   VMAX_CAS: Descent + Vertical episode-length distributions (162.5..163.5 bracket)
 #   VSMAX:    Descent final-altitude distribution (the terminal dive runs at the limit)
 #   VMAX_GD:  Horizontal + PlanWaypoint episode lengths (aircraft created at alt 0)
