@@ -139,6 +139,7 @@ def main():
     ap.add_argument("--no-gather", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--skip-cpu-baseline", action="store_true")
+    ap.add_argument("--no-c5", action="store_true", help="skip the short C5 (Descent + policy) leg")
     ap.add_argument("--workload", default="merge", choices=("merge", "descent-sac"),
                     help="merge: the BASELINE metric (default); descent-sac: BASELINE configs[4], "
                          "DescentEnv-v0 with the SAC learner in the loop")
@@ -219,6 +220,19 @@ def main():
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     kern_avg_ms = ev0.elapsed_time(ev1) / args.steps
+    step_avg_ms = kern_avg_ms
+    if gather:
+        # with the gather the bracket above also holds the RCCL Work.wait() stream waits;
+        # the kernel's own time comes from the same launches without the collective
+        for k in range(args.warmup):
+            batch.step(bank[k % 16])
+        torch.cuda.synchronize()
+        ev0.record()
+        for k in range(args.steps):
+            batch.step(bank[k % 16])
+        ev1.record()
+        torch.cuda.synchronize()
+        kern_avg_ms = ev0.elapsed_time(ev1) / args.steps
     # cross-check after the timed region: an event pair around every TIMING_EVERY-th launch
     # (each pair serialises the stream, so it is kept out of the timed region), >= 10 samples
     batch.step_timing()                       # discard
@@ -230,9 +244,12 @@ def main():
     samp_ms, samples = batch.step_timing()
     samp_ms = samp_ms / max(samples, 1)
     if world > 1:
-        t = torch.tensor([el, kern_avg_ms, samp_ms], dtype=torch.float64, device=dev)
+        t = torch.tensor([el, kern_avg_ms, samp_ms, step_avg_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el, kern_avg_ms, samp_ms = float(t[0]), float(t[1]), float(t[2])
+        el, kern_avg_ms, samp_ms, step_avg_ms = (float(x) for x in t)
+    c5 = None
+    if world == 1 and not args.no_c5:
+        c5 = bench_c5_quick(args, dev)
 
     if rank == 0:
         total = world * E * args.steps
@@ -288,10 +305,17 @@ def main():
                                    f"this workload ({prof.get('source', '')}), not this run")
                                   if prof else None,
                 "kernel": "bsg::step_kernel<MERGE,32>",
+                # achieved / frac / kernel_avg_ms describe ONE GPU: a rank's shard of E envs
+                "scope": f"per GPU (one rank's launch over its {E} envs)",
                 "kernel_avg_ms": kern_avg_ms,
-                "kernel_timing": f"HIP events on the launch stream bracketing the {args.steps} "
-                                 f"back-to-back launches of the timed region (GPU time per launch, "
-                                 f"incl. the dispatch gap between launches)",
+                "kernel_timing": (f"HIP events on the launch stream bracketing the {args.steps} "
+                                  f"back-to-back launches of the timed region (GPU time per launch, "
+                                  f"incl. the dispatch gap between launches)") if not gather else
+                                 (f"HIP events bracketing {args.steps} back-to-back launches of a "
+                                  f"second pass WITHOUT the gather (max over ranks); the timed "
+                                  f"region's bracket incl. the gather's stream waits is "
+                                  f"step_avg_ms"),
+                "step_avg_ms": step_avg_ms,
                 "sampled_launch_ms": samp_ms,
                 "sampled_launch_timing": f"cross-check after the timed region: event pair around "
                                          f"every {TIMING_EVERY}th launch, {samples} samples "
@@ -303,10 +327,82 @@ def main():
         }
         if cpu is not None:
             out["cpu_baseline"] = cpu
+        if c5 is not None:
+            out["c5"] = c5
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def bench_c5_quick(args, dev):
+    """BASELINE configs[4] on this GPU, in a few seconds, after the headline timing
+    (its own buffers; the headline value is unaffected): DescentEnv-v0 x 4096 envs, SAME_STEP
+    autoreset + final_obs as SB3 consumes it, (a) env only (U(-1,1) actions from HBM) and
+    (b) env + the policy's action sample -- the reference's saved Descent SAC actor,
+    stochastic, as the fused HIP kernel bsg_policy_sac on the kernel's own fp32 obs rows,
+    the iteration captured as one HIP graph.  The SAC update itself (learner-bound, tools/
+    sac_torch.py) is `--workload descent-sac`; DESIGN.md §12."""
+    import numpy as np
+    import torch
+    from bluesky_gym import _native as nat, config, core
+    from bluesky_gym.policy import SACPolicy
+    E = 4096
+    steps, warm = max(args.steps, 20), max(args.warmup, 5)
+    b = core.DeviceBatch(config.descent_config(), E, autoreset=nat.AUTORESET_SAME_STEP,
+                         compute_cd=False, seed=1234)
+    b.reset()
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(29)
+    bank = torch.rand((16, E, 1), dtype=torch.float64, device=dev, generator=gen) * 2 - 1
+
+    def timed(fn):
+        for k in range(warm):
+            fn(k)
+        torch.cuda.synchronize()
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev1 = torch.cuda.Event(enable_timing=True)
+        t0 = time.perf_counter()
+        ev0.record()
+        for k in range(steps):
+            fn(k)
+        ev1.record()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) / steps, ev0.elapsed_time(ev1) / steps
+
+    wall_env, ev_env = timed(lambda k: b.step(bank[k % 16]))
+    W = dict(np.load(os.path.join(REPO, "tests", "golden", "sac_actors.npz")))
+    pol = SACPolicy({k: W[f"descent/{k}"] for k in ("latent_pi.0.weight", "latent_pi.0.bias",
+                     "latent_pi.2.weight", "latent_pi.2.bias", "mu.weight", "mu.bias",
+                     "log_std.weight", "log_std.bias")}, dev)
+    act = torch.zeros((E, 1), dtype=torch.float64, device=dev)
+    eps = torch.zeros((E, 1), dtype=torch.float32, device=dev)
+
+    def it():
+        eps.normal_()
+        pol(b.obs, eps, out=act)
+        b.step(act)
+
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(3):
+            it()
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        it()
+    wall_pol, ev_pol = timed(lambda k: g.replay())
+    return {"workload": "DescentEnv-v0 4096 envs, 30 substeps x DT 1 s, SAME_STEP autoreset + "
+                        "final_obs (BASELINE configs[4], one GPU; learner: --workload descent-sac)",
+            "steps": steps,
+            "env_only": {"value": E / wall_env, "ms_per_step": wall_env * 1e3,
+                         "kernel_avg_ms": ev_env, "kernel": "bsg::step_kernel<DESCENT,1>"},
+            "env_policy": {"value": E / wall_pol, "ms_per_step": wall_pol * 1e3,
+                           "event_ms_per_step": ev_pol,
+                           "policy": "reference's saved Descent SAC actor, stochastic, fused HIP "
+                                     "kernel bsg_policy_sac, HIP graph of sample + step"},
+            "unit": "env_steps/s"}
 
 
 def bench_descent_sac(args):

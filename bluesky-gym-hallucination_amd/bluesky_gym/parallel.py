@@ -56,7 +56,11 @@ class ShardedVectorEnv:
     three calls matters: a full re-bind plus event bookkeeping per step cost ~70 us of host
     time, as much as the kernel itself (tools/shard_overhead.py)."""
 
-    def __init__(self, make_local, total_envs: int, *, overlap=True, group=None):
+    def __init__(self, make_local, total_envs: int, *, overlap=True, group=None, collective=None):
+        """collective: optional ``f(out, rows) -> Work`` that starts the gather of this
+        rank's rows into ``out`` asynchronously (``Work.wait()`` = a stream wait), in place
+        of RCCL's all_gather_into_tensor -- another transport, or a test's delayed copy
+        (tests/test_gpu_sharded.py).  With it the overlapped path is used at any world size."""
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         self.group = group
@@ -69,7 +73,8 @@ class ShardedVectorEnv:
         self._gathered = [torch.empty((total_envs, d), dtype=torch.float32, device=dev)
                           for _ in range(2)]
         self._cur = 0
-        self.overlap = overlap and self.world > 1
+        self._collective = collective
+        self.overlap = collective is not None or (overlap and self.world > 1)
         self._work = [None, None]
 
     def _swap_in(self):
@@ -104,13 +109,17 @@ class ShardedVectorEnv:
         return self._gather(cur)
 
     def _gather(self, cur):
-        if self.world == 1:
-            self._gathered[cur][: self.n_local].copy_(self._rows[cur])
-            ready = Ready()
-        elif self.overlap:
-            work = all_gather_rows(self._gathered[cur], self._rows[cur], self.group, async_op=True)
+        if self.overlap:
+            if self._collective is not None:
+                work = self._collective(self._gathered[cur], self._rows[cur])
+            else:
+                work = all_gather_rows(self._gathered[cur], self._rows[cur], self.group,
+                                       async_op=True)
             self._work[cur] = work
             ready = Ready(work)
+        elif self.world == 1:
+            self._gathered[cur][: self.n_local].copy_(self._rows[cur])
+            ready = Ready()
         else:
             all_gather_rows(self._gathered[cur], self._rows[cur], self.group)
             ready = Ready()

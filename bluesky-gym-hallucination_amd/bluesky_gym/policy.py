@@ -113,26 +113,43 @@ class SACPolicy:
         """Actions [E, act_dim] fp64 for fp32 obs rows [E, >= obs_dim] (row stride = obs's).
         ``eps``: fp32 [E, act_dim] standard normals (stochastic SAC sample) or None
         (deterministic, tanh(mu)).  ``log_prob``: optional fp32 [E] output."""
-        if obs.dtype != torch.float32 or obs.dim() != 2 or obs.stride(1) != 1 or obs.device != self.device:
-            raise ValueError("SACPolicy: obs must be fp32 [E, D] rows (unit column stride) on the "
-                             "policy's device")
-        E = obs.shape[0]
+        E = self._check(obs, eps, out, log_prob)
         if out is None:
             out = torch.empty((E, self.act_dim), dtype=torch.float64, device=self.device)
-        if out.dtype != torch.float64 or tuple(out.shape) != (E, self.act_dim) or not out.is_contiguous():
-            raise ValueError("SACPolicy: out must be contiguous fp64 [E, act_dim]")
-        if eps is not None and (eps.dtype != torch.float32 or tuple(eps.shape) != (E, self.act_dim)
-                                or not eps.is_contiguous()):
-            raise ValueError("SACPolicy: eps must be contiguous fp32 [E, act_dim]")
-        if log_prob is not None and (log_prob.dtype != torch.float32 or tuple(log_prob.shape) != (E,)):
-            raise ValueError("SACPolicy: log_prob must be fp32 [E]")
         if E == 0:
             return out
         ptr = lambda x: None if x is None else C.c_void_p(x.data_ptr())  # noqa: E731
-        stream = C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
-        nat.check(self._lib.bsg_policy_sac(C.byref(self._w), ptr(obs), E, obs.stride(0), ptr(eps),
-                                           ptr(out), ptr(log_prob), stream), "bsg_policy_sac")
+        with torch.cuda.device(self.device):       # the launch goes to the policy's device
+            stream = C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+            nat.check(self._lib.bsg_policy_sac(C.byref(self._w), ptr(obs), E, obs.stride(0),
+                                               ptr(eps), ptr(out), ptr(log_prob), stream),
+                      "bsg_policy_sac")
         return out
+
+    def _check(self, obs, eps, out, log_prob) -> int:
+        """Every tensor the kernel reads or writes by raw pointer: dtype, shape, layout and
+        device (the kernel reads obs_dim floats per row at obs.stride(0) and writes out /
+        log_prob at unit stride)."""
+        dev = self.device
+        if obs.dtype != torch.float32 or obs.dim() != 2 or obs.stride(1) != 1 or obs.device != dev:
+            raise ValueError("SACPolicy: obs must be fp32 [E, D] rows (unit column stride) on the "
+                             "policy's device")
+        if obs.shape[1] < self.obs_dim:
+            raise ValueError(f"SACPolicy: obs rows hold {obs.shape[1]} features, the actor reads "
+                             f"{self.obs_dim}")
+        E = obs.shape[0]
+        if out is not None and (out.dtype != torch.float64 or tuple(out.shape) != (E, self.act_dim)
+                                or not out.is_contiguous() or out.device != dev):
+            raise ValueError("SACPolicy: out must be contiguous fp64 [E, act_dim] on the policy's "
+                             "device")
+        if eps is not None and (eps.dtype != torch.float32 or tuple(eps.shape) != (E, self.act_dim)
+                                or not eps.is_contiguous() or eps.device != dev):
+            raise ValueError("SACPolicy: eps must be contiguous fp32 [E, act_dim] on the policy's "
+                             "device")
+        if log_prob is not None and (log_prob.dtype != torch.float32 or tuple(log_prob.shape) != (E,)
+                                     or not log_prob.is_contiguous() or log_prob.device != dev):
+            raise ValueError("SACPolicy: log_prob must be contiguous fp32 [E] on the policy's device")
+        return E
 
     def predict(self, obs: torch.Tensor, deterministic: bool = True, generator=None):
         """SB3's ``predict`` shape: (actions, None)."""

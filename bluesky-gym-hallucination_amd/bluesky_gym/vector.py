@@ -81,12 +81,27 @@ class BlueSkyVectorEnv(_gym.VectorEnv):
                            compute_cd=self.compute_cd, seed=seed, device=self.device,
                            learner=self.learner, env_offset=self.env_offset)
 
+    # step_tensors() is the asynchronous device path: it only records the SectorCR overflow
+    # flag on the device and reads it back every OVERFLOW_CHECK_EVERY calls (and in step()
+    # / reset(), which copy to the host anyway), so it adds no per-step host sync.
+    OVERFLOW_CHECK_EVERY = 64
+
+    def _note_overflow(self):
+        """Device-side: OR this launch's SectorCR spawn-overflow flags into a sticky
+        per-env mask (no host sync)."""
+        if self.kind_cfg.kind != nat.ENV_SECTOR_CR:
+            return
+        over = (self.batch.envs["flags"] & nat.FLAG_SPAWN_OVERFLOW) != 0
+        prev = getattr(self, "_over", None)
+        self._over = over if prev is None or prev.shape != over.shape else prev | over
+
     def _check_overflow(self):
         """SectorCR: an episode that drew more aircraft than the capacity raises, as the
         host-spawn path does (bsg.h BSG_FLAG_SPAWN_OVERFLOW; sector_cr_env.py:95-100)."""
         if self.kind_cfg.kind != nat.ENV_SECTOR_CR:
             return
-        over = (self.batch.envs["flags"] & nat.FLAG_SPAWN_OVERFLOW) != 0
+        self._note_overflow()
+        over, self._over = self._over, None
         if bool(over.any()):
             e = int(torch.nonzero(over)[0, 0])
             raise RuntimeError(f"SectorCR env {e}: the episode drew more aircraft than "
@@ -151,12 +166,18 @@ class BlueSkyVectorEnv(_gym.VectorEnv):
             pend = self.batch.envs["flags"].cpu().numpy() & 1
             sp = self._host_spawn(pend.astype(bool)) if pend.any() else None
         out = self.batch.step(actions, spawn=sp)
-        self._check_overflow()
+        self._since_check = getattr(self, "_since_check", 0) + 1
+        if self._since_check >= self.OVERFLOW_CHECK_EVERY:
+            self._since_check = 0
+            self._check_overflow()
+        else:
+            self._note_overflow()
         return out
 
     def step(self, actions):
         a = actions if isinstance(actions, torch.Tensor) else torch.as_tensor(np.asarray(actions, np.float64))
         obs, rew, term, trunc = self.step_tensors(a)
+        self._check_overflow()                   # the host copies below sync anyway
         term_np = term.cpu().numpy().astype(bool)
         trunc_np = trunc.cpu().numpy().astype(bool)
         return (self.layout.split(obs.cpu().numpy()), rew.cpu().numpy().astype(np.float64),

@@ -105,8 +105,9 @@ bsg::KParams make_params(const bsg_ctx* c, int mode) {
 // waited for.
 constexpr size_t kMaxPending = 1024;
 
-int fold_pair(bsg_ctx* c, size_t i) {
-  auto pr = c->pending[i];
+// Folds one pair into the running totals and recycles its events; on failure the pair is
+// left alone (still the caller's to keep in `pending`).
+int fold_pair(bsg_ctx* c, std::pair<hipEvent_t, hipEvent_t> pr) {
   hipError_t e = hipEventSynchronize(pr.second);
   if (e != hipSuccess) return hip_fail(e, "hipEventSynchronize");
   float ms = 0.f;
@@ -124,14 +125,19 @@ int trim_pending(bsg_ctx* c) {
   size_t keep = 0;
   for (size_t i = 0; i < c->pending.size(); ++i) {
     if (hipEventQuery(c->pending[i].second) == hipSuccess) {
-      if (int r = fold_pair(c, i)) return r;
+      if (int r = fold_pair(c, c->pending[i])) {
+        // drop the pairs already folded (their events are back in the pool); keep the
+        // failing one and the unvisited tail
+        c->pending.erase(c->pending.begin() + keep, c->pending.begin() + i);
+        return r;
+      }
     } else {
       c->pending[keep++] = c->pending[i];
     }
   }
   c->pending.resize(keep);
   if (keep >= kMaxPending) {            // nothing finished yet: wait for the oldest
-    if (int r = fold_pair(c, 0)) return r;
+    if (int r = fold_pair(c, c->pending.front())) return r;
     c->pending.erase(c->pending.begin());
   }
   return BSG_OK;
@@ -422,24 +428,19 @@ int32_t bsg_set_timing(bsg_ctx* c, int32_t enable) {
 
 int32_t bsg_step_timing(bsg_ctx* c, double* total_ms, int32_t* launches) {
   if (!c || !total_ms || !launches) return fail(BSG_E_INVALID_ARG, "bsg_step_timing: null argument%s%lld");
-  double tot = c->folded_ms;
-  int n = c->folded_n;
-  c->folded_ms = 0.0;
-  c->folded_n = 0;
-  for (auto& pr : c->pending) {
-    hipError_t e = hipEventSynchronize(pr.second);
-    if (e != hipSuccess) return hip_fail(e, "hipEventSynchronize");
-    float ms = 0.f;
-    e = hipEventElapsedTime(&ms, pr.first, pr.second);
-    if (e != hipSuccess) return hip_fail(e, "hipEventElapsedTime");
-    tot += ms;
-    ++n;
-    c->ev_pool.push_back(pr.first);
-    c->ev_pool.push_back(pr.second);
+  // fold every pending pair; on a failure the pairs folded so far stay in the totals
+  // (reported by the next call) and only the unfolded ones remain pending
+  for (size_t i = 0; i < c->pending.size(); ++i) {
+    if (int r = fold_pair(c, c->pending[i])) {
+      c->pending.erase(c->pending.begin(), c->pending.begin() + i);
+      return r;
+    }
   }
   c->pending.clear();
-  *total_ms = tot;
-  *launches = n;
+  *total_ms = c->folded_ms;
+  *launches = c->folded_n;
+  c->folded_ms = 0.0;
+  c->folded_n = 0;
   return BSG_OK;
 }
 

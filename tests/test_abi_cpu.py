@@ -129,6 +129,36 @@ def test_policy_host_validation_without_gpu():
     assert lib.bsg_policy_sac(C.byref(w), p, 0, 4, None, C.cast(act, C.c_void_p), None, None) == 0
 
 
+def test_policy_rejects_every_bad_pointer_argument():
+    """SACPolicy._check runs before any raw pointer reaches bsg_policy_sac: narrow obs
+    views, eps / out / log_prob on another device, strided log_prob.  The
+    policy object is built without a device (the checks are host logic), with the CPU as
+    its 'device' so that tensors on another device can be made here."""
+    import torch
+    from bluesky_gym.policy import SACPolicy
+    pol = SACPolicy.__new__(SACPolicy)
+    pol.device, pol.obs_dim, pol.act_dim = torch.device("cpu"), 4, 1
+    E = 8
+    big = torch.zeros((E, 10), dtype=torch.float32)
+    ok = dict(eps=torch.zeros((E, 1)), out=torch.zeros((E, 1), dtype=torch.float64),
+              log_prob=torch.zeros(E))
+    assert pol._check(big[:, 2:6], **ok) == E           # a 4-wide column view: stride 10, fine
+    with pytest.raises(ValueError, match="features"):
+        pol._check(big[:, 7:10], **ok)                   # 3 < obs_dim: would read past the row
+    with pytest.raises(ValueError, match="log_prob"):
+        pol._check(big, ok["eps"], ok["out"], torch.zeros((E, 2))[:, 0])   # strided [E] view
+    with pytest.raises(ValueError, match="obs"):
+        pol._check(big.double(), **ok)
+    meta = torch.device("meta")                          # "another device" without a GPU
+    with pytest.raises(ValueError, match="eps"):
+        pol._check(big, torch.zeros((E, 1), device=meta), ok["out"], ok["log_prob"])
+    with pytest.raises(ValueError, match="log_prob"):
+        pol._check(big, ok["eps"], ok["out"], torch.zeros(E, device=meta))
+    with pytest.raises(ValueError, match="out"):
+        pol._check(big, ok["eps"], torch.zeros((E, 1), dtype=torch.float64, device=meta),
+                   ok["log_prob"])
+
+
 def test_load_sb3_actor_from_zip(tmp_path):
     """SACPolicy.from_sb3_zip's loader: policy.pth inside an SB3 archive, weights only, actor.*
     keys (a synthetic archive of the SB3 layout; critic keys and the pickled `data` member

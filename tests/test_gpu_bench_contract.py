@@ -37,3 +37,8 @@ def test_bench_json_line():
     assert cb["value"] > 0 and cb["cores"] >= 1 and cb["kind"] in ("port", "reference")
     assert cb["per_env"]["value"] > 0
     assert "workload" in r["config"]
+    # the short C5 leg (BASELINE configs[4]) rides along in the default line
+    c5 = r["c5"]
+    assert c5["env_only"]["value"] > 0 and c5["env_policy"]["value"] > 0
+    assert c5["env_policy"]["value"] <= c5["env_only"]["value"] * 1.05
+    assert rf["scope"].startswith("per GPU") and rf["step_avg_ms"] == rf["kernel_avg_ms"]

@@ -37,7 +37,7 @@ def test_hip_adam_matches_torch_adam():
         assert torch.allclose(x, y, rtol=1e-5, atol=1e-7), (x - y).abs().max().item()
 
 
-@pytest.mark.parametrize("fused_dist", ["0"])
+@pytest.mark.parametrize("fused_dist", ["0", "1"])
 def test_sac_update_hip_adam_matches_fused_adam(monkeypatch, fused_dist):
     dev = torch.device("cuda", 0)
     out = []

@@ -101,6 +101,83 @@ def test_sharded_rows_match_one_batch(overlap):
         np.argwhere(got.view(np.uint32) != want.view(np.uint32))[:5]
 
 
+class _DelayedGather:
+    """A stand-in for RCCL's asynchronous all_gather_into_tensor with RCCL's stream
+    semantics: the collective's stream waits for the caller's stream at enqueue, then (here)
+    spins for a long delay before it reads the rows; Work.wait() makes the caller's
+    current stream wait for the copy's completion event (the host never blocks).
+    honour_wait=False is the negative control: a Work whose wait() orders nothing."""
+
+    def __init__(self, delay_cycles, honour_wait=True):
+        self.side = torch.cuda.Stream()
+        self.delay = delay_cycles
+        self.honour = honour_wait
+
+    def __call__(self, out, rows):
+        cur = torch.cuda.current_stream()
+        self.side.wait_stream(cur)
+        with torch.cuda.stream(self.side):
+            torch.cuda._sleep(self.delay)
+            out[: rows.shape[0]].copy_(rows)
+            done = torch.cuda.Event()
+            done.record(self.side)
+        honour = self.honour
+
+        class Work:
+            def wait(self):
+                if honour:
+                    torch.cuda.current_stream().wait_event(done)
+        return Work()
+
+
+def _ordering_run(gather, T_steps=64, E=256):
+    """ShardedVectorEnv (one rank) over the delayed gather, with no host sync between steps:
+    each step's gathered rows are cloned on the compute stream after ready.wait()."""
+    from bluesky_gym.parallel import ShardedVectorEnv
+    from bluesky_gym.vector import MergeVectorEnv
+    env = ShardedVectorEnv(lambda **kw: MergeVectorEnv(num_ac=32, seed=SEED, compute_cd=True,
+                                                       max_episode_steps=MAXEP, **kw),
+                           E, collective=gather)
+    g = torch.Generator().manual_seed(9)
+    acts = (torch.rand((T_steps, E, 2), dtype=torch.float64, generator=g) * 2 - 1).cuda()
+    hist = []
+    rows, ready = env.reset()
+    ready.wait()
+    hist.append(rows.clone())
+    for t in range(T_steps):
+        rows, ready = env.step(acts[t])
+        ready.wait()
+        hist.append(rows.clone())
+    torch.cuda.synchronize()
+    env.close()
+    return torch.stack(hist).cpu().numpy(), acts
+
+
+def test_overlapped_gather_never_reads_rewritten_rows():
+    """the stream ordering of ShardedVectorEnv's overlapped gather.  The
+    kernel of step t+2 rewrites the rows buffer step t's gather reads; _swap_in's
+    Work.wait() must order it after that (delayed) read.  Bit-exact against one batch over
+    64 steps with autoresets; the negative control (a wait() that orders nothing) must be
+    caught by the same comparison, so the test can see the hazard it guards against."""
+    from bluesky_gym import config, core
+    delay = 1_000_000                   # >> one 256-env step kernel at either clock rate
+    got, acts = _ordering_run(_DelayedGather(delay))
+    E = acts.shape[1]
+    b = core.DeviceBatch(config.merge_config(num_ac=32, max_episode_steps=MAXEP), E,
+                         compute_cd=True, seed=SEED, learner=True)
+    b.reset()
+    want = [b.learner.clone()]
+    for t in range(acts.shape[0]):
+        b.step(acts[t])
+        want.append(b.learner.clone())
+    want = torch.stack(want).cpu().numpy()
+    assert np.array_equal(got.view(np.uint32), want.view(np.uint32)), \
+        np.argwhere(got.view(np.uint32) != want.view(np.uint32))[:5]
+    bad, _ = _ordering_run(_DelayedGather(delay, honour_wait=False))
+    assert not np.array_equal(bad.view(np.uint32), want.view(np.uint32)), \
+        "the un-ordered control gathered correct rows: the delay does not expose the hazard"
+
+
 def test_reset_with_seed_is_reproducible():
     from bluesky_gym.vector import MergeVectorEnv
     env = MergeVectorEnv(num_envs=64, num_ac=16, seed=0)
@@ -131,3 +208,21 @@ def test_sector_capacity_overflow_raises():
     for _ in range(3):
         ok.step(np.zeros((64, 2)))
     ok.close()
+
+
+def test_sector_overflow_check_is_lazy_on_the_tensor_path():
+    """step_tensors() adds no host sync per call: the overflow flag is OR-ed on the device
+    and read back every OVERFLOW_CHECK_EVERY calls, so an overflowing batch
+    raises at that call and not before."""
+    import torch
+    from bluesky_gym.vector import SectorCRVectorEnv
+    env = SectorCRVectorEnv(num_envs=64, num_ac=8, seed=1)
+    with pytest.raises(RuntimeError, match="more aircraft"):
+        env.reset()                                  # the flag persists until the next reset
+    K = env.OVERFLOW_CHECK_EVERY
+    a = torch.zeros((64, 2), dtype=torch.float64, device=env.batch.device)
+    for _ in range(K - 1):
+        env.step_tensors(a)
+    with pytest.raises(RuntimeError, match="more aircraft"):
+        env.step_tensors(a)
+    env.close()

@@ -316,7 +316,9 @@ class SAC:
         # step together); fused | foreach: torch's Adam (A/B; the CPU tests use torch's)
         impl = os.environ.get("SAC_ADAM", "hip" if self.dev.type == "cuda" else "torch")
         self.hip_adam = impl == "hip"
-        self.actor.fused_dist = self.hip_adam and os.environ.get("SAC_FUSED_DIST", "0") == "1"
+        # SB3's squashed Gaussian as one launch each way (on by default once the whole-update
+        # equivalence test, tests/test_gpu_sac_adam.py, covers it; SAC_FUSED_DIST=0 = autograd)
+        self.actor.fused_dist = self.hip_adam and os.environ.get("SAC_FUSED_DIST", "1") == "1"
         if self.hip_adam:
             t = torch.zeros((), dtype=torch.float32, device=self.dev)
             self.opt_q = HipAdam(self.q.parameters(), lr, step=t)
