@@ -91,7 +91,7 @@ EXPORTED_SYMBOLS = (
     "bsg_abi_version", "bsg_last_error", "bsg_obs_dim", "bsg_action_dim", "bsg_spawn_width",
     "bsg_create", "bsg_destroy", "bsg_bind", "bsg_reset", "bsg_step", "bsg_set_timing",
     "bsg_step_timing", "bsg_set_stamps", "bsg_set_wind", "bsg_ctx_obs_dim", "bsg_geom_width",
-    "bsg_set_learner", "bsg_policy_sac",
+    "bsg_set_learner", "bsg_policy_sac", "bsg_lookahead_bytes", "bsg_set_lookahead",
 )
 
 
@@ -154,6 +154,10 @@ def load_library(path: str | None = None):
     lib.bsg_set_wind.argtypes = [C.c_void_p, C.POINTER(BsgWind)]
     lib.bsg_ctx_obs_dim.restype = C.c_int32
     lib.bsg_ctx_obs_dim.argtypes = [C.c_void_p]
+    lib.bsg_lookahead_bytes.restype = C.c_int64
+    lib.bsg_lookahead_bytes.argtypes = [C.c_void_p]
+    lib.bsg_set_lookahead.restype = C.c_int32
+    lib.bsg_set_lookahead.argtypes = [C.c_void_p, C.c_void_p, C.c_int64]
     lib.bsg_policy_sac.restype = C.c_int32
     lib.bsg_policy_sac.argtypes = [C.POINTER(BsgSacActor), C.c_void_p, C.c_int32, C.c_int32,
                                    C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]

@@ -18,9 +18,16 @@ F64_ENV = ("total_reward", "drift_sum", "target_alt", "final_altitude")
 
 
 class DeviceBatch:
+    # auto lookahead up to this many envs per GPU: below it the launch leaves SIMDs idle
+    # and the intruders' substeps are the critical path (C4 shards); DESIGN.md §3
+    LOOKAHEAD_MAX_ENVS = 2048
     def __init__(self, cfg: EnvKindConfig, num_envs: int, *, autoreset=nat.AUTORESET_NEXT_STEP,
                  compute_cd=True, seed=0, device=None, learner=False, env_offset=0,
-                 memo_cache=True):
+                 memo_cache=True, lookahead=None):
+        """lookahead: propagate Merge's intruders one RL step ahead in extra workgroups
+        (bsg_set_lookahead; bit-identical results).  None = on where the library supports
+        it and the batch is small enough to leave SIMDs idle (LOOKAHEAD_MAX_ENVS); True /
+        False force it."""
         if not torch.cuda.is_available():
             raise nat.BsgError("bluesky_gym needs a HIP device (MI355X); none is visible")
         self.lib = nat.load_library()
@@ -49,6 +56,18 @@ class DeviceBatch:
         self._ctx = ctx
         self._alloc()
         self._bind()
+        self.lookahead = False
+        self._la_buf = None
+        nbytes = int(self.lib.bsg_lookahead_bytes(self._ctx))
+        want = (lookahead if lookahead is not None
+                else self.E <= self.LOOKAHEAD_MAX_ENVS)
+        if want and nbytes > 0:
+            self._la_buf = torch.empty((nbytes + 7) // 8, dtype=torch.float64, device=self.device)
+            nat.check(self.lib.bsg_set_lookahead(self._ctx, C.c_void_p(self._la_buf.data_ptr()),
+                                                 nbytes), "bsg_set_lookahead")
+            self.lookahead = True
+        elif lookahead:
+            raise nat.BsgError("lookahead: MergeEnv with NEXT_STEP (or no) autoreset only")
 
     # ------------------------------------------------------------------ buffers
     def _alloc(self):
@@ -140,6 +159,15 @@ class DeviceBatch:
                     else ptype())
         self._bufs = b
         nat.check(self.lib.bsg_bind(self._ctx, C.byref(b)), "bsg_bind")
+
+    def invalidate_caches(self):
+        """After writing self.state directly: the memo cache and the lookahead restart
+        from the buffers (bsg.h: memo_cache, bsg_set_lookahead)."""
+        if self.memo_cache is not None:
+            self.memo_cache.fill_(float("nan"))
+        if self._la_buf is not None:
+            nat.check(self.lib.bsg_set_lookahead(self._ctx, C.c_void_p(self._la_buf.data_ptr()),
+                                                 self._la_buf.numel() * 8), "bsg_set_lookahead")
 
     def set_learner(self, rows: torch.Tensor | None):
         """Point the kernel's learner-row output at `rows` ([E, obs_dim + 3] fp32 on this

@@ -34,6 +34,14 @@ struct bsg_ctx {
   std::vector<std::pair<hipEvent_t, hipEvent_t>> pending;
   double folded_ms = 0.0;          // timed launches already folded out of `pending`
   int folded_n = 0;
+  // lookahead scratch (bsg_set_lookahead): slot parity, tag generation, and what the next
+  // launch must re-initialise first (la_dirty: the scratch; memo_dirty: the caller's
+  // memo_cache, whose intruder entries the main workgroups do not keep current while the
+  // lookahead runs)
+  double* la = nullptr;
+  int la_par = 0;
+  uint32_t la_gen = 0;
+  bool la_dirty = false, memo_dirty = false, la_was_active = false;
 };
 
 namespace {
@@ -79,6 +87,8 @@ int wind_obs_pos(const bsg_config& cfg) {
   }
 }
 
+bool la_active(const bsg_ctx* c);
+
 bsg::KParams make_params(const bsg_ctx* c, int mode) {
   bsg::KParams p;
   std::memset(&p, 0, sizeof(p));
@@ -96,7 +106,44 @@ bsg::KParams make_params(const bsg_ctx* c, int mode) {
   p.lds_pad = c->lds_pad;
   p.wind = c->wind;
   p.wpos = wind_obs_pos(c->cfg);
+  p.la = la_active(c) ? c->la : nullptr;
+  p.la_par = c->la_par;
+  p.la_gen = c->la_gen;
   return p;
+}
+
+// the lookahead runs for a bound Merge scratch without a wind field (bsg_set_lookahead
+// refuses the configurations it cannot serve: other kinds, SAME_STEP autoreset)
+bool la_active(const bsg_ctx* c) { return c->la != nullptr && c->wind.np == 0; }
+
+size_t la_bytes(const bsg_config& cfg) {
+  return 8 * bsg::la_doubles((size_t)cfg.num_envs, (size_t)cfg.num_ac);
+}
+
+// Before a launch: re-initialise what a lookahead transition left stale (0xFF bytes = a
+// NaN double: a memo miss / a tag no generation produces), on the launch stream.
+int la_prepare(bsg_ctx* c, hipStream_t st) {
+  const bool act = la_active(c);
+  if (act != c->la_was_active) {
+    c->la_dirty = c->la_dirty || act;
+    c->memo_dirty = true;
+    c->la_was_active = act;
+  }
+  if (c->memo_dirty && c->bufs.memo_cache) {
+    const size_t EN = (size_t)c->cfg.num_envs * c->cfg.num_ac;
+    hipError_t e = hipMemsetAsync(c->bufs.memo_cache, 0xFF,
+                                  8 * (2 * EN + 4 * (size_t)c->cfg.num_envs), st);
+    if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(memo_cache)");
+  }
+  c->memo_dirty = false;
+  if (act && c->la_dirty) {
+    hipError_t e = hipMemsetAsync(c->la, 0xFF, la_bytes(c->cfg), st);
+    if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(lookahead)");
+    c->la_gen = (c->la_gen % 0x7ffe) + 1;
+    c->la_par = 0;
+    c->la_dirty = false;
+  }
+  return BSG_OK;
 }
 
 // A caller that enables timing and never polls bsg_step_timing must not grow `pending`
@@ -143,10 +190,16 @@ int trim_pending(bsg_ctx* c) {
   return BSG_OK;
 }
 
-int launch(bsg_ctx* c, const bsg::KParams& p, void* stream) {
+int launch(bsg_ctx* c, int mode, const double* actions, const double* spawn,
+           const uint8_t* env_mask, void* stream) {
   hipError_t e = hipSetDevice(c->cfg.device);
   if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (int r = la_prepare(c, st)) return r;
+  bsg::KParams p = make_params(c, mode);
+  p.actions = actions;
+  p.spawn = spawn;
+  p.env_mask = env_mask;
   hipEvent_t t0 = nullptr, t1 = nullptr;
   const bool timed = c->timing > 0 && (c->launch_count++ % c->timing) == 0;
   if (timed) {
@@ -177,6 +230,7 @@ int launch(bsg_ctx* c, const bsg::KParams& p, void* stream) {
     }
     c->pending.emplace_back(t0, t1);
   }
+  if (p.la && mode == bsg::MODE_STEP) c->la_par ^= 1;   // this step wrote the other slot
   return BSG_OK;
 }
 
@@ -324,6 +378,31 @@ int32_t bsg_bind(bsg_ctx* c, const bsg_buffers* b) {
     return fail(BSG_E_INVALID_ARG, "bsg_bind: compute_cd needs conf_mask/los_mask/tcpamax/min_sep%s%lld");
   c->bufs = *b;
   c->bound = true;
+  c->la_dirty = true;               // new buffers: the lookahead restarts from them
+  return BSG_OK;
+}
+
+int64_t bsg_lookahead_bytes(const bsg_ctx* c) {
+  if (!c) return fail(BSG_E_INVALID_ARG, "bsg_lookahead_bytes: null ctx%s%lld");
+  if (c->cfg.env_kind != BSG_ENV_MERGE || c->cfg.autoreset_mode == BSG_AUTORESET_SAME_STEP)
+    return 0;
+  return (int64_t)la_bytes(c->cfg);
+}
+
+int32_t bsg_set_lookahead(bsg_ctx* c, void* scratch, int64_t bytes) {
+  if (!c) return fail(BSG_E_INVALID_ARG, "bsg_set_lookahead: null ctx%s%lld");
+  if (scratch) {
+    if (bsg_lookahead_bytes(c) == 0)
+      return fail(BSG_E_UNSUPPORTED, "bsg_set_lookahead: MergeEnv with NEXT_STEP or no autoreset "
+                  "only%s%lld");
+    if (bytes < (int64_t)la_bytes(c->cfg))
+      return fail(BSG_E_INVALID_ARG, "bsg_set_lookahead: scratch too small%s (need %lld bytes)", "",
+                  (long long)la_bytes(c->cfg));
+    if (reinterpret_cast<uintptr_t>(scratch) & 7)
+      return fail(BSG_E_INVALID_ARG, "bsg_set_lookahead: scratch must be 8-byte aligned%s%lld");
+  }
+  c->la = static_cast<double*>(scratch);
+  c->la_dirty = true;               // also re-arms after the caller wrote state directly
   return BSG_OK;
 }
 
@@ -337,20 +416,14 @@ int32_t bsg_set_learner(bsg_ctx* c, float* learner) {
 int32_t bsg_reset(bsg_ctx* c, const uint8_t* env_mask, const double* spawn, void* stream) {
   if (!c) return fail(BSG_E_INVALID_ARG, "bsg_reset: null ctx%s%lld");
   if (!c->bound) return fail(BSG_E_STATE, "bsg_reset: buffers not bound%s%lld");
-  bsg::KParams p = make_params(c, bsg::MODE_RESET);
-  p.env_mask = env_mask;
-  p.spawn = spawn;
-  return launch(c, p, stream);
+  return launch(c, bsg::MODE_RESET, nullptr, spawn, env_mask, stream);
 }
 
 int32_t bsg_step(bsg_ctx* c, const double* actions, const double* spawn, void* stream) {
   if (!c) return fail(BSG_E_INVALID_ARG, "bsg_step: null ctx%s%lld");
   if (!c->bound) return fail(BSG_E_STATE, "bsg_step: buffers not bound%s%lld");
   if (!actions) return fail(BSG_E_INVALID_ARG, "bsg_step: actions is NULL%s%lld");
-  bsg::KParams p = make_params(c, bsg::MODE_STEP);
-  p.actions = actions;
-  p.spawn = spawn;
-  return launch(c, p, stream);
+  return launch(c, bsg::MODE_STEP, actions, spawn, nullptr, stream);
 }
 
 int32_t bsg_set_wind(bsg_ctx* c, const bsg_wind* w) {
@@ -374,6 +447,7 @@ int32_t bsg_set_wind(bsg_ctx* c, const bsg_wind* w) {
   c->wind = d;
   c->obs_dim = base + (d.augment ? 2 : 0);
   c->bound = false;
+  c->la_dirty = true;
   return BSG_OK;
 }
 

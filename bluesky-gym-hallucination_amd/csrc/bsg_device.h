@@ -138,6 +138,19 @@ constexpr AtmosK kAtmosSL_K = {kAtmosSL, 0x1.5a535faa0890cp+19, 0x1.7a76ee408d54
                                0x1.4b2810787baa0p-17, 0x1.1ab6ffb9d2bf5p+19,
                                0x1.544b42cc9d77cp+8, 0x1.812c3ee51ffb9p-9};
 
+// PerfModel.limits' CAS clamp at those two atmospheres, as TAS: vcas2tas(vmin), vcas2tas(vmax)
+// for the airborne envelope and for phase GD (vmin 0 -> 0), the values NumPy computes
+// (tests/test_fastmath_cpu.py checks the literals against oracle/bluesky_subset.vcas2tas).
+// limits() converts ap_tas to CAS, clamps, and converts back at one constant atmosphere;
+// vtas2cas and vcas2tas are inverse and increasing, so the clamp is decided on ap_tas
+// against these thresholds and an unclamped ap_tas is its own round trip (NumPy's round
+// trip returns it within its own cancellation error, < 1e-13 relative over 60..300 m/s:
+// the (1 + x)^3.5 - 1 and y^(2/7) - 1 steps).  Saves four powers, two square roots and
+// two divisions on the climbing / descending aircraft's substep chain.
+struct LimK { double tvmin, tvmax, tvmax_gd; };
+constexpr LimK kLimHMAX = {0x1.1a6f5cb8f15bcp+7, 0x1.2959d9f9eb8a9p+8, 0x1.5760fe910b786p+7};
+constexpr LimK kLimSL = {0x1.2016b11c07f8ap+6, 0x1.45fffffdd454fp+7, 0x1.61ffffff45996p+6};
+
 // vtas2cas / vcas2tas: both powers by polynomial with one range test for the pair (a
 // branch is ~80 cycles of latency even when not taken); outside, both by the libm.
 __device__ __forceinline__ double tas2cas_at(double tas, const Atmos& a) {

@@ -26,6 +26,15 @@ struct WindDev {
   const double *lat, *lon, *vn, *ve;
 };
 
+// Lookahead scratch layout (bsg_set_lookahead; bsg_kernels.hip lookahead_role), in doubles
+// for EN = E*N: two slots of LA_F fields x EN, the lookahead blocks' memo [LA_MC][EN], two
+// tag rows [E] (u64).
+constexpr int LA_F = 10;
+constexpr int LA_MC = 2;           // = MC_FIELDS (bsg_kernels.hip)
+__host__ __device__ constexpr size_t la_doubles(size_t E, size_t N) {
+  return (2 * LA_F + LA_MC) * E * N + 2 * E;
+}
+
 // Passed by value to every launch (kernarg segment).
 struct KParams {
   bsg_config cfg;
@@ -41,6 +50,12 @@ struct KParams {
   unsigned lds_pad;          // extra dynamic LDS per workgroup (occupancy shaping)
   WindDev wind;
   int wpos;                  // obs offset of wind_u (sorted-key position) when augmenting
+  // lookahead (bsg_set_lookahead; Merge, no wind, not SAME_STEP): workgroups
+  // [la_grid0, 2*la_grid0) propagate the intruders one RL step ahead into `la`
+  double* la;                // scratch (layout: bsg_kernels.hip la_*), nullptr = off
+  int la_par;                // slot the main workgroups read (a step's lookahead writes 1 - la_par)
+  uint32_t la_gen;           // generation: tags of other generations are stale
+  int la_grid0;              // main workgroups (set by the launcher)
 };
 
 hipError_t launch_step(const KParams& p, hipStream_t stream);

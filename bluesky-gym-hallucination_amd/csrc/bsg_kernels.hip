@@ -491,14 +491,17 @@ __device__ __forceinline__ void substep(AC& s, Memo& m, double dt, const RouteRe
       double allow_tas;
       const bool khi = bits(allow_h) == bits(HMAX);
       if (hb != ab && (khi || allow_h == 0.0)) {
-        // the Vertical/Descent commands (selalt 1e6 or 0): a constant atmosphere whose
-        // divisors have precomputed reciprocals
+        // the Vertical/Descent commands (selalt 1e6 or 0): a constant atmosphere, so the
+        // CAS clamp is a TAS clamp against NumPy's own converted limits (bsg_device.h LimK)
+        // and the Mach cap a TAS cap (snd_k > 0: allow_tas / snd_k > MMO <=> allow_tas >
+        // MMO * snd_k up to the last bit, whose two sides give the same value either way)
         const AtmosK& k = khi ? kAtmosHMAX_K : kAtmosSL_K;
-        const double intent_cas = tas2cas_k(m.ap_tas, k);
-        double allow_cas = intent_cas < vmin ? vmin : intent_cas;
-        allow_cas = intent_cas > vmax ? vmax : allow_cas;
-        allow_tas = cas2tas_k(allow_cas, k);
-        if (div_r_nn(allow_tas, k.snd, k.r_snd) > MMO) allow_tas = MMO * k.snd;   // allow_tas >= 0
+        const LimK& lk = khi ? kLimHMAX : kLimSL;
+        const double tvmin = gd ? 0.0 : lk.tvmin, tvmax = gd ? lk.tvmax_gd : lk.tvmax;
+        allow_tas = m.ap_tas < tvmin ? tvmin : m.ap_tas;
+        allow_tas = m.ap_tas > tvmax ? tvmax : allow_tas;
+        const double tmmo = MMO * k.snd;
+        if (allow_tas > tmmo) allow_tas = tmmo;
       } else {
         const Atmos ah = (hb == ab) ? memo_at(m, s.alt, ab) : vatmos(allow_h);
         const double intent_cas = tas2cas_at(m.ap_tas, ah);
@@ -1488,11 +1491,13 @@ constexpr int kActDim = (KIND == BSG_ENV_MERGE || KIND == BSG_ENV_STATIC_OBSTACL
                          KIND == BSG_ENV_SECTOR_CR) ? 2 : 1;
 
 // act: the env's action row, mc: its memo-cache entries (both fetched at kernel entry)
+// mcache: the memo-cache buffer this aircraft's entries live in (b.memo_cache; the
+// lookahead blocks' own region; nullptr = no memo -- the same bits, computed in full)
 template <int KIND, bool WIND>
 __device__ __forceinline__ void propagate(const KParams& p, int e, int j, size_t a, AC& s,
                                           EnvScalars& ev, double& sub_reward, bool& sub_done,
                                           const double act[2], const double mc[MC_FIELDS],
-                                          const double oat[4]) {
+                                          const double oat[4], double* mcache) {
   const Buffers& b = p.b;
   const int N = p.N;
   const AC s0 = s;                  // as loaded: the cross-step memo's keys (memo_load)
@@ -1519,8 +1524,8 @@ __device__ __forceinline__ void propagate(const KParams& p, int e, int j, size_t
   if (S > 0) {
     Memo m;
     memo_init(m, s);
-    if (b.memo_cache) memo_load(m, mc, s0);
-    if (j == 0) { m.alt_bits = bits(oat[0]); m.at = Atmos{oat[1], oat[2], oat[3]}; }
+    if (mcache) memo_load(m, mc, s0);
+    if (j == 0 && mcache) { m.alt_bits = bits(oat[0]); m.at = Atmos{oat[1], oat[2], oat[3]}; }
     RouteRegs rt;
     rt.load(p.route);
     memo_lnav(m, s, rt);
@@ -1574,12 +1579,107 @@ __device__ __forceinline__ void propagate(const KParams& p, int e, int j, size_t
 #endif
     }
     memo_final_cas(m, s);
-    if (b.memo_cache) memo_store(m, s, mc, b.memo_cache, a, (size_t)p.E * N);
-    if (j == 0 && b.memo_cache && m.alt_bits != bits(oat[0])) {
-      double* t = b.memo_cache + (size_t)MC_FIELDS * p.E * N + (size_t)e * 4;
+    if (mcache) memo_store(m, s, mc, mcache, a, (size_t)p.E * N);
+    if (j == 0 && mcache && m.alt_bits != bits(oat[0])) {
+      double* t = mcache + (size_t)MC_FIELDS * p.E * N + (size_t)e * 4;
       t[0] = key_as_double(m.alt_bits); t[1] = m.at.p; t[2] = m.at.rho; t[3] = m.at.T;
     }
   }
+}
+
+// ---- lookahead: the Merge intruders one RL step ahead ------------------------------------
+// Merge's intruders fly LNAV to FIX then RWY at constant speed and altitude (RESO OFF,
+// merge_env.py:155-157): their next step depends neither on the ownship nor on the
+// action.  With a lookahead scratch bound (bsg_set_lookahead), a step launch has twice the
+// workgroups: the main ones consume the intruders' post-step states the previous launch
+// computed and propagate only the ownship before the observation/CD phases, while the
+// lookahead ones (blockIdx >= la_grid0, one wave each) propagate the intruders one step
+// further.  So the intruders' ten substeps leave the launch's critical path (a C4 shard of
+// 512 envs runs one wave per SIMD: its time is that path).  The same substep() runs on the
+// same inputs: the states are bit-identical to the inline path (tests/test_gpu_lookahead.py).
+// Scratch (doubles, EN = E*N): two slots of LA_F fields x EN (lat lon alt hdg tas cas vs ax
+// ap_trk, nav bits; selspd/selalt/selvs never change for an intruder), the lookahead
+// blocks' own memo [MC_FIELDS][EN], then two tag rows [E] (u64).  A slot entry is valid for
+// the launch whose env scalars give the same tag (episode, step_count, generation).
+static_assert(LA_MC == MC_FIELDS, "lookahead memo layout");
+
+__device__ __forceinline__ uint64_t la_tag(uint32_t episode, int step, uint32_t gen) {
+  return ((uint64_t)(gen & 0x7fffu) << 48) | ((uint64_t)(episode & 0xffffffu) << 24) |
+         (uint64_t)((uint32_t)step & 0xffffffu);
+}
+
+__device__ __forceinline__ void la_load(const double* slot, size_t a, size_t EN, AC& s) {
+  s.lat = slot[a]; s.lon = slot[EN + a]; s.alt = slot[2 * EN + a]; s.hdg = slot[3 * EN + a];
+  s.tas = slot[4 * EN + a]; s.cas = slot[5 * EN + a]; s.vs = slot[6 * EN + a];
+  s.ax = slot[7 * EN + a]; s.ap_trk = slot[8 * EN + a];
+  s.nav = (int)__double_as_longlong(slot[9 * EN + a]);
+}
+
+__device__ __forceinline__ void la_store(double* slot, size_t a, size_t EN, const AC& s) {
+  slot[a] = s.lat; slot[EN + a] = s.lon; slot[2 * EN + a] = s.alt; slot[3 * EN + a] = s.hdg;
+  slot[4 * EN + a] = s.tas; slot[5 * EN + a] = s.cas; slot[6 * EN + a] = s.vs;
+  slot[7 * EN + a] = s.ax; slot[8 * EN + a] = s.ap_trk;
+  slot[9 * EN + a] = __longlong_as_double((long long)s.nav);
+}
+
+// One lookahead wave: the intruders of the same 64/GS envs as main workgroup
+// (blockIdx - la_grid0).  Post-step state of this launch: a spawn (resetting env), the
+// slot the main workgroups read (valid tag), or -- priming, after the scratch was (re)bound
+// -- this launch's step computed here too; then one more step into the other slot (a reset
+// launch writes the slot the next step reads).
+template <int KIND, int GS, bool WIND>
+__device__ __forceinline__ void lookahead_role(const KParams& p) {
+  if (threadIdx.x >= 64) return;
+  const int lane = threadIdx.x;
+  const int g = lane / GS, j = lane % GS;
+  const int e = ((int)blockIdx.x - p.la_grid0) * (64 / GS) + g;
+  const int N = p.N;
+  if (e >= p.E || j == 0 || j >= N) return;
+  const Buffers& b = p.b;
+  const size_t EN = (size_t)p.E * N;
+  const size_t a = (size_t)e * N + j;
+  double* memo = p.la + 2 * LA_F * EN;
+  uint64_t* tags = reinterpret_cast<uint64_t*>(p.la + (2 * LA_F + MC_FIELDS) * EN);
+  EnvScalars ev = {};
+  load_env(b, e, ev);
+  bool resetting;
+  if (p.mode == MODE_RESET) resetting = p.env_mask ? (p.env_mask[e] != 0) : true;
+  else resetting = (p.cfg.autoreset_mode == BSG_AUTORESET_NEXT_STEP) && (ev.flags & 1);
+  if (!resetting && p.mode != MODE_STEP) return;            // untouched by a masked reset
+  const double act[2] = {0.0, 0.0};
+  const double oat[4] = {0.0, 0.0, 0.0, 0.0};
+  double mc[MC_FIELDS];
+  double sub_reward = 0.0;
+  bool sub_done = false;
+  AC s = {};
+  uint64_t tag_out;
+  if (resetting) {
+    double aux[4] = {ev.target_alt, 0.0, 0.0, 0.0};
+    spawn<KIND>(p, e, j, ev.episode, s, aux, false);
+    memo_invalidate(memo, a, EN);
+#pragma unroll
+    for (int f = 0; f < MC_FIELDS; ++f) mc[f] = key_as_double(kNoKey);
+    tag_out = la_tag(ev.episode + 1u, 0, p.la_gen);
+  } else {
+    const double* rslot = p.la + (size_t)p.la_par * LA_F * EN;
+    if (tags[(size_t)p.la_par * p.E + e] == la_tag(ev.episode, ev.step_count, p.la_gen)) {
+      load_ac<false>(b, a, s);                   // selspd / selalt / selvs
+      la_load(rslot, a, EN, s);
+      memo_fetch(mc, memo, a, EN);
+    } else {
+      load_ac<false>(b, a, s);
+      memo_invalidate(memo, a, EN);
+#pragma unroll
+      for (int f = 0; f < MC_FIELDS; ++f) mc[f] = key_as_double(kNoKey);
+      propagate<KIND, WIND>(p, e, j, a, s, ev, sub_reward, sub_done, act, mc, oat, memo);
+      memo_fetch(mc, memo, a, EN);
+    }
+    tag_out = la_tag(ev.episode, ev.step_count + 1, p.la_gen);
+  }
+  propagate<KIND, WIND>(p, e, j, a, s, ev, sub_reward, sub_done, act, mc, oat, memo);
+  const int wslot = p.mode == MODE_STEP ? 1 - p.la_par : p.la_par;
+  la_store(p.la + (size_t)wslot * LA_F * EN, a, EN, s);
+  if (j == 1) tags[(size_t)wslot * p.E + e] = tag_out;
 }
 
 // CDW: waves per workgroup.  Wave 0 owns the workgroup's 64/GS envs as always; waves 1..CDW-1
@@ -1592,6 +1692,13 @@ __global__ __launch_bounds__(64 * CDW) void step_kernel(KParams p) {
   BSG_STAMP(0, __builtin_amdgcn_s_memrealtime());
   BSG_STAMP(1, stamp_clock());
 #endif
+  constexpr bool kLA = KIND == BSG_ENV_MERGE && !WIND;
+  if constexpr (kLA) {
+    if (p.la && (int)blockIdx.x >= p.la_grid0) {
+      lookahead_role<KIND, GS, WIND>(p);
+      return;                                  // the whole workgroup: no barrier below
+    }
+  }
   __shared__ Lds<WIND> L;
   const int lane = threadIdx.x & 63;
   const int wv = CDW > 1 ? (int)(threadIdx.x >> 6) : 0;   // CD helper waves: wv > 0
@@ -1620,16 +1727,28 @@ __global__ __launch_bounds__(64 * CDW) void step_kernel(KParams p) {
 #pragma unroll
     for (int k = 0; k < kActDim<KIND>; ++k) act[k] = p.actions[(size_t)e * kActDim<KIND> + k];
   }
+  // lookahead on: the intruders' memo entries belong to the lookahead blocks; an
+  // intruder's post-step state comes from the slot when its tag matches
+  const bool la_intr = kLA && p.la != nullptr && j > 0;
+  double* const mcache = la_intr ? nullptr : b.memo_cache;
+  AC s_la = {};
+  uint64_t la_tag_in = 0;
+  if (la_intr && ok && p.mode == MODE_STEP) {
+    const size_t EN = (size_t)p.E * N;
+    la_load(p.la + (size_t)p.la_par * LA_F * EN, a, EN, s_la);
+    la_tag_in = reinterpret_cast<const uint64_t*>(p.la + (2 * LA_F + MC_FIELDS) * EN)
+        [(size_t)p.la_par * p.E + e];
+  }
   double mc[MC_FIELDS];
 #pragma unroll
   for (int f = 0; f < MC_FIELDS; ++f) mc[f] = key_as_double(kNoKey);
-  if (ok && b.memo_cache && p.mode == MODE_STEP && p.cfg.action_frequency > 0)
-    memo_fetch(mc, b.memo_cache, a, (size_t)p.E * N);
+  if (ok && mcache && p.mode == MODE_STEP && p.cfg.action_frequency > 0)
+    memo_fetch(mc, mcache, a, (size_t)p.E * N);
   // the ownship's atmosphere memo (key = altitude bits, then p, rho, T): vatmos is a pure
   // function of the altitude, so an entry is valid whenever its key matches -- a level
   // ownship skips the pow + exp its speed chain would open with every RL step
   double oat[4] = {key_as_double(kNoKey), 0.0, 0.0, 0.0};
-  if (ok && j == 0 && b.memo_cache && p.mode == MODE_STEP && p.cfg.action_frequency > 0) {
+  if (ok && j == 0 && mcache && p.mode == MODE_STEP && p.cfg.action_frequency > 0) {
     const double* t = b.memo_cache + (size_t)MC_FIELDS * p.E * N + (size_t)e * 4;
 #pragma unroll
     for (int k = 0; k < 4; ++k) oat[k] = t[k];
@@ -1668,9 +1787,17 @@ __global__ __launch_bounds__(64 * CDW) void step_kernel(KParams p) {
     AC s = (!resetting || keep) ? s_in : AC{};
     if (ok) {
       if (resetting) spawn<KIND>(p, e, j, ev.episode, s, aux, keep);
-      if (stepping && on) propagate<KIND, WIND>(p, e, j, a, s, ev, sub_reward, sub_done, act, mc, oat);
+      if (stepping && on) {
+        if (la_intr && la_tag_in == la_tag(ev.episode, ev.step_count, p.la_gen)) {
+          s.lat = s_la.lat; s.lon = s_la.lon; s.alt = s_la.alt; s.hdg = s_la.hdg;
+          s.tas = s_la.tas; s.cas = s_la.cas; s.vs = s_la.vs; s.ax = s_la.ax;
+          s.ap_trk = s_la.ap_trk; s.nav = s_la.nav;
+        } else {
+          propagate<KIND, WIND>(p, e, j, a, s, ev, sub_reward, sub_done, act, mc, oat, mcache);
+        }
+      }
       if (active) store_ac_changed<WIND>(b, a, s, s_in);
-      if (resetting && b.memo_cache) memo_invalidate(b.memo_cache, a, (size_t)p.E * N);
+      if (resetting && mcache) memo_invalidate(mcache, a, (size_t)p.E * N);
     }
     if (resetting && j == 0) {
       reset_scalars<KIND>(ev, aux);
@@ -2022,18 +2149,27 @@ __global__ __launch_bounds__(64 * CDW) void step_kernel(KParams p) {
 
 // ---------------------------------------------------------------------------------------
 template <int KIND, bool WIND>
-static hipError_t launch_kind_w(const KParams& p, hipStream_t st) {
+static hipError_t launch_kind_w(const KParams& p0, hipStream_t st) {
   int gs = 1;
-  while (gs < p.N) gs <<= 1;
+  while (gs < p0.N) gs <<= 1;
   const int epb = 64 / gs;
-  const int grid = (p.E + epb - 1) / epb;
+  const int grid0 = (p0.E + epb - 1) / epb;
+  KParams p = p0;
+  p.la_grid0 = grid0;
+  if (!(KIND == BSG_ENV_MERGE && !WIND)) p.la = nullptr;
+  const int grid = p.la ? 2 * grid0 : grid0;
 #define BSG_CASE(G) \
   case G: hipLaunchKernelGGL((step_kernel<KIND, G, WIND>), dim3(grid), dim3(64), p.lds_pad, st, p); break;
   if constexpr (KIND == BSG_ENV_MERGE && !WIND) {
     // small batches (C4's per-GPU shards): CD helper waves while the workgroups, at 2..4
     // waves each, still fit the 2 waves per SIMD the step kernel's VGPRs allow on 1,024
     // SIMDs -- 512 envs x 32: 256 workgroups x 4 waves, 1,024 envs: 512 x 4, 2,048: 1,024 x 2
-    const int cdw = (!p.cfg.compute_cd || gs < 32) ? 1 : (grid <= 512 ? 4 : (grid <= 1024 ? 2 : 1));
+    // with the lookahead the grid doubles: fewer helper waves so that all of it is resident
+    // at once (2 waves per SIMD x 1,024 SIMDs), or the lookahead blocks would queue behind
+    // the main ones (1,024 envs at 4 waves: 98.6 us against 45.8 without the lookahead)
+    const int slots = p.la ? 1024 : 2048;     // waves per copy of the grid
+    const int cdw = (!p.cfg.compute_cd || gs < 32) ? 1
+                    : (grid0 * 4 <= slots ? 4 : (grid0 * 2 <= slots ? 2 : 1));
 #define BSG_CASE_CD(G, W) \
   case G: hipLaunchKernelGGL((step_kernel<KIND, G, WIND, W>), dim3(grid), dim3(64 * W), p.lds_pad, st, p); break;
     if (cdw == 4) {

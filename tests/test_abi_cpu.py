@@ -17,7 +17,7 @@ HDR = os.path.join(REPO, "include", "bsg.h")
 
 def declared_functions():
     src = open(HDR).read()
-    return sorted(set(re.findall(r"^\s*(?:int32_t|const char\*)\s+(bsg_\w+)\s*\(", src, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int32_t|int64_t|const char\*)\s+(bsg_\w+)\s*\(", src, re.M)))
 
 
 def test_header_declares_the_ctypes_symbol_set():

@@ -71,3 +71,23 @@ def test_constant_atmosphere_divisors():
         snd = float(np.sqrt(1.4 * 287.05287 * T))
         want = [p7, 1.0 / p7, 1.0 / p, p7 / rho, snd, 1.0 / snd]
         assert got == want, (name, got, want)
+
+
+def test_constant_atmosphere_clamp_thresholds():
+    """kLim*: PerfModel.limits' CAS clamp at the two constant atmospheres as TAS values --
+    vcas2tas(vmin), vcas2tas(vmax), vcas2tas(vmax_gd) -- exactly as the oracle (NumPy)
+    computes them (bsg_device.h LimK), and ordered as the clamp needs."""
+    txt = open(os.path.join(CSRC, "bsg_device.h")).read()
+    for name, h in (("kLimHMAX", bs.HMAX), ("kLimSL", 0.0)):
+        lits = re.search(rf"constexpr LimK {name} = \{{([^}}]+)\}};", txt).group(1).split(",")
+        got = [float.fromhex(v.strip()) for v in lits]
+        want = [float(bs.vcas2tas(np.float64(c), np.float64(h)))
+                for c in (bs.VMIN_CAS, bs.VMAX_CAS, bs.VMAX_GD)]
+        assert got == want, (name, got, want)
+        assert 0.0 < got[0] < got[1]
+    # the round trip the threshold form replaces: NumPy's tas -> cas -> tas at the constant
+    # atmospheres returns its argument within 1e-13 relative over the flown speed range
+    for h in (bs.HMAX, 0.0):
+        tas = np.linspace(60.0, 300.0, 2001)
+        rt = bs.vcas2tas(bs.vtas2cas(tas, np.float64(h)), np.float64(h))
+        assert np.max(np.abs(rt / tas - 1.0)) < 1e-13

@@ -59,8 +59,13 @@ def test_sac_update_hip_adam_matches_fused_adam(monkeypatch, fused_dist):
         torch.cuda.synchronize()
         out.append([p.detach().clone() for p in
                     list(s.actor.parameters()) + list(s.q.parameters()) + [s.log_alpha]])
+    # SAC_FUSED_DIST=1: the squashed Gaussian's backward is written out (bsg fused kernel)
+    # in another association than autograd's, so the gradients differ in the last bits and
+    # ten Adam steps (which normalise them) leave parameters within 1e-5 absolute (measured
+    # 3.2e-6 on weights of ~0.05); without it the two optimizers agree to 1e-6
+    atol = 1e-5 if fused_dist == "1" else 1e-6
     for x, y in zip(*out):
-        assert torch.allclose(x, y, rtol=1e-4, atol=1e-6), (x - y).abs().max().item()
+        assert torch.allclose(x, y, rtol=1e-4, atol=atol), (x - y).abs().max().item()
 
 
 def test_replay_insert_kernel_matches_torch_insert():

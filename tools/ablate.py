@@ -5,9 +5,9 @@ sys.path[:0] = [os.getcwd(), os.path.join(os.getcwd(), "bluesky-gym-hallucinatio
 import torch
 from bluesky_gym import core, config
 
-def run(cfg, E, cd, steps=60, warm=10):
+def run(cfg, E, cd, steps=60, warm=10, la=None):
     b = core.DeviceBatch(cfg, E, compute_cd=cd, seed=1,
-                         memo_cache=os.environ.get("BSG_NO_MEMO", "0") != "1")
+                         memo_cache=os.environ.get("BSG_NO_MEMO", "0") != "1", lookahead=la)
     b.reset()
     act = torch.rand((8, E, b.act_dim), dtype=torch.float64, device="cuda") * 2 - 1
     for k in range(warm):
@@ -27,7 +27,7 @@ def run(cfg, E, cd, steps=60, warm=10):
 
 only = set(sys.argv[1:])
 res = {}
-for name, cfg, E, cd in [
+for spec in [
     ("merge32_full", config.merge_config(num_ac=32), 4096, True),
     ("merge32_nocd", config.merge_config(num_ac=32), 4096, False),
     ("merge32_S1", config.merge_config(num_ac=32, action_frequency=1), 4096, True),
@@ -46,9 +46,16 @@ for name, cfg, E, cd in [
     ("merge32_nocd_2048", config.merge_config(num_ac=32), 2048, False),
     ("merge32_full_8192", config.merge_config(num_ac=32), 8192, True),
     ("merge32_full_16384", config.merge_config(num_ac=32), 16384, True),
+    # the Merge lookahead forced off / on (DeviceBatch's default: on up to 2048 envs)
+    ("merge32_full_512_nola", config.merge_config(num_ac=32), 512, True, False),
+    ("merge32_full_1024_nola", config.merge_config(num_ac=32), 1024, True, False),
+    ("merge32_full_2048_nola", config.merge_config(num_ac=32), 2048, True, False),
+    ("merge32_full_la", config.merge_config(num_ac=32), 4096, True, True),
 ]:
+    name, cfg, E, cd = spec[:4]
+    la = spec[4] if len(spec) > 4 else None
     if only and name not in only:
         continue
-    res[name] = run(cfg, E, cd)
+    res[name] = run(cfg, E, cd, la=la)
     print(name, f"{res[name]*1e3:.1f} us  (wall/step untimed {WALL[0]*1e3:.1f} us)", flush=True)
 json.dump(res, open(os.environ.get("ABLATE_OUT", "gpurun_out/ablate.json"), "w"), indent=1)
