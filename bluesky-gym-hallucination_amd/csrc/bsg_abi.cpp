@@ -42,6 +42,7 @@ struct bsg_ctx {
   int la_par = 0;
   uint32_t la_gen = 0;
   bool la_dirty = false, memo_dirty = false, la_was_active = false;
+  int no_fastpath = 0;
 };
 
 namespace {
@@ -109,6 +110,7 @@ bsg::KParams make_params(const bsg_ctx* c, int mode) {
   p.la = la_active(c) ? c->la : nullptr;
   p.la_par = c->la_par;
   p.la_gen = c->la_gen;
+  p.no_fastpath = c->no_fastpath;
   return p;
 }
 
@@ -337,6 +339,7 @@ int32_t bsg_create(const bsg_config* cfg, bsg_ctx** out) {
     c->route.rwgs[k] = std::sqrt((an * an + bn * bn) / (ad * ad + bd * bd));
   }
   if (const char* pad = std::getenv("BSG_LDS_PAD_BYTES")) c->lds_pad = (unsigned)std::atoi(pad);
+  if (const char* nf = std::getenv("BSG_NO_FASTPATH")) c->no_fastpath = std::atoi(nf) != 0;
   *out = c;
   return BSG_OK;
 }

@@ -56,6 +56,8 @@ struct KParams {
   int la_par;                // slot the main workgroups read (a step's lookahead writes 1 - la_par)
   uint32_t la_gen;           // generation: tags of other generations are stale
   int la_grid0;              // main workgroups (set by the launcher)
+  int no_fastpath;           // BSG_NO_FASTPATH=1 at bsg_create: the general substep only
+                             // (tests compare the specialised paths against it)
 };
 
 hipError_t launch_step(const KParams& p, hipStream_t stream);

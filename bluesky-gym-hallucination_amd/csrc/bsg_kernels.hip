@@ -1483,6 +1483,89 @@ __device__ __forceinline__ void hdg_spd_action(const KParams& p, AC& s, double a
   s.selspd = speed_new >= 1.0 ? speed_new * KTS : speed_new;
 }
 
+// ---- Vertical / Descent ownship: the substep loop without memo or branch overhead --------
+// Between its altitude commands (selalt 1e6 or 0, vertical_cr_env.py:251-256,
+// descent_env.py:155-160) the ownship climbs or descends on a constant heading: its
+// altitude changes every substep, so every speed-schedule memo of substep() misses and
+// its branches are pure latency (~2,400 of a 4,500-cycle substep, tools/probe).  This is
+// substep<false, true> for exactly that case, each value computed by the same expression
+// in the same order -- speculatively: it checks every condition the specialisation
+// assumes (no LNAV, heading already on its command, CAS speed target, the constant
+// limit atmosphere with the aircraft off its target altitude, not phase GD, every power's
+// argument in its polynomial's range) and reports failure, and the caller then reruns the
+// step through substep() from the saved state (bit-identical either way:
+// tests/test_gpu_fastpath.py).  s.cas and the ownship atmosphere memo (oat) are finished
+// as propagate() does; the lane's speed-schedule memo entries are left invalid.
+__device__ __forceinline__ bool vert_own_fast(AC& s, int S, double dt, Atmos* at_last,
+                                              double* alt_last) {
+  const double allow_h = s.selalt > HMAX ? HMAX : s.selalt;
+  const uint64_t hb = bits(allow_h);
+  const bool khi = hb == bits(HMAX);
+  bool ok = (s.nav & 1) == 0 && (khi || allow_h == 0.0) && fabs(s.selspd) >= 2.0;
+  ok = ok && s.hdg >= 0.0 && s.hdg < 360.0 && fabs(s.ap_trk) < 360.0 &&
+       bits(pymod360_s(s.ap_trk)) == bits(s.hdg);
+  const AtmosK& k = khi ? kAtmosHMAX_K : kAtmosSL_K;
+  const LimK& lk = khi ? kLimHMAX : kLimSL;
+  const double tmmo = MMO * k.snd;
+  // cas2tas_at's altitude-independent part (selspd is the CAS target: constant all step)
+  const double z = 1.0 + divk_nn(RHO0 * s.selspd * s.selspd, 7.0 * P0);
+  const double qdyn = P0 * (poly_3p5(z) - 1.0);
+  ok = ok && in_3p5(z);
+  const double ap_vs = fabs(s.selvs) > 0.1 ? s.selvs : APVSDEF;
+  const double vs_cmd0 = fabs(ap_vs);
+  double shdg, chdg;
+  sincos_t(s.hdg * kD2R, &shdg, &chdg);
+  Atmos at = {0.0, 0.0, 0.0};
+  double h = s.alt;
+  for (int it = 0; it < S; ++it) {
+    h = s.alt;
+    ok = ok && bits(h) != hb && !ground_phase(h);
+    // vatmos (troposphere polynomial)
+    at.T = npmax(288.15 - 0.0065 * h, TSTRAT);
+    const double x = divk_nn(at.T, 288.15);
+    ok = ok && in_trop(x) && npmax(0.0, h - 11000.0) == 0.0;
+    at.rho = 1.225 * poly_trop(x);
+    at.p = at.rho * RGAS * at.T;
+    // ap_tas = vcas2tas(selspd, h)
+    const double y = 1.0 + qdyn / at.p;
+    const double yp = poly_2o7(y);
+    ok = ok && in_2o7(y);
+    const double ap_tas = sqrt(7.0 * at.p / at.rho * (yp - 1.0));
+    // PerfModel.limits at the constant atmosphere (bsg_device.h LimK)
+    double allow_tas = ap_tas < lk.tvmin ? lk.tvmin : ap_tas;
+    allow_tas = ap_tas > lk.tvmax ? lk.tvmax : allow_tas;
+    if (allow_tas > tmmo) allow_tas = tmmo;
+    const double vs_max_with_acc = (1 - s.ax * (1.0 / AXMAX)) * VSMAX;
+    double vs_cmd = (vs_cmd0 > 0 && vs_cmd0 > VSMAX) ? vs_max_with_acc : vs_cmd0;
+    vs_cmd = (vs_cmd0 < 0 && vs_cmd0 < VSMIN) ? VSMIN : vs_cmd;
+    // update_airspeed
+    const double delta_spd = allow_tas - s.tas;
+    const bool need_ax = fabs(delta_spd) > fabs(dt * AXMAX);
+    s.ax = (double)need_ax * sgn(delta_spd) * AXMAX;
+    s.tas = need_ax ? s.tas + s.ax * dt : allow_tas;
+    // (heading on its command: unchanged)  vertical speed
+    const double delta_alt = allow_h - s.alt;
+    const bool swaltsel = fabs(delta_alt) > npmax(10 * FT, fabs(2 * fabs(dt * s.vs)));
+    const double target_vs = (double)swaltsel * sgn(delta_alt) * fabs(vs_cmd);
+    const double delta_vs = target_vs - s.vs;
+    const bool need_az = fabs(delta_vs) > 300 * FPM;
+    const double az = (double)need_az * sgn(delta_vs) * (300 * FPM);
+    s.vs = need_az ? s.vs + az * dt : target_vs;
+    if (!isfinite(s.vs)) s.vs = 0.0;
+    // update_groundspeed + update_pos
+    const double gsnorth = s.tas * chdg;
+    const double gseast = s.tas * shdg;
+    s.alt = swaltsel ? divk(rint((s.alt + s.vs * dt) * 1e6), 1e6) : allow_h;
+    s.lat = s.lat + divk(dt * gsnorth, Rearth) * kR2D;
+    double sinlat, coslat;
+    sincos_t(s.lat * kD2R, &sinlat, &coslat);
+    s.lon = s.lon + divk(dt * gseast / coslat, Rearth) * kR2D;
+  }
+  *at_last = at;
+  *alt_last = h;                    // the altitude `at` belongs to (the last substep's start)
+  return ok && S > 0;
+}
+
 // One RL step of aircraft (e, j) whose state is in s: the ownship's action decode (j == 0),
 // ACTION_FREQUENCY substeps with the cross-step memo, the deferred cas.  StaticObstacle also
 // evaluates its per-substep reward here (sub_reward / sub_done).
@@ -1521,6 +1604,25 @@ __device__ __forceinline__ void propagate(const KParams& p, int e, int j, size_t
     }
   }
   const int S = p.cfg.action_frequency;
+  if constexpr ((KIND == BSG_ENV_VERTICAL_CR || KIND == BSG_ENV_DESCENT) && !WIND) {
+    if (j == 0 && S > 0 && !p.no_fastpath) {
+      const AC saved = s;
+      Atmos at;
+      double alt_last;
+      if (vert_own_fast(s, S, p.cfg.simdt, &at, &alt_last)) {
+        s.cas = tas2cas_at(s.tas, at);     // memo_final_cas: the last substep's atmosphere
+        if (mcache) {
+          if (mc[MC_ALLOW_TAS] == mc[MC_ALLOW_TAS])     // a valid entry: now stale
+            mcache[(size_t)MC_ALLOW_TAS * p.E * N + a] = key_as_double(kNoKey);
+          // the ownship atmosphere memo: vatmos(alt_last), keyed by its altitude
+          double* t = mcache + (size_t)MC_FIELDS * p.E * N + (size_t)e * 4;
+          t[0] = alt_last; t[1] = at.p; t[2] = at.rho; t[3] = at.T;
+        }
+        return;
+      }
+      s = saved;
+    }
+  }
   if (S > 0) {
     Memo m;
     memo_init(m, s);
@@ -1686,8 +1788,15 @@ __device__ __forceinline__ void lookahead_role(const KParams& p) {
 // (small batches only, launch_kind_w) take no aircraft and only share the StateBased CD's
 // pair tests and exact pairs -- a C4 shard of 512-1024 envs leaves most SIMDs idle, and
 // the CD is a serial tail after the substeps of each wave.
+// BSG_WAVES_PER_EU (experiment builds only, tools/ab.sh): cap the registers for that many
+// waves per SIMD (the compiler spills the rest to scratch)
+#if defined(BSG_WAVES_PER_EU)
+#define BSG_WPE __attribute__((amdgpu_waves_per_eu(BSG_WAVES_PER_EU, BSG_WAVES_PER_EU)))
+#else
+#define BSG_WPE
+#endif
 template <int KIND, int GS, bool WIND, int CDW = 1>
-__global__ __launch_bounds__(64 * CDW) void step_kernel(KParams p) {
+__global__ __launch_bounds__(64 * CDW) BSG_WPE void step_kernel(KParams p) {
 #if defined(BSG_STAMPS) && BSG_STAMPS
   BSG_STAMP(0, __builtin_amdgcn_s_memrealtime());
   BSG_STAMP(1, stamp_clock());

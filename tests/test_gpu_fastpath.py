@@ -1,0 +1,71 @@
+"""Specialised substep paths (csrc/bsg_kernels.hip vert_own_fast: the Vertical / Descent
+ownship climbing or descending between its altitude commands) against the general
+substep() they specialise: a batch created with BSG_NO_FASTPATH=1 runs substep() only.
+Every output and every state buffer must be bit-identical step by step, through
+autoresets (both conventions), crashes (alt <= 0), the kept aircraft of Descent and the
+speculation's fallbacks (ground phase near the runway, a target altitude reached)."""
+import os
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+OUTS = ("obs", "reward", "terminated", "truncated", "intr_mask", "conf_mask", "los_mask",
+        "tcpamax", "min_sep", "ep_info", "final_obs")
+
+
+def _batch(cfg, E, general, autoreset, cd):
+    from bluesky_gym import core
+    old = os.environ.get("BSG_NO_FASTPATH")
+    os.environ["BSG_NO_FASTPATH"] = "1" if general else "0"
+    try:
+        return core.DeviceBatch(cfg, E, autoreset=autoreset, compute_cd=cd, seed=21)
+    finally:
+        if old is None:
+            os.environ.pop("BSG_NO_FASTPATH")
+        else:
+            os.environ["BSG_NO_FASTPATH"] = old
+
+
+def _snap(b):
+    d = {k: getattr(b, k).clone() for k in OUTS if getattr(b, k, None) is not None}
+    d.update({"state." + k: v.clone() for k, v in b.state.items()})
+    d.update({"env." + k: v.clone() for k, v in b.envs.items()})
+    return d
+
+
+def _same(x, y, t):
+    for k in x:
+        a, b = x[k], y[k]
+        if a.dtype.is_floating_point:
+            a = a.view(torch.int64 if a.element_size() == 8 else torch.int32)
+            b = b.view(torch.int64 if b.element_size() == 8 else torch.int32)
+        if not torch.equal(a, b):
+            raise AssertionError(f"step {t}: {k} differs at {torch.nonzero(a != b)[:4].tolist()}")
+
+
+@pytest.mark.parametrize("kind,autoreset", [("descent", 1), ("descent", 2), ("vertical", 1),
+                                            ("vertical", 2)])
+def test_vertical_ownship_fastpath_bit_identical(kind, autoreset):
+    from bluesky_gym import config
+    cfg = (config.descent_config(max_episode_steps=60) if kind == "descent"
+           else config.vertical_config(num_intruders=31, max_episode_steps=60))
+    E = 1024 if kind == "descent" else 256
+    cd = kind == "vertical"
+    gen, fast = _batch(cfg, E, True, autoreset, cd), _batch(cfg, E, False, autoreset, cd)
+    g = torch.Generator(device="cuda").manual_seed(4)
+    gen.reset()
+    fast.reset()
+    ends = 0
+    for t in range(150):
+        # mostly dives and climbs at the command limits (the binding vsmax and the ground
+        # phase included), some small commands (|selvs| <= 0.1: the default 1500 fpm)
+        a = torch.rand((E, 1), dtype=torch.float64, device="cuda", generator=g) * 2.4 - 1.2
+        a = a.clamp(-1, 1)
+        a[::7] *= 0.005
+        gen.step(a)
+        fast.step(a)
+        _same(_snap(gen), _snap(fast), t)
+        ends += int((gen.terminated | gen.truncated).sum())
+    assert ends >= E                                     # episodes ended inside the window

@@ -7,7 +7,7 @@ kind, N, E, S, cd, steps = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), int(
 cfg = {"merge": lambda: config.merge_config(num_ac=N, action_frequency=S),
        "vertical": lambda: config.vertical_config(num_intruders=N - 1, action_frequency=S),
        "descent": lambda: config.descent_config(action_frequency=S)}[kind]()
-b = core.DeviceBatch(cfg, E, compute_cd=bool(cd), seed=1)
+b = core.DeviceBatch(cfg, E, compute_cd=bool(cd), seed=1)   # lookahead: DeviceBatch default
 b.reset()
 act = torch.rand((8, E, b.act_dim), dtype=torch.float64, device="cuda") * 2 - 1
 for k in range(steps):

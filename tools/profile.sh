@@ -8,7 +8,7 @@ STEPS=${STEPS:-50}
 OUT=gpurun_out/prof_$TAG
 mkdir -p "$OUT" "profiles/$TAG"
 export TMPDIR=/tmp
-B="python3 bench.py --steps $STEPS --warmup 5 --skip-cpu-baseline"
+B="python3 bench.py --steps $STEPS --warmup 5 --skip-cpu-baseline --no-c5"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- $B > "$OUT/bench_trace.json"
 timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- $B > /dev/null
 timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- $B > /dev/null
