@@ -1483,65 +1483,102 @@ __device__ __forceinline__ void hdg_spd_action(const KParams& p, AC& s, double a
   s.selspd = speed_new >= 1.0 ? speed_new * KTS : speed_new;
 }
 
-// ---- Vertical / Descent ownship: the substep loop without memo or branch overhead --------
+// ---- Descent ownship: the substep loop without memo or branch overhead ------------------
 // Between its altitude commands (selalt 1e6 or 0, vertical_cr_env.py:251-256,
 // descent_env.py:155-160) the ownship climbs or descends on a constant heading: its
 // altitude changes every substep, so every speed-schedule memo of substep() misses and
 // its branches are pure latency (~2,400 of a 4,500-cycle substep, tools/probe).  This is
 // substep<false, true> for exactly that case, each value computed by the same expression
 // in the same order -- speculatively: it checks every condition the specialisation
-// assumes (no LNAV, heading already on its command, CAS speed target, the constant
-// limit atmosphere with the aircraft off its target altitude, not phase GD, every power's
-// argument in its polynomial's range) and reports failure, and the caller then reruns the
+// assumes (no LNAV, heading already on its command, CAS speed target, an altitude
+// command (constant limit atmosphere), the CAS/TAS powers' arguments in their polynomials'
+// ranges) and reports failure, and the caller then reruns the
 // step through substep() from the saved state (bit-identical either way:
 // tests/test_gpu_fastpath.py).  s.cas and the ownship atmosphere memo (oat) are finished
 // as propagate() does; the lane's speed-schedule memo entries are left invalid.
+#ifndef BSG_FAST_DEBUG
+#define BSG_FAST_DEBUG 0
+#endif
 __device__ __forceinline__ bool vert_own_fast(AC& s, int S, double dt, Atmos* at_last,
-                                              double* alt_last) {
+                                              double* alt_last, int* why = nullptr) {
   const double allow_h = s.selalt > HMAX ? HMAX : s.selalt;
   const uint64_t hb = bits(allow_h);
   const bool khi = hb == bits(HMAX);
-  bool ok = (s.nav & 1) == 0 && (khi || allow_h == 0.0) && fabs(s.selspd) >= 2.0;
-  ok = ok && s.hdg >= 0.0 && s.hdg < 360.0 && fabs(s.ap_trk) < 360.0 &&
-       bits(pymod360_s(s.ap_trk)) == bits(s.hdg);
+  // (bitwise & on the conditions: short-circuit && would compile to branches)
+  bool ok = ((s.nav & 1) == 0) & (khi | (allow_h == 0.0)) & (fabs(s.selspd) >= 2.0);
+  if (BSG_FAST_DEBUG && why && !ok) *why |= 1;
+  ok = ok & (s.hdg >= 0.0) & (s.hdg < 360.0) & (fabs(s.ap_trk) < 360.0) &
+       (bits(pymod360_s(s.ap_trk)) == bits(s.hdg));
+  if (BSG_FAST_DEBUG && why && !ok) *why |= 2;
   const AtmosK& k = khi ? kAtmosHMAX_K : kAtmosSL_K;
   const LimK& lk = khi ? kLimHMAX : kLimSL;
   const double tmmo = MMO * k.snd;
   // cas2tas_at's altitude-independent part (selspd is the CAS target: constant all step)
   const double z = 1.0 + divk_nn(RHO0 * s.selspd * s.selspd, 7.0 * P0);
   const double qdyn = P0 * (poly_3p5(z) - 1.0);
-  ok = ok && in_3p5(z);
+  if (BSG_FAST_DEBUG && why && !in_3p5(z)) *why |= 16;
+  ok = ok & in_3p5(z);
   const double ap_vs = fabs(s.selvs) > 0.1 ? s.selvs : APVSDEF;
   const double vs_cmd0 = fabs(ap_vs);
   double shdg, chdg;
   sincos_t(s.hdg * kD2R, &shdg, &chdg);
   Atmos at = {0.0, 0.0, 0.0};
   double h = s.alt;
+  // the on-target limits below are a pure function of (ap_tas, gd) there: kept while equal
+  // (an aircraft that reached the ground stays there with the same ap_tas)
+  uint64_t ot_key = kNoKey;
+  bool ot_gd = false;
+  double ot_tas = 0.0;
   for (int it = 0; it < S; ++it) {
     h = s.alt;
-    ok = ok && bits(h) != hb && !ground_phase(h);
-    // vatmos (troposphere polynomial)
+    const bool gd = ground_phase(h);
+    const double axmax = gd ? AXMAX_GD : AXMAX;
+    // vatmos: the density-ratio polynomial (x stays in its range up to HMAX), times the
+    // stratosphere factor above 11 km (exactly vatmos' (1.225 * pow) * exp; * 1.0 below)
     at.T = npmax(288.15 - 0.0065 * h, TSTRAT);
     const double x = divk_nn(at.T, 288.15);
-    ok = ok && in_trop(x) && npmax(0.0, h - 11000.0) == 0.0;
-    at.rho = 1.225 * poly_trop(x);
+    const double dhstrat = npmax(0.0, h - 11000.0);
+    // (x > 1: an aircraft a little below the ground within a step, the libm pow as vatmos)
+    double pt = poly_trop(x);
+    if (!in_trop(x)) pt = pow(x, 4.256848030018761);
+    double strat = 1.0;
+    if (dhstrat > 0.0) strat = exp(divk(-dhstrat, 6341.552161));
+    at.rho = 1.225 * pt * strat;
     at.p = at.rho * RGAS * at.T;
     // ap_tas = vcas2tas(selspd, h)
     const double y = 1.0 + qdyn / at.p;
     const double yp = poly_2o7(y);
-    ok = ok && in_2o7(y);
+    if (BSG_FAST_DEBUG && why && !in_2o7(y)) *why |= 8;
+    ok = ok & in_2o7(y);
     const double ap_tas = sqrt(7.0 * at.p / at.rho * (yp - 1.0));
     // PerfModel.limits at the constant atmosphere (bsg_device.h LimK)
-    double allow_tas = ap_tas < lk.tvmin ? lk.tvmin : ap_tas;
-    allow_tas = ap_tas > lk.tvmax ? lk.tvmax : allow_tas;
+    const double tvmin = gd ? 0.0 : lk.tvmin, tvmax = gd ? lk.tvmax_gd : lk.tvmax;
+    double allow_tas = ap_tas < tvmin ? tvmin : ap_tas;
+    allow_tas = ap_tas > tvmax ? tvmax : allow_tas;
     if (allow_tas > tmmo) allow_tas = tmmo;
-    const double vs_max_with_acc = (1 - s.ax * (1.0 / AXMAX)) * VSMAX;
+    if (bits(h) == hb) {
+      // on its target altitude (a descent that reached the ground): substep()'s limits at
+      // the aircraft's own atmosphere, the CAS/TAS round trip
+      if (bits(ap_tas) != ot_key || gd != ot_gd) {
+        const double vmin = gd ? 0.0 : VMIN_CAS, vmax = gd ? VMAX_GD : VMAX_CAS;
+        const double intent_cas = tas2cas_at(ap_tas, at);
+        double allow_cas = intent_cas < vmin ? vmin : intent_cas;
+        allow_cas = intent_cas > vmax ? vmax : allow_cas;
+        ot_tas = cas2tas_at(allow_cas, at);
+        const double snd_h = sound_at(at);
+        if (ot_tas / snd_h > MMO) ot_tas = MMO * snd_h;
+        ot_key = bits(ap_tas);
+        ot_gd = gd;
+      }
+      allow_tas = ot_tas;
+    }
+    const double vs_max_with_acc = (1 - s.ax * (gd ? 1.0 / AXMAX_GD : 1.0 / AXMAX)) * VSMAX;
     double vs_cmd = (vs_cmd0 > 0 && vs_cmd0 > VSMAX) ? vs_max_with_acc : vs_cmd0;
     vs_cmd = (vs_cmd0 < 0 && vs_cmd0 < VSMIN) ? VSMIN : vs_cmd;
     // update_airspeed
     const double delta_spd = allow_tas - s.tas;
-    const bool need_ax = fabs(delta_spd) > fabs(dt * AXMAX);
-    s.ax = (double)need_ax * sgn(delta_spd) * AXMAX;
+    const bool need_ax = fabs(delta_spd) > fabs(dt * axmax);
+    s.ax = (double)need_ax * sgn(delta_spd) * axmax;
     s.tas = need_ax ? s.tas + s.ax * dt : allow_tas;
     // (heading on its command: unchanged)  vertical speed
     const double delta_alt = allow_h - s.alt;
@@ -1563,7 +1600,7 @@ __device__ __forceinline__ bool vert_own_fast(AC& s, int S, double dt, Atmos* at
   }
   *at_last = at;
   *alt_last = h;                    // the altitude `at` belongs to (the last substep's start)
-  return ok && S > 0;
+  return ok & (S > 0);
 }
 
 // One RL step of aircraft (e, j) whose state is in s: the ownship's action decode (j == 0),
@@ -1604,12 +1641,21 @@ __device__ __forceinline__ void propagate(const KParams& p, int e, int j, size_t
     }
   }
   const int S = p.cfg.action_frequency;
-  if constexpr ((KIND == BSG_ENV_VERTICAL_CR || KIND == BSG_ENV_DESCENT) && !WIND) {
+  // (Vertical's intruders would run substep() after the ownship's loop in the same wave:
+  // the union measured slower than substep() alone, 121.7 against 90.6 us at 2,048 envs)
+  if constexpr (KIND == BSG_ENV_DESCENT && !WIND) {
+    bool fast_ok = false;
     if (j == 0 && S > 0 && !p.no_fastpath) {
       const AC saved = s;
       Atmos at;
       double alt_last;
-      if (vert_own_fast(s, S, p.cfg.simdt, &at, &alt_last)) {
+#ifndef BSG_FAST_ALWAYS
+#define BSG_FAST_ALWAYS 0                 // experiment builds: take the fast loop's result even
+#endif                                    // where its speculation failed (timing only)
+      int why = 0;
+      fast_ok = vert_own_fast(s, S, p.cfg.simdt, &at, &alt_last, &why) || BSG_FAST_ALWAYS;
+      if (BSG_FAST_DEBUG && p.b.ep_info) p.b.ep_info[(size_t)e * 4 + 3] = (double)why;
+      if (fast_ok) {
         s.cas = tas2cas_at(s.tas, at);     // memo_final_cas: the last substep's atmosphere
         if (mcache) {
           if (mc[MC_ALLOW_TAS] == mc[MC_ALLOW_TAS])     // a valid entry: now stale
@@ -1618,10 +1664,14 @@ __device__ __forceinline__ void propagate(const KParams& p, int e, int j, size_t
           double* t = mcache + (size_t)MC_FIELDS * p.E * N + (size_t)e * 4;
           t[0] = alt_last; t[1] = at.p; t[2] = at.rho; t[3] = at.T;
         }
-        return;
+      } else {
+        s = saved;
       }
-      s = saved;
     }
+    // leave on a wave-uniform condition: a uniform loop below would otherwise still issue
+    // every straight-line instruction of its 30 substeps with an empty exec mask
+    if (__ballot(!fast_ok) == 0) return;
+    if (fast_ok) return;
   }
   if (S > 0) {
     Memo m;

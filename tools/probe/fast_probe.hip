@@ -1,0 +1,101 @@
+// Probe on gfx950: the Vertical/Descent ownship's specialised substep loop (vert_own_fast,
+// bsg_kernels.hip) against substep() on one wave of real Descent aircraft -- cycles of
+// each, how many lanes' speculation held, and whether the states agree bit for bit.
+// State from tools/probe/substep_probe.py --descent (64 lanes).
+//   hipcc -O3 -std=c++17 --offload-arch=gfx950 -ffp-contract=off -fno-fast-math \
+//         -mllvm -disable-machine-licm tools/probe/fast_probe.hip -o tools/probe/fast_probe
+#include "../../bluesky-gym-hallucination_amd/csrc/bsg_kernels.hip"
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+constexpr int NF = 12;
+
+__global__ void probe(bsg::Route route, const double* st, int S, double dt, long long* cyc,
+                      int* okc, double* out_fast, double* out_gen) {
+  using namespace bsg;
+  const int l = threadIdx.x;
+  AC s{};
+  double* f[NF] = {&s.lat, &s.lon, &s.alt, &s.hdg, &s.tas, &s.cas, &s.vs, &s.ax, &s.ap_trk,
+                   &s.selspd, &s.selalt, &s.selvs};
+  for (int k = 0; k < NF; ++k) *f[k] = st[k * 64 + l];
+  s.nav = (int)st[NF * 64 + l];
+  s.gs = s.tas; s.trk = s.hdg;
+  // the Descent action decode of a dive (selalt 0, selvs -12.5 * 0.8)
+  s.selalt = 0.0; s.selvs = -10.0;
+  const AC s0 = s;
+  AC a = s0;
+  Atmos at;
+  double alt_last;
+  long long t0 = __builtin_amdgcn_s_memtime();
+  const bool ok = vert_own_fast(a, S, dt, &at, &alt_last);
+  a.cas = tas2cas_at(a.tas, at);
+  long long t1 = __builtin_amdgcn_s_memtime();
+  AC b = s0;
+  Memo m;
+  memo_init(m, b);
+  RouteRegs rt;
+  rt.load(route);
+  memo_lnav(m, b, rt);
+  WindDev w{};
+  long long t2 = __builtin_amdgcn_s_memtime();
+  for (int it = 0; it < S; ++it) substep<false, true>(b, m, dt, rt, w, true);
+  memo_final_cas(m, b);
+  long long t3 = __builtin_amdgcn_s_memtime();
+  if (l == 0) { cyc[0] = t1 - t0; cyc[1] = t3 - t2; }
+  okc[l] = ok;
+  double* fa[NF] = {&a.lat, &a.lon, &a.alt, &a.hdg, &a.tas, &a.cas, &a.vs, &a.ax, &a.ap_trk,
+                    &a.selspd, &a.selalt, &a.selvs};
+  double* fb[NF] = {&b.lat, &b.lon, &b.alt, &b.hdg, &b.tas, &b.cas, &b.vs, &b.ax, &b.ap_trk,
+                    &b.selspd, &b.selalt, &b.selvs};
+  for (int k = 0; k < NF; ++k) { out_fast[k * 64 + l] = *fa[k]; out_gen[k * 64 + l] = *fb[k]; }
+}
+
+int main(int argc, char** argv) {
+  if (argc < 2) { std::printf("usage: fast_probe state.bin\n"); return 2; }
+  FILE* fp = std::fopen(argv[1], "rb");
+  if (!fp) return 2;
+  std::vector<double> hdr(1 + 3 * BSG_MAX_ROUTE), st((NF + 1) * 64);
+  if (std::fread(hdr.data(), 8, hdr.size(), fp) != hdr.size() ||
+      std::fread(st.data(), 8, st.size(), fp) != st.size()) return 2;
+  std::fclose(fp);
+  bsg::Route route{};
+  route.len = (int)hdr[0];
+  double *dst, *dfa, *dgb;
+  long long* dcyc;
+  int* dok;
+  if (hipMalloc(&dst, st.size() * 8) != hipSuccess || hipMalloc(&dfa, NF * 64 * 8) != hipSuccess ||
+      hipMalloc(&dgb, NF * 64 * 8) != hipSuccess || hipMalloc(&dcyc, 16) != hipSuccess ||
+      hipMalloc(&dok, 64 * 4) != hipSuccess) return 1;
+  (void)hipMemcpy(dst, st.data(), st.size() * 8, hipMemcpyHostToDevice);
+  long long best[2] = {1LL << 62, 1LL << 62};
+  for (int rep = 0; rep < 5; ++rep) {
+    hipLaunchKernelGGL(probe, dim3(1), dim3(64), 0, 0, route, dst, 30, 1.0, dcyc, dok, dfa, dgb);
+    long long c[2];
+    (void)hipMemcpy(c, dcyc, 16, hipMemcpyDeviceToHost);
+    for (int i = 0; i < 2; ++i) best[i] = c[i] < best[i] ? c[i] : best[i];
+  }
+  std::vector<int> ok(64);
+  std::vector<double> fa(NF * 64), gb(NF * 64);
+  (void)hipMemcpy(ok.data(), dok, 64 * 4, hipMemcpyDeviceToHost);
+  (void)hipMemcpy(fa.data(), dfa, NF * 64 * 8, hipMemcpyDeviceToHost);
+  (void)hipMemcpy(gb.data(), dgb, NF * 64 * 8, hipMemcpyDeviceToHost);
+  int nok = 0, diff = 0;
+  for (int l = 0; l < 64; ++l) {
+    nok += ok[l];
+    if (!ok[l]) continue;
+    for (int k = 0; k < NF; ++k)
+      if (fa[k * 64 + l] != gb[k * 64 + l]) {
+        if (diff < 8) std::printf("lane %d field %d fast %.17g gen %.17g\n", l, k, fa[k * 64 + l], gb[k * 64 + l]);
+        ++diff;
+      }
+  }
+  std::printf("30 substeps: fast loop %lld cycles, substep() %lld cycles; speculation held on %d/64 "
+              "lanes; %d field mismatches on those\n", best[0], best[1], nok, diff);
+  for (int l = 0; l < 64 && nok < 64; ++l)
+    if (!ok[l]) std::printf("  lane %d failed: alt %.6f hdg %.17g ap_trk %.17g selspd %g nav %d\n", l,
+                            st[2 * 64 + l], st[3 * 64 + l], st[8 * 64 + l], st[9 * 64 + l],
+                            (int)st[NF * 64 + l]);
+  return 0;
+}

@@ -7,3 +7,4 @@ timeout -k 10 300 python bench.py > gpurun_out/r03/bench.log 2>&1 || { echo BENC
 grep "^{" gpurun_out/r03/bench.log > gpurun_out/r03/bench.json
 timeout -k 10 900 bash tools/profile.sh r03 > gpurun_out/r03/profile.log 2>&1 || { echo PROF_FAILED; tail -20 gpurun_out/r03/profile.log; exit 1; }
 tail -3 gpurun_out/r03/profile.log
+timeout -k 10 600 bash tools/ab.sh gpurun_out/r03/ab_w4 merge32_full merge32_full_la merge32_full_512 -- bluesky-gym-hallucination_amd/bluesky_gym/_lib/libbsg.so bluesky-gym-hallucination_amd/bluesky_gym/_lib/libbsg_w4.so > gpurun_out/r03/ab_w4.txt 2>&1; cat gpurun_out/r03/ab_w4.txt
