@@ -13,6 +13,24 @@ import shutil
 import sys
 
 out, tag = sys.argv[1], sys.argv[2]
+
+
+def _compiler_vgprs(kernel):
+    """VGPRs of `kernel` from the committed resource-usage remarks, or None."""
+    try:
+        lines = open(f"profiles/{tag}/resource_usage.txt").read().splitlines()
+    except OSError:
+        return None
+    # "void bsg::step_kernel<0, 32, false, 1>(bsg::KParams)" -> "step_kernelILi0ELi32ELb0ELi1E"
+    args = [a.strip() for a in kernel.split("<", 1)[1].split(">", 1)[0].split(",")]
+    mangled = "step_kernelI" + "".join(
+        ("Lb1E" if a == "true" else "Lb0E") if a in ("true", "false") else f"Li{a}E" for a in args)
+    for i, ln in enumerate(lines):
+        if ln.startswith("Function Name:") and mangled in ln:
+            return int(lines[i + 1].split(":")[1])
+    return None
+
+
 os.makedirs(f"profiles/{tag}", exist_ok=True)
 agg = {}
 meta = None
@@ -28,7 +46,10 @@ avg_ns = float(stats[k]["AverageNs"])
 f64 = (m["SQ_INSTS_VALU_FMA_F64"] + m["SQ_INSTS_VALU_MUL_F64"] + m["SQ_INSTS_VALU_ADD_F64"]
        + m["SQ_INSTS_VALU_TRANS_F64"])
 res = {
-    "tag": tag, "kernel": k, "envs": 4096, "num_ac": 32, "grid": meta[0], "vgpr": meta[1],
+    "tag": tag, "kernel": k, "envs": 4096, "num_ac": 32, "grid": meta[0],
+    # rocprofv3's VGPR_Count reads half the granulated allocation (208 -> 104); the compiler's
+    # own count comes from -Rpass-analysis=kernel-resource-usage (profiles/<tag>/resource_usage.txt)
+    "vgpr": _compiler_vgprs(k), "vgpr_rocprof_field": meta[1],
     "sgpr": meta[2], "lds_bytes": meta[3], "kernel_avg_ns_rocprof": avg_ns,
     "kernel_calls_rocprof": int(stats[k]["Calls"]),
     "fetch_size_kb": m["FETCH_SIZE"], "write_size_kb": m["WRITE_SIZE"],
