@@ -327,14 +327,11 @@ __device__ __forceinline__ bool b_times_dphi_far(double latd1, double latd2, dou
   return bmin * (fabs(latd2 - latd1) * kD2R) * 0.999999 > far_m;
 }
 
-// First half of geo.qdrdist for the LNAV loop: the bearing (exact, as qdrdist) and the
-// acos argument x of its distance (bit-identical to the argument the full path passes to
-// acos).
-__device__ __forceinline__ void qdr_x(double latd1, double lond1, double coslat1, double sinlat1,
-                                      double latd2, double lond2, double coslat2, double sinlat2,
-                                      double* qdr, double* x) {
-  double sdl, cdl;
-  sincos_t(lond2 * kD2R - lond1 * kD2R, &sdl, &cdl);
+// First half of geo.qdrdist for the LNAV loop: the bearing (as qdrdist) and the acos
+// argument x of its distance (the argument the full path passes to acos), given the
+// longitude gap's sin/cos (sdl, cdl of lond2 * D2R - lond1 * D2R).
+__device__ __forceinline__ void qdr_x_t(double coslat1, double sinlat1, double coslat2, double sinlat2,
+                                        double sdl, double cdl, double* qdr, double* x) {
   *qdr = atan2(sdl * coslat2, coslat1 * sinlat2 - sinlat1 * coslat2 * cdl) * kR2D;
   *x = coslat1 * coslat2 * cdl + sinlat1 * sinlat2;
 }

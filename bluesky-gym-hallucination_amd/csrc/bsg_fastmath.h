@@ -104,6 +104,14 @@ __host__ __device__ __forceinline__ double div_r(double x, double y, double ry) 
 // divisor known at compile time: 1.0 / y folds to RN(1/y)
 __host__ __device__ __forceinline__ double divk(double x, double y) { return div_r(x, y, 1.0 / y); }
 
+// divk for a finite numerator and y > 0: the zero quotient's sign by copysign (one bit
+// operation) instead of divk's compare/select guard
+__host__ __device__ __forceinline__ double divk_f(double x, double y) {
+  const double ry = 1.0 / y;
+  const double q = x * ry;
+  return copysign(fma(fma(-q, y, x), ry, q), x);
+}
+
 // the same for a finite numerator whose zero, if any, is +0 (every physically non-negative
 // quantity: temperatures, squared speeds, dynamic pressures, distances): the guard's
 // compare/select pair is half the latency of the division itself
@@ -192,6 +200,93 @@ __host__ __device__ __forceinline__ double cos_t(double x) {
   const double z = t.r * t.r;
   const double v = (t.q & 1) ? ksin(t.r, t.rr, z) : kcos(t.r, t.rr, z);
   return ((t.q + 1) & 2) ? -v : v;
+}
+
+// ---- sin / cos carried along a trajectory --------------------------------------------
+// The latitude and the LNAV longitude gap of an aircraft move by < 2e-3 rad per substep
+// (300 m/s, 5 s, below 80 deg).  Their sin/cos are carried from substep to substep by the
+// angle-addition formulas instead of being evaluated afresh -- ~50 cycles of dependent
+// latency instead of sincos_t's ~330, twice per substep on the LNAV chain.
+// The pair is carried in double-double: (s + sl, c + cl), seeded by sincos_dd (sincos_t's
+// kernels with their tails kept, ~0.1 ulp) at every launch, advanced by
+//   sin(x + d) = s + (s (cos d - 1) + c sin d),  cos(x + d) = c + (c (cos d - 1) - s sin d)
+// whose corrections are ~|d| times the values (their roundings ~|d| ulp), summed with the
+// low parts by TwoSum.  s and c (the rounded values) are what the substep uses: within
+// ~0.6 ulp of the exact sin/cos of the carried angle, which stays the angle NumPy
+// evaluates (the increments are exact differences of the rounded radian values).
+// tools/fastmath/angle_add_check.cpp measures it against glibc over 30-step trajectories.
+struct SinCos { double s, sl, c, cl; };
+
+__host__ __device__ __forceinline__ void ksin_dd(double r, double rr, double z, double* hi, double* lo) {
+  const double v = z * r;
+  double p = kSinC[6];
+#pragma unroll
+  for (int k = 5; k >= 1; --k) p = fma(p, z, kSinC[k]);
+  const double e = (z * (0.5 * rr - v * p) - rr) - fma(v, kSinC0Lo, v * kSinC[0]);
+  *hi = r - e;                                       // ksin's value
+  *lo = (r - *hi) - e;                               // Fast2Sum: |r| >= |e|
+}
+
+__host__ __device__ __forceinline__ void kcos_dd(double r, double rr, double z, double* hi, double* lo) {
+  double p = kCosC[5];
+#pragma unroll
+  for (int k = 4; k >= 0; --k) p = fma(p, z, kCosC[k]);
+  const double zl = fma(r, r, -z);
+  const double hz = 0.5 * z;
+  const double w = 1.0 - hz;
+  const double t = (((1.0 - w) - hz) - 0.5 * zl) + (z * (z * p) - r * rr);
+  *hi = w + t;                                       // kcos's value
+  *lo = (w - *hi) + t;                               // Fast2Sum: w >= 1/2 > |t|
+}
+
+// sincos_t with the kernels' tails: (s, c) are sincos_t's values bit for bit
+__host__ __device__ __forceinline__ SinCos sincos_dd(double x) {
+  const TrigRed t = trig_reduce(x);
+  const double z = t.r * t.r;
+  double sh, sl, ch, cl;
+  ksin_dd(t.r, t.rr, z, &sh, &sl);
+  kcos_dd(t.r, t.rr, z, &ch, &cl);
+  const bool sw = t.q & 1, ns = t.q & 2, nc = (t.q + 1) & 2;
+  SinCos o;
+  o.s = sw ? ch : sh; o.sl = sw ? cl : sl;
+  o.c = sw ? sh : ch; o.cl = sw ? sl : cl;
+  if (ns) { o.s = -o.s; o.sl = -o.sl; }
+  if (nc) { o.c = -o.c; o.cl = -o.cl; }
+  if (x == 0.0) { o.s = x; o.sl = 0.0; }              // sin(-0) = -0
+  return o;
+}
+
+// advance by d (|d| <= 0.2): sin d to d^11, cos d - 1 to d^12 (truncation < 2^-70 |d|) --
+// a heading that turns at the standard rate moves up to ~0.18 rad in a 5 s substep
+__host__ __device__ __forceinline__ void sincos_add_w(SinCos& a, double d) {
+  const double z = d * d;
+  const double sd = fma(d * z, fma(z, fma(z, fma(z, fma(z, -1.0 / 39916800.0, 1.0 / 362880.0),
+                                                  -1.0 / 5040.0), 1.0 / 120.0), -1.0 / 6.0), d);
+  const double cm1 = z * fma(z, fma(z, fma(z, fma(z, fma(z, 1.0 / 479001600.0, -1.0 / 3628800.0),
+                                                  1.0 / 40320.0), -1.0 / 720.0), 1.0 / 24.0), -0.5);
+  const double ts = fma(a.s, cm1, a.c * sd) + a.sl;
+  const double tc = fma(a.c, cm1, -(a.s * sd)) + a.cl;
+  const double hs = a.s + ts, hc = a.c + tc;
+  const double bs = hs - a.s, bc = hc - a.c;
+  a.sl = (a.s - (hs - bs)) + (ts - bs);
+  a.cl = (a.c - (hc - bc)) + (tc - bc);
+  a.s = hs;
+  a.c = hc;
+}
+
+// advance by d (|d| <= 0.05): sin d to d^7, cos d - 1 to d^8 (truncation < 2^-70 |d|)
+__host__ __device__ __forceinline__ void sincos_add(SinCos& a, double d) {
+  const double z = d * d;
+  const double sd = fma(d * z, fma(z, fma(z, -1.0 / 5040.0, 1.0 / 120.0), -1.0 / 6.0), d);
+  const double cm1 = z * fma(z, fma(z, fma(z, 1.0 / 40320.0, -1.0 / 720.0), 1.0 / 24.0), -0.5);
+  const double ts = fma(a.s, cm1, a.c * sd) + a.sl;
+  const double tc = fma(a.c, cm1, -(a.s * sd)) + a.cl;
+  const double hs = a.s + ts, hc = a.c + tc;
+  const double bs = hs - a.s, bc = hc - a.c;         // TwoSum remainders
+  a.sl = (a.s - (hs - bs)) + (ts - bs);
+  a.cl = (a.c - (hc - bc)) + (tc - bc);
+  a.s = hs;
+  a.c = hc;
 }
 
 }  // namespace bsg

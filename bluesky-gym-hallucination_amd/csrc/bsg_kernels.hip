@@ -201,6 +201,9 @@ struct RouteRegs {
   }
 };
 
+#ifndef BSG_X_HDG
+#define BSG_X_HDG 0
+#endif
 struct Memo {
   uint64_t alt_bits;               // key of at = vatmos(alt)
   Atmos at;
@@ -211,10 +214,16 @@ struct Memo {
   double allow_tas;
   int wp_k;                        // cached waypoint (coords, next-leg bearing, trig)
   double wp_lat, wp_lon, wp_nq, wp_cos, wp_sin, wp_rw, wp_pnq;   // wp_pnq = pymod360(wp_nq)
-  double coslat, sinlat;           // cos/sin(lat * D2R) of the current latitude
+  double latr;                     // lat * D2R and its sin/cos (carried through the
+  SinCos lat_sc;                   //   substeps by sincos_add, bsg_fastmath.h)
+  double wp_lonr;                  // wp_lon * D2R
+  double dlr;                      // LNAV longitude gap wp_lonr - lon * D2R and its sin/cos
+  SinCos dl_sc;
   double phdg;                     // pymod360(hdg), for LNAV's waypoint-behind test
   uint64_t hdg_bits;               // key of (shdg, chdg) = sincos(hdg * D2R)
   double shdg, chdg;
+  double hdgr;                     // hdg * D2R and its sin/cos carried (!HMEMO kinds)
+  SinCos hdg_sc;
   double turnrad;                  // LNAV turn radius tas^2/(g0*tan(bank)) of the current tas
   double last_alt;                 // altitude at the start of the latest substep
   uint64_t cas_tas_bits, cas_alt_bits;  // key of the stored cas = vtas2cas(tas, alt)
@@ -253,11 +262,15 @@ __device__ __forceinline__ void memo_init(Memo& m, const AC& s) {
   m.wp_k = -1; m.wp_lat = 0; m.wp_lon = 0; m.wp_nq = 0; m.wp_cos = 0; m.wp_sin = 0; m.wp_rw = 0;
   m.wp_pnq = 0;
   m.hdg_bits = kNoKey; m.shdg = 0; m.chdg = 0;
+  m.hdgr = s.hdg * kD2R;
+  m.hdg_sc = BSG_X_HDG ? sincos_dd(m.hdgr) : SinCos{0.0, 0.0, 1.0, 0.0};
   m.phdg = pymod360(s.hdg);
   m.turnrad = 0;
   m.last_alt = s.alt;
   m.cas_tas_bits = kNoKey; m.cas_alt_bits = kNoKey;
-  sincos_t(s.lat * kD2R, &m.sinlat, &m.coslat);
+  m.latr = s.lat * kD2R;
+  m.lat_sc = sincos_dd(m.latr);
+  m.wp_lonr = 0; m.dlr = 0; m.dl_sc = SinCos{0.0, 0.0, 1.0, 0.0};
 }
 
 // issued at kernel entry together with the state loads (one memory round trip)
@@ -331,12 +344,19 @@ __device__ __forceinline__ void memo_wp(Memo& m, const RouteRegs& rt, int k) {
   rt.get(k, &m.wp_lat, &m.wp_lon, &m.wp_nq, &m.wp_rw);
   m.wp_pnq = pymod360(m.wp_nq);
   sincos_t(m.wp_lat * kD2R, &m.wp_sin, &m.wp_cos);
+  m.wp_lonr = m.wp_lon * kD2R;
+}
+
+// the LNAV longitude gap's trig evaluated in full (launch start, a new active waypoint)
+__device__ __forceinline__ void memo_dl(Memo& m, const AC& s) {
+  m.dlr = m.wp_lonr - s.lon * kD2R;
+  m.dl_sc = sincos_dd(m.dlr);
 }
 
 // the LNAV terms at the start of a launch: the active waypoint's (LNAV lanes) and the turn
 // radius of the loaded tas
 __device__ __forceinline__ void memo_lnav(Memo& m, const AC& s, const RouteRegs& rt) {
-  if (s.nav & 1) memo_wp(m, rt, (s.nav >> 8) & 0xff);
+  if (s.nav & 1) { memo_wp(m, rt, (s.nav >> 8) & 0xff); memo_dl(m, s); }
   m.turnrad = turnrad_of(s.tas);
 }
 
@@ -367,7 +387,12 @@ __device__ __forceinline__ void substep(AC& s, Memo& m, double dt, const RouteRe
     // branch here (~85 cycles per substep even when never taken).
     const double turnrad = m.turnrad;
     double qdr, x;
-    qdr_x(s.lat, s.lon, m.coslat, m.sinlat, m.wp_lat, m.wp_lon, m.wp_cos, m.wp_sin, &qdr, &x);
+    // geo.qdrdist's sin/cos of the longitude gap, carried from the previous substep's
+    // (the gap moves by the aircraft's own longitude step, |d| < 2e-3 rad)
+    const double dlr = m.wp_lonr - s.lon * kD2R;
+    sincos_add(m.dl_sc, dlr - m.dlr);
+    m.dlr = dlr;
+    qdr_x_t(m.lat_sc.c, m.lat_sc.s, m.wp_cos, m.wp_sin, m.dl_sc.s, m.dl_sc.c, &qdr, &x);
     BSG_SUBSTEP_MARK(5);
     // pymod360 of the bearing (atan2 * R2D: one select) and of the leg's next bearing
     // (memo_wp); half = 0.5 |degto180(.)| of their difference (two selects)
@@ -448,8 +473,9 @@ __device__ __forceinline__ void substep(AC& s, Memo& m, double dt, const RouteRe
           ++k;
           s.nav = (k << 8) | 1;
           memo_wp(m, rt, k);
-          qdr_x(s.lat, s.lon, m.coslat, m.sinlat, m.wp_lat, m.wp_lon, m.wp_cos, m.wp_sin,
-                &qdr, &x);                 // only the bearing to the new waypoint is used
+          memo_dl(m, s);
+          qdr_x_t(m.lat_sc.c, m.lat_sc.s, m.wp_cos, m.wp_sin, m.dl_sc.s, m.dl_sc.c, &qdr,
+                  &x);                     // only the bearing to the new waypoint is used
         }
       }
     }
@@ -569,6 +595,14 @@ __device__ __forceinline__ void substep(AC& s, Memo& m, double dt, const RouteRe
       sincos_t(s.hdg * kD2R, &m.shdg, &m.chdg);
       m.hdg_bits = bits(s.hdg);
     }
+  } else if (BSG_X_HDG) {
+    const double hr = s.hdg * kD2R;
+    const double d = hr - m.hdgr;
+    if (fabs(d) <= 0.2) sincos_add_w(m.hdg_sc, d);
+    else m.hdg_sc = sincos_dd(hr);
+    m.hdgr = hr;
+    m.shdg = m.hdg_sc.s;
+    m.chdg = m.hdg_sc.c;
   } else {
     // LNAV lanes re-aim at the waypoint's bearing every substep, so some lane of a wave
     // always misses the memo: its branch would only add latency
@@ -592,9 +626,13 @@ __device__ __forceinline__ void substep(AC& s, Memo& m, double dt, const RouteRe
   if (swaltsel) s.alt = divk(rint((s.alt + s.vs * dt) * 1e6), 1e6);   // a branch: level flight
   else s.alt = allow_h;                                            // skips the division
   BSG_SUBSTEP_MARK(4);
-  s.lat = s.lat + divk(dt * gsnorth, Rearth) * kR2D;
-  sincos_t(s.lat * kD2R, &m.sinlat, &m.coslat);
-  s.lon = s.lon + divk(dt * gseast / m.coslat, Rearth) * kR2D;
+  // (divk_f: the numerators are finite -- tas is clamped by the envelope, |cos| <= 1)
+  s.lat = s.lat + divk_f(dt * gsnorth, Rearth) * kR2D;
+  const double latr = s.lat * kD2R;          // |latr - m.latr| < 3e-4 rad: angle addition
+  sincos_add(m.lat_sc, latr - m.latr);
+  m.latr = latr;
+  const double ge = dt * gseast / m.lat_sc.c;
+  s.lon = s.lon + divk_f(ge, Rearth) * kR2D;
 }
 
 // ---- LDS staging (one wave per block; GS lanes per env) -------------------------------
@@ -1522,6 +1560,9 @@ __device__ __forceinline__ bool vert_own_fast(AC& s, int S, double dt, Atmos* at
   const double vs_cmd0 = fabs(ap_vs);
   double shdg, chdg;
   sincos_t(s.hdg * kD2R, &shdg, &chdg);
+  // the latitude's trig carried as substep() carries it (memo_init's seed, sincos_add)
+  double latr = s.lat * kD2R;
+  SinCos lsc = sincos_dd(latr);
   Atmos at = {0.0, 0.0, 0.0};
   double h = s.alt;
   // the on-target limits below are a pure function of (ap_tas, gd) there: kept while equal
@@ -1593,10 +1634,11 @@ __device__ __forceinline__ bool vert_own_fast(AC& s, int S, double dt, Atmos* at
     const double gsnorth = s.tas * chdg;
     const double gseast = s.tas * shdg;
     s.alt = swaltsel ? divk(rint((s.alt + s.vs * dt) * 1e6), 1e6) : allow_h;
-    s.lat = s.lat + divk(dt * gsnorth, Rearth) * kR2D;
-    double sinlat, coslat;
-    sincos_t(s.lat * kD2R, &sinlat, &coslat);
-    s.lon = s.lon + divk(dt * gseast / coslat, Rearth) * kR2D;
+    s.lat = s.lat + divk_f(dt * gsnorth, Rearth) * kR2D;
+    const double nlr = s.lat * kD2R;
+    sincos_add(lsc, nlr - latr);
+    latr = nlr;
+    s.lon = s.lon + divk_f(dt * gseast / lsc.c, Rearth) * kR2D;
   }
   *at_last = at;
   *alt_last = h;                    // the altitude `at` belongs to (the last substep's start)
