@@ -135,6 +135,10 @@ def main():
     ap.add_argument("--weak", action="store_true", help="weak scaling: --envs-per-gpu on every GPU")
     ap.add_argument("--envs-per-gpu", type=int, default=4096)
     ap.add_argument("--num-ac", type=int, default=32)
+    ap.add_argument("--steps-per-gather", type=int, default=8,
+                    help="N>1: learner rows all-gathered once per block of this many steps "
+                         "(one RCCL all_gather of [k, E, obs+3] fp32; the last partial block is "
+                         "flushed inside the timed region); 1 = one all_gather per step")
     ap.add_argument("--no-cd", action="store_true")
     ap.add_argument("--no-gather", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
@@ -182,7 +186,8 @@ def main():
     make_local = lambda **kw: MergeVectorEnv(num_ac=args.num_ac, seed=1234,  # noqa: E731
                                              compute_cd=not args.no_cd, **kw)
     if gather:
-        env = ShardedVectorEnv(make_local, world * E, overlap=(backend == "nccl"))
+        env = ShardedVectorEnv(make_local, world * E, overlap=(backend == "nccl"),
+                               steps_per_gather=args.steps_per_gather)
         batch = env.local.batch
         env.reset()
     else:
@@ -192,15 +197,18 @@ def main():
     gen = torch.Generator(device=dev)
     gen.manual_seed(17 + rank)
     bank = torch.rand((16, E, 2), dtype=torch.float64, device=dev, generator=gen) * 2 - 1
+    acts = [bank[k] for k in range(16)]          # views made once, outside the timed region
 
     def one(k):
         if gather:
-            env.step(bank[k % 16])
+            env.step(acts[k % 16])
         else:
-            batch.step(bank[k % 16])
+            batch.step(acts[k % 16])
 
     for k in range(args.warmup):
         one(k)
+    if gather:
+        env.flush()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -213,6 +221,10 @@ def main():
     ev0.record()
     for k in range(args.steps):
         one(k)
+    if gather:
+        _, ready = env.flush()                 # the last partial block's rows, inside the region
+        if ready is not None:
+            ready.wait()
     ev1.record()
     torch.cuda.synchronize()
     if world > 1:
@@ -225,11 +237,11 @@ def main():
         # with the gather the bracket above also holds the RCCL Work.wait() stream waits;
         # the kernel's own time comes from the same launches without the collective
         for k in range(args.warmup):
-            batch.step(bank[k % 16])
+            batch.step(acts[k % 16])
         torch.cuda.synchronize()
         ev0.record()
         for k in range(args.steps):
-            batch.step(bank[k % 16])
+            batch.step(acts[k % 16])
         ev1.record()
         torch.cuda.synchronize()
         kern_avg_ms = ev0.elapsed_time(ev1) / args.steps
@@ -283,7 +295,9 @@ def main():
             "config": {
                 "workload": f"MergeEnv-v0 {world * E} envs x {N} aircraft ({E} per GPU), 10 substeps x DT 5 s, "
                             f"StateBased CD {'off' if args.no_cd else 'on'}, NEXT_STEP autoreset"
-                            + ((", RCCL" if backend == "nccl" else f", {backend}") + " all_gather of [E, obs+3] fp32 per step"
+                            + ((", RCCL" if backend == "nccl" else f", {backend}")
+                               + (" all_gather of [E, obs+3] fp32 per step" if args.steps_per_gather == 1 else
+                                  f" all_gather of [{args.steps_per_gather}, E, obs+3] fp32 per {args.steps_per_gather} steps")
                                if gather else ""),
                 "envs_total": world * E,
                 "envs_per_gpu": E,
@@ -291,6 +305,7 @@ def main():
                 "parallelism": f"env-shard x{world}" + ((" + RCCL all_gather (overlapped)" if backend == "nccl"
                                                           else f" + {backend} all_gather") if gather else ""),
                 "backend": backend if world > 1 else None,
+                "steps_per_gather": args.steps_per_gather if gather else None,
             },
             "roofline": {
                 # the binding limit is fp64 VALU dependency latency; `frac`

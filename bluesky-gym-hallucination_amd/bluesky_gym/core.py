@@ -11,6 +11,10 @@ import torch
 from . import _native as nat
 from .config import EnvKindConfig
 
+# torch's raw current-stream getter (an int handle; the public torch.cuda.current_stream()
+# builds a Stream object per call); absent in some builds -> the public API
+_raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+
 F64_STATE = ("lat", "lon", "alt", "hdg", "tas", "cas", "vs", "ax",
              "ap_trk", "selspd", "selalt", "selvs")
 I32_ENV = ("step_count", "flags", "wpt_reach", "faf_reached", "total_intrusions")
@@ -37,6 +41,7 @@ class DeviceBatch:
         self.K = cfg.num_ac_state
         self.device = torch.device("cuda", torch.cuda.current_device() if device is None
                                    else torch.device(device).index or 0)
+        self._dev_index = self.device.index
         self.autoreset = autoreset
         self.want_learner = bool(learner)
         self.want_memo = bool(memo_cache)
@@ -182,6 +187,10 @@ class DeviceBatch:
         self.learner = rows
 
     def _stream(self):
+        # the caller's current stream on this device (the raw handle getter skips building a
+        # torch.cuda.Stream object: ~2.4 -> ~0.3 us of host time per launch)
+        if _raw_stream is not None:
+            return C.c_void_p(_raw_stream(self._dev_index))
         return C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
 
     # ------------------------------------------------------------------ API

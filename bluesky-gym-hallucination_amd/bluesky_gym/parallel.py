@@ -1,6 +1,7 @@
 """Multi-GPU: one process per GPU (torch.distributed over RCCL/xGMI), env shards with no
-exchange during the step, and one all-gather per RL step of the learner rows
-[obs..., reward, terminated, truncated] (fp32) so every rank sees the whole node's batch.
+exchange during the step, and an all-gather of the learner rows [obs..., reward,
+terminated, truncated] (fp32) so every rank sees the whole node's batch -- one per RL step,
+or one per block of k steps (steps_per_gather: fewer, larger collectives).
 
 The gather of step t runs on RCCL's own stream while step t+1's kernel runs on the
 compute stream (double-buffered learner rows, async Work handles), so at 4096 envs per
@@ -46,85 +47,118 @@ class Ready:
 
 
 class ShardedVectorEnv:
-    """Local shard of a node-wide vector env + per-step learner-row all-gather.
+    """Local shard of a node-wide vector env + the learner-row all-gather.
 
-    Per step the host does: one bsg_step launch, one pointer swap of the learner rows
-    (bsg_set_learner) and one asynchronous all_gather_into_tensor -- RCCL runs it on its
-    own stream after the step kernel, concurrently with the next step's kernel; the
-    kernel two steps later, which rewrites the same rows buffer, is ordered after it by
-    Work.wait() (a stream wait, the host does not block).  Keeping the host side to these
-    three calls matters: a full re-bind plus event bookkeeping per step cost ~70 us of host
-    time, as much as the kernel itself (tools/shard_overhead.py)."""
+    Per step the host does: one bsg_step launch and one pointer swap of the learner rows
+    (bsg_set_learner); per block of k = steps_per_gather steps one asynchronous
+    all_gather_into_tensor of the block's k x [n_local, obs+3] rows.  RCCL runs it on its
+    own stream after the block's last kernel, concurrently with the next block's kernels;
+    the kernel that next rewrites the block's rows (two blocks later: the rows are a ring
+    of two blocks) is ordered after it by Work.wait() (a stream wait, the host does not
+    block).  The host side matters at C4's shard sizes: a 512-env shard's kernel is ~30 us,
+    while one all_gather enqueue costs ~13-30 us and Work.wait ~7 us of host time
+    (profiles/r03/shard_host_breakdown.txt) -- per step they made the loop host-bound;
+    per block of 8 they are ~5 us a step.  (A full re-bind plus event bookkeeping per step
+    cost ~70 us of host time, tools/shard_overhead.py.)
 
-    def __init__(self, make_local, total_envs: int, *, overlap=True, group=None, collective=None):
+    k = 1 (default): step() returns (rows [total_envs, obs+3], Ready) every step.
+    k > 1: step() returns (None, None) inside a block and, at the block's last step,
+    (block, Ready) with block a [k, world, n_local, obs+3] view (step, rank, env of the
+    rank; .reshape(k, total_envs, -1) gives global env order, as a copy).  flush()
+    gathers a partial block (call it before reading the rows of the last steps)."""
+
+    def __init__(self, make_local, total_envs: int, *, overlap=True, group=None, collective=None,
+                 steps_per_gather: int = 1):
         """collective: optional ``f(out, rows) -> Work`` that starts the gather of this
         rank's rows into ``out`` asynchronously (``Work.wait()`` = a stream wait), in place
         of RCCL's all_gather_into_tensor -- another transport, or a test's delayed copy
         (tests/test_gpu_sharded.py).  With it the overlapped path is used at any world size."""
+        if int(steps_per_gather) < 1:
+            raise ValueError("steps_per_gather must be >= 1")
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         self.group = group
         self.offset, self.n_local = shard_range(total_envs, self.world, self.rank)
+        self.total_envs = total_envs
+        self.k = int(steps_per_gather)
         self.local = make_local(num_envs=self.n_local, env_offset=self.offset, learner=True)
         b = self.local.batch
         d = b.obs_dim + 3
+        self.row_dim = d
         dev = b.device
-        self._rows = [b.learner, torch.zeros_like(b.learner)]
-        self._gathered = [torch.empty((total_envs, d), dtype=torch.float32, device=dev)
-                          for _ in range(2)]
-        self._cur = 0
+        # rows[blk, i]: the kernel's learner output of step i of block blk (a ring of 2 blocks)
+        self._rows = torch.zeros((2, self.k, self.n_local, d), dtype=torch.float32, device=dev)
+        self._gathered = [torch.empty((self.world * self.k, self.n_local, d), dtype=torch.float32,
+                                      device=dev) for _ in range(2)]
+        self._blk, self._i = 0, 0
         self._collective = collective
         self.overlap = collective is not None or (overlap and self.world > 1)
         self._work = [None, None]
 
-    def _swap_in(self):
-        """rows[cur] becomes the kernel's learner output, once the gather two launches ago
-        (which reads the same buffer) is done."""
-        b = self.local.batch
-        cur = self._cur
-        w = self._work[cur]
-        if w is not None:
-            w.wait()
-            self._work[cur] = None
-        if b.learner is not self._rows[cur]:
-            b.set_learner(self._rows[cur])
-        return cur
+    def _slot(self):
+        """Point the kernel's learner output at the next slot; before the first write into a
+        block, wait (on the stream) for that block's previous gather."""
+        blk, i = self._blk, self._i
+        if i == 0:
+            w = self._work[blk]
+            if w is not None:
+                w.wait()
+                self._work[blk] = None
+        self.local.batch.set_learner(self._rows[blk, i])
+        return blk, i
 
     def reset(self, **kw):
         """Resets the local shard and gathers every rank's reset rows (obs, reward 0,
-        terminated 0, truncated 0): returns (gathered rows [total_envs, obs+3], Ready) like
-        step(), so a learner on any rank sees the node's first observations.  The local
+        terminated 0, truncated 0) at once, as a block of one step: returns (rows, Ready)
+        shaped as step() does (k = 1: [total_envs, obs+3]; k > 1: [1, world, n_local,
+        obs+3]).  A partial block of earlier steps is flushed (gathered) first.  The local
         shard's Dict observation stays available as self.local_obs."""
-        cur = self._swap_in()
+        if self._i:
+            self.flush()
+        blk, _ = self._slot()
         # (a reset(seed=) that rebuilds the batch keeps the learner buffer: vector.py)
         self.local_obs, self.local_info = self.local.reset(**kw)
-        assert self.local.batch.learner is self._rows[cur]
-        return self._gather(cur)
+        return self._gather(blk, 1)
 
     def step(self, local_actions):
-        """Steps the local shard; returns (gathered rows [total_envs, obs+3], Ready).  The
-        rows of this step may be read after ready.wait(), until the step after next."""
-        cur = self._swap_in()
+        """Steps the local shard.  k = 1: returns (gathered rows [total_envs, obs+3],
+        Ready); they may be read after ready.wait(), until the step after next.  k > 1:
+        (None, None) inside a block, (block, Ready) at its last step; a block stays valid
+        until the end of the next block."""
+        blk, i = self._slot()
         self.local.step_tensors(local_actions)
-        return self._gather(cur)
+        if i + 1 < self.k:
+            self._i = i + 1
+            return None, None
+        return self._gather(blk, self.k)
 
-    def _gather(self, cur):
+    def flush(self):
+        """Gather the steps of the current partial block now (k > 1); (None, None) if the
+        block is empty."""
+        if self._i == 0:
+            return None, None
+        return self._gather(self._blk, self._i)
+
+    def _gather(self, blk, n):
+        src = self._rows[blk, :n]                       # [n, n_local, d], contiguous
+        out = self._gathered[blk][: self.world * n]     # rank-major: out[r * n + i]
         if self.overlap:
             if self._collective is not None:
-                work = self._collective(self._gathered[cur], self._rows[cur])
+                work = self._collective(out, src)
             else:
-                work = all_gather_rows(self._gathered[cur], self._rows[cur], self.group,
-                                       async_op=True)
-            self._work[cur] = work
+                work = all_gather_rows(out, src, self.group, async_op=True)
+            self._work[blk] = work
             ready = Ready(work)
         elif self.world == 1:
-            self._gathered[cur][: self.n_local].copy_(self._rows[cur])
+            out.copy_(src)
             ready = Ready()
         else:
-            all_gather_rows(self._gathered[cur], self._rows[cur], self.group)
+            all_gather_rows(out, src, self.group)
             ready = Ready()
-        self._cur = 1 - cur
-        return self._gathered[cur], ready
+        self._blk, self._i = 1 - blk, 0
+        if self.k == 1:
+            return out.view(self.total_envs, self.row_dim), ready
+        return out.view(self.world, n, self.n_local, self.row_dim).permute(1, 0, 2, 3), ready
 
     def close(self):
         for w in self._work:

@@ -256,24 +256,6 @@ __host__ __device__ __forceinline__ SinCos sincos_dd(double x) {
   return o;
 }
 
-// advance by d (|d| <= 0.2): sin d to d^11, cos d - 1 to d^12 (truncation < 2^-70 |d|) --
-// a heading that turns at the standard rate moves up to ~0.18 rad in a 5 s substep
-__host__ __device__ __forceinline__ void sincos_add_w(SinCos& a, double d) {
-  const double z = d * d;
-  const double sd = fma(d * z, fma(z, fma(z, fma(z, fma(z, -1.0 / 39916800.0, 1.0 / 362880.0),
-                                                  -1.0 / 5040.0), 1.0 / 120.0), -1.0 / 6.0), d);
-  const double cm1 = z * fma(z, fma(z, fma(z, fma(z, fma(z, 1.0 / 479001600.0, -1.0 / 3628800.0),
-                                                  1.0 / 40320.0), -1.0 / 720.0), 1.0 / 24.0), -0.5);
-  const double ts = fma(a.s, cm1, a.c * sd) + a.sl;
-  const double tc = fma(a.c, cm1, -(a.s * sd)) + a.cl;
-  const double hs = a.s + ts, hc = a.c + tc;
-  const double bs = hs - a.s, bc = hc - a.c;
-  a.sl = (a.s - (hs - bs)) + (ts - bs);
-  a.cl = (a.c - (hc - bc)) + (tc - bc);
-  a.s = hs;
-  a.c = hc;
-}
-
 // advance by d (|d| <= 0.05): sin d to d^7, cos d - 1 to d^8 (truncation < 2^-70 |d|)
 __host__ __device__ __forceinline__ void sincos_add(SinCos& a, double d) {
   const double z = d * d;

@@ -201,9 +201,6 @@ struct RouteRegs {
   }
 };
 
-#ifndef BSG_X_HDG
-#define BSG_X_HDG 0
-#endif
 struct Memo {
   uint64_t alt_bits;               // key of at = vatmos(alt)
   Atmos at;
@@ -222,8 +219,6 @@ struct Memo {
   double phdg;                     // pymod360(hdg), for LNAV's waypoint-behind test
   uint64_t hdg_bits;               // key of (shdg, chdg) = sincos(hdg * D2R)
   double shdg, chdg;
-  double hdgr;                     // hdg * D2R and its sin/cos carried (!HMEMO kinds)
-  SinCos hdg_sc;
   double turnrad;                  // LNAV turn radius tas^2/(g0*tan(bank)) of the current tas
   double last_alt;                 // altitude at the start of the latest substep
   uint64_t cas_tas_bits, cas_alt_bits;  // key of the stored cas = vtas2cas(tas, alt)
@@ -262,8 +257,6 @@ __device__ __forceinline__ void memo_init(Memo& m, const AC& s) {
   m.wp_k = -1; m.wp_lat = 0; m.wp_lon = 0; m.wp_nq = 0; m.wp_cos = 0; m.wp_sin = 0; m.wp_rw = 0;
   m.wp_pnq = 0;
   m.hdg_bits = kNoKey; m.shdg = 0; m.chdg = 0;
-  m.hdgr = s.hdg * kD2R;
-  m.hdg_sc = BSG_X_HDG ? sincos_dd(m.hdgr) : SinCos{0.0, 0.0, 1.0, 0.0};
   m.phdg = pymod360(s.hdg);
   m.turnrad = 0;
   m.last_alt = s.alt;
@@ -595,14 +588,6 @@ __device__ __forceinline__ void substep(AC& s, Memo& m, double dt, const RouteRe
       sincos_t(s.hdg * kD2R, &m.shdg, &m.chdg);
       m.hdg_bits = bits(s.hdg);
     }
-  } else if (BSG_X_HDG) {
-    const double hr = s.hdg * kD2R;
-    const double d = hr - m.hdgr;
-    if (fabs(d) <= 0.2) sincos_add_w(m.hdg_sc, d);
-    else m.hdg_sc = sincos_dd(hr);
-    m.hdgr = hr;
-    m.shdg = m.hdg_sc.s;
-    m.chdg = m.hdg_sc.c;
   } else {
     // LNAV lanes re-aim at the waypoint's bearing every substep, so some lane of a wave
     // always misses the memo: its branch would only add latency

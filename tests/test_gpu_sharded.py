@@ -30,7 +30,15 @@ def _actions(total):
     return torch.rand((T, total, 2), dtype=torch.float64, generator=g) * 2 - 1
 
 
-def _shard_worker(rank, world, port, overlap, q):
+def _rows_list(rows, total):
+    """The per-step [total, d] rows of a gathered result (k = 1: one step; k > 1: a block
+    [n, world, n_local, d])."""
+    if rows.dim() == 2:
+        return [rows.cpu().numpy().copy()]
+    return [rows[i].reshape(total, -1).cpu().numpy().copy() for i in range(rows.shape[0])]
+
+
+def _shard_worker(rank, world, port, overlap, k, q):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
                       HSA_ENABLE_IPC_MODE_LEGACY="0")
@@ -42,18 +50,20 @@ def _shard_worker(rank, world, port, overlap, q):
         total = world * E_LOCAL
         env = ShardedVectorEnv(lambda **kw: MergeVectorEnv(num_ac=32, seed=SEED, compute_cd=True,
                                                            max_episode_steps=MAXEP, **kw),
-                               total, overlap=overlap)
+                               total, overlap=overlap, steps_per_gather=k)
         acts = _actions(total)
         rows, ready = env.reset()
         ready.wait()
         torch.cuda.synchronize()
-        out = [rows.cpu().numpy().copy()]
+        out = _rows_list(rows, total)
         for t in range(T):
             a = acts[t, env.offset:env.offset + env.n_local].cuda()
             rows, ready = env.step(a)
+            if rows is None:
+                continue
             ready.wait()
             torch.cuda.synchronize()
-            out.append(rows.cpu().numpy().copy())
+            out += _rows_list(rows, total)
         env.close()
         q.put((rank, np.stack(out) if rank == 0 else None, None))
     except Exception as ex:  # pragma: no cover - reported to the parent
@@ -62,8 +72,9 @@ def _shard_worker(rank, world, port, overlap, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("overlap", [True, False])
-def test_sharded_rows_match_one_batch(overlap):
+@pytest.mark.parametrize("overlap,k", [(True, 1), (False, 1), (True, 4)])
+def test_sharded_rows_match_one_batch(overlap, k):
+    """k = steps_per_gather: one all-gather per step, or per block of 4 steps."""
     import torch.multiprocessing as mp
     from bluesky_gym import config, core
     world = 2
@@ -71,7 +82,7 @@ def test_sharded_rows_match_one_batch(overlap):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_shard_worker, args=(r, world, port, overlap, q)) for r in range(world)]
+    procs = [ctx.Process(target=_shard_worker, args=(r, world, port, overlap, k, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = {}
@@ -130,38 +141,45 @@ class _DelayedGather:
         return Work()
 
 
-def _ordering_run(gather, T_steps=64, E=256):
+def _ordering_run(gather, T_steps=64, E=256, k=1):
     """ShardedVectorEnv (one rank) over the delayed gather, with no host sync between steps:
-    each step's gathered rows are cloned on the compute stream after ready.wait()."""
+    each gathered step's rows are cloned on the compute stream after ready.wait()."""
     from bluesky_gym.parallel import ShardedVectorEnv
     from bluesky_gym.vector import MergeVectorEnv
     env = ShardedVectorEnv(lambda **kw: MergeVectorEnv(num_ac=32, seed=SEED, compute_cd=True,
                                                        max_episode_steps=MAXEP, **kw),
-                           E, collective=gather)
+                           E, collective=gather, steps_per_gather=k)
     g = torch.Generator().manual_seed(9)
     acts = (torch.rand((T_steps, E, 2), dtype=torch.float64, generator=g) * 2 - 1).cuda()
     hist = []
+    def take(rows):
+        return [rows.clone()] if rows.dim() == 2 else [rows[i].reshape(E, -1).clone()
+                                                        for i in range(rows.shape[0])]
     rows, ready = env.reset()
     ready.wait()
-    hist.append(rows.clone())
+    hist += take(rows)
     for t in range(T_steps):
         rows, ready = env.step(acts[t])
+        if rows is None:
+            continue
         ready.wait()
-        hist.append(rows.clone())
+        hist += take(rows)
     torch.cuda.synchronize()
     env.close()
     return torch.stack(hist).cpu().numpy(), acts
 
 
-def test_overlapped_gather_never_reads_rewritten_rows():
+@pytest.mark.parametrize("k", [1, 4])
+def test_overlapped_gather_never_reads_rewritten_rows(k):
     """the stream ordering of ShardedVectorEnv's overlapped gather.  The
-    kernel of step t+2 rewrites the rows buffer step t's gather reads; _swap_in's
-    Work.wait() must order it after that (delayed) read.  Bit-exact against one batch over
-    64 steps with autoresets; the negative control (a wait() that orders nothing) must be
-    caught by the same comparison, so the test can see the hazard it guards against."""
+    kernel that next writes a block's rows (two blocks later: k = 1, the step after next)
+    rewrites the buffer that block's gather reads; _slot's Work.wait() must order it after
+    that (delayed) read.  Bit-exact against one batch over 64 steps with autoresets; the
+    negative control (a wait() that orders nothing) must be caught by the same comparison,
+    so the test can see the hazard it guards against.  k = 4: blocks of 4 steps per gather."""
     from bluesky_gym import config, core
     delay = 1_000_000                   # >> one 256-env step kernel at either clock rate
-    got, acts = _ordering_run(_DelayedGather(delay))
+    got, acts = _ordering_run(_DelayedGather(delay), k=k)
     E = acts.shape[1]
     b = core.DeviceBatch(config.merge_config(num_ac=32, max_episode_steps=MAXEP), E,
                          compute_cd=True, seed=SEED, learner=True)
@@ -173,7 +191,7 @@ def test_overlapped_gather_never_reads_rewritten_rows():
     want = torch.stack(want).cpu().numpy()
     assert np.array_equal(got.view(np.uint32), want.view(np.uint32)), \
         np.argwhere(got.view(np.uint32) != want.view(np.uint32))[:5]
-    bad, _ = _ordering_run(_DelayedGather(delay, honour_wait=False))
+    bad, _ = _ordering_run(_DelayedGather(delay, honour_wait=False), k=k)
     assert not np.array_equal(bad.view(np.uint32), want.view(np.uint32)), \
         "the un-ordered control gathered correct rows: the delay does not expose the hazard"
 

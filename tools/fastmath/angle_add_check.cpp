@@ -19,10 +19,6 @@ static int64_t ord(double v) {
   return i < 0 ? INT64_MIN - i : i;
 }
 
-#ifndef WIDE
-#define WIDE 0
-#endif
-
 int main() {
   std::mt19937_64 rng(5);
   std::uniform_real_distribution<double> U(-1.0, 1.0);
@@ -33,14 +29,14 @@ int main() {
   for (int t = 0; t < T; ++t) {
     const bool gap = t & 1;
     double x = gap ? 3.0 * U(rng) * (M_PI / 180) : 80.0 * U(rng) * (M_PI / 180);
-    const double step = (WIDE ? 0.18 : 2e-3) * U(rng);
+    const double step = 2e-3 * U(rng);
     bsg::SinCos sc = bsg::sincos_dd(x);
     double s0, c0;
     bsg::sincos_t(x, &s0, &c0);
     if (s0 != sc.s || c0 != sc.c) { std::printf("sincos_dd != sincos_t at %a\n", x); return 1; }
     for (int k = 0; k < K; ++k) {
       const double xn = x + step * (1.0 + 0.1 * U(rng));
-      if (WIDE) bsg::sincos_add_w(sc, xn - x); else bsg::sincos_add(sc, xn - x);
+      bsg::sincos_add(sc, xn - x);
       x = xn;
       const double s = sc.s, c = sc.c;
       const double rs = std::sin(x), rc = std::cos(x);

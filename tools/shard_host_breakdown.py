@@ -3,7 +3,7 @@ path (world-size-1 NCCL group on one GPU, as tools/shard_overhead_nccl.py): the 
 of two steps ago, the learner-row pointer swap, the step launch (and its parts), the
 all-gather enqueue.  Finds what to cut so that a C4 shard's host side stays below its
 ~30 us kernel.
-    python tools/shard_host_breakdown.py [E]
+    python tools/shard_host_breakdown.py [E] [steps_per_gather]
 """
 import os
 import sys
@@ -28,8 +28,9 @@ def main():
     torch.cuda.set_device(0)
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
     coll = lambda out, rows: dist.all_gather_into_tensor(out, rows, async_op=True)  # noqa: E731
+    K = int(sys.argv[2]) if len(sys.argv) > 2 else 1
     s = parallel.ShardedVectorEnv(lambda **kw: MergeVectorEnv(num_ac=32, seed=1, compute_cd=True, **kw),
-                                  E, collective=coll)
+                                  E, collective=coll, steps_per_gather=K)
     s.reset()
     b = s.local.batch
     bank = torch.rand((16, E, 2), dtype=torch.float64, device="cuda") * 2 - 1
@@ -39,8 +40,9 @@ def main():
     def tick(name, t0):
         acc[name] = acc.get(name, 0.0) + time.perf_counter() - t0
 
-    for k in range(30):
+    for k in range(32):
         s.step(views[k % 16])
+    s.flush()
     torch.cuda.synchronize()
     acc.clear()
     t_all = time.perf_counter()
@@ -49,30 +51,25 @@ def main():
         x = bank[k % 16]
         tick("bank[k] view", t0)
         t0 = time.perf_counter()
-        cur = s._cur
-        w = s._work[cur]
-        if w is not None:
-            w.wait()
-            s._work[cur] = None
-        tick("Work.wait", t0)
-        t0 = time.perf_counter()
-        if b.learner is not s._rows[cur]:
-            b.set_learner(s._rows[cur])
-        tick("set_learner", t0)
+        blk, i = s._slot()
+        tick("_slot (Work.wait + set_learner)", t0)
         t0 = time.perf_counter()
         st = torch.cuda.current_stream(b.device).cuda_stream
-        tick("  current_stream", t0)
+        tick("  torch.cuda.current_stream", t0)
         t0 = time.perf_counter()
         s.local.step_tensors(x)
         tick("step_tensors", t0)
         t0 = time.perf_counter()
-        s._gather(cur)
+        if i + 1 < s.k:
+            s._i = i + 1
+        else:
+            s._gather(blk, s.k)
         tick("_gather (all_gather enqueue)", t0)
     torch.cuda.synchronize()
     wall = (time.perf_counter() - t_all) / T * 1e6
     for n, v in acc.items():
-        print(f"E={E} {n:32s} {v / T * 1e6:7.2f} us/call", flush=True)
-    print(f"E={E} wall per step {wall:.1f} us (incl. the instrumentation)", flush=True)
+        print(f"E={E} k={K} {n:32s} {v / T * 1e6:7.2f} us/call", flush=True)
+    print(f"E={E} k={K} wall per step {wall:.1f} us (incl. the instrumentation)", flush=True)
     t0 = time.perf_counter()
     for k in range(T):
         b.lib.bsg_abi_version()

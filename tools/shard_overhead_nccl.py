@@ -50,16 +50,20 @@ def main():
               flush=True)
         v.close()
         coll = lambda out, rows: dist.all_gather_into_tensor(out, rows, async_op=True)  # noqa: E731
-        s = parallel.ShardedVectorEnv(
-            lambda **kw: MergeVectorEnv(num_ac=32, seed=1, compute_cd=True, **kw), E,
-            collective=coll)
-        s.reset()
-        w, h = timed(lambda k: s.step(bank[k % 16]))
-        print(f"E={E:5d} ShardedVectorEnv.step (RCCL) wall/step {w:7.1f} us  host/call {h:6.1f} us",
-              flush=True)
+        for K in (1, 8):
+            s = parallel.ShardedVectorEnv(
+                lambda **kw: MergeVectorEnv(num_ac=32, seed=1, compute_cd=True, **kw), E,
+                collective=coll, steps_per_gather=K)
+            s.reset()
+            w, h = timed(lambda k: s.step(bank[k % 16]))
+            print(f"E={E:5d} ShardedVectorEnv.step (RCCL, {K} step(s) per gather) wall/step {w:7.1f} us  "
+                  f"host/call {h:6.1f} us", flush=True)
+            if K == 8:
+                break
+            s.close()
         # the enqueue cost of the collective alone
         out = torch.empty((E, s.local.batch.obs_dim + 3), dtype=torch.float32, device="cuda")
-        rows = s._rows[0]
+        rows = s._rows[0, 0]
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for k in range(T):
