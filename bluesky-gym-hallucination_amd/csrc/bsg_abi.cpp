@@ -23,6 +23,7 @@ struct bsg_ctx {
   int obs_dim = 0;
   int spawn_width = 0;
   bsg::Route route{};
+  bsg::RouteTrig route_t{};
   bsg::WindDev wind{};
   // optional per-launch timing (bsg_set_timing): an event pair around every
   // `timing`-th launch (0 = off)
@@ -95,6 +96,7 @@ bsg::KParams make_params(const bsg_ctx* c, int mode) {
   std::memset(&p, 0, sizeof(p));
   p.cfg = c->cfg;
   p.route = c->route;
+  p.route_t = c->route_t;
   p.b = c->bufs;
   p.mode = mode;
   p.E = c->cfg.num_envs;
@@ -337,6 +339,9 @@ int32_t bsg_create(const bsg_config* cfg, bsg_ctx** out) {
     const double an = a * a * std::cos(lat), bn = b * b * std::sin(lat);
     const double ad = a * std::cos(lat), bd = b * std::sin(lat);
     c->route.rwgs[k] = std::sqrt((an * an + bn * bn) / (ad * ad + bd * bd));
+    bsg::sincos_t(cfg->route_lat[k] * bsg::kD2R, &c->route_t.sinlat[k], &c->route_t.coslat[k]);
+    c->route_t.lonr[k] = cfg->route_lon[k] * bsg::kD2R;
+    c->route_t.pnq[k] = bsg::pymod360(cfg->route_next_qdr[k]);
   }
   if (const char* pad = std::getenv("BSG_LDS_PAD_BYTES")) c->lds_pad = (unsigned)std::atoi(pad);
   if (const char* nf = std::getenv("BSG_NO_FASTPATH")) c->no_fastpath = std::atoi(nf) != 0;

@@ -56,6 +56,14 @@ __device__ __forceinline__ uint64_t bits(double x) { return (uint64_t)__double_a
 
 __device__ __forceinline__ double sgn(double x) { return (double)((x > 0.0) - (x < 0.0)); }
 
+// (double)on * sgn(d) * c for c >= 0, bit for bit (the zero's sign included: -0.0 when
+// d < 0), without the int -> double conversion and two multiplies.  Every use has
+// on => d != 0 (on is |d| > some threshold >= 0), where sgn(d) * c = +-c.
+__device__ __forceinline__ double sgnmul(bool on, double d, double c) {
+  const double v = on ? c : 0.0;
+  return d < 0.0 ? -v : v;
+}
+
 // np.remainder(a, 360.0) (numpy npy_divmod: fmod, then the sign fix).  |a| < 360 is every
 // call but a rare one: there fmod(a, 360) = a exactly, and the result is a + 360 for
 // a < 0 (npy_divmod's one rounding) or a + 0.0 otherwise (the identity, with -0 -> +0 as

@@ -18,6 +18,15 @@ struct Route {
                                 // only inside rounding-slack bounds, bsg_device.h)
 };
 
+// The per-waypoint terms of the LNAV loop, computed once on the host with the device's own
+// functions (bit-identical there, tools/probe/fastmath_probe.hip): sincos_t of lat * D2R,
+// lon * D2R, pymod360(next_qdr).  At the end of KParams, so that the offsets of the fields
+// every launch reads stay as they were (moving the buffer pointers measured +2 % on
+// Vertical / Descent).
+struct RouteTrig {
+  double sinlat[BSG_MAX_ROUTE], coslat[BSG_MAX_ROUTE], lonr[BSG_MAX_ROUTE], pnq[BSG_MAX_ROUTE];
+};
+
 struct WindDev {
   int np;                    // points (0: wind off)
   int nlev;                  // 1 or BSG_WIND_NALT
@@ -58,6 +67,7 @@ struct KParams {
   int la_grid0;              // main workgroups (set by the launcher)
   int no_fastpath;           // BSG_NO_FASTPATH=1 at bsg_create: the general substep only
                              // (tests compare the specialised paths against it)
+  RouteTrig route_t;         // (last: see RouteTrig)
 };
 
 hipError_t launch_step(const KParams& p, hipStream_t stream);

@@ -188,8 +188,10 @@ struct RouteRegs {
   int len;
   double lat0, lon0, nq0, rw0, lat1, lon1, nq1, rw1;
   const Route* r;
-  __device__ __forceinline__ void load(const Route& rr) {
+  const RouteTrig* t;
+  __device__ __forceinline__ void load(const Route& rr, const RouteTrig& tt) {
     r = &rr;
+    t = &tt;
     len = rr.len;
     lat0 = rr.lat[0]; lon0 = rr.lon[0]; nq0 = rr.next_qdr[0]; rw0 = rr.rwgs[0];
     lat1 = rr.lat[1]; lon1 = rr.lon[1]; nq1 = rr.next_qdr[1]; rw1 = rr.rwgs[1];
@@ -198,6 +200,11 @@ struct RouteRegs {
     if (k == 0) { *la = lat0; *lo = lon0; *q = nq0; *rw = rw0; }
     else if (k == 1) { *la = lat1; *lo = lon1; *q = nq1; *rw = rw1; }
     else { *la = r->lat[k]; *lo = r->lon[k]; *q = r->next_qdr[k]; *rw = r->rwgs[k]; }
+  }
+  // the host-computed trig / radian / pymod terms of waypoint k (Route)
+  __device__ __forceinline__ void get_t(int k, double* sl, double* cl, double* lr, double* pq) const {
+    const int i = k < 0 ? 0 : (k < BSG_MAX_ROUTE ? k : BSG_MAX_ROUTE - 1);
+    *sl = t->sinlat[i]; *cl = t->coslat[i]; *lr = t->lonr[i]; *pq = t->pnq[i];
   }
 };
 
@@ -335,9 +342,7 @@ __device__ __forceinline__ double turnrad_of(double tas) {
 __device__ __forceinline__ void memo_wp(Memo& m, const RouteRegs& rt, int k) {
   m.wp_k = k;
   rt.get(k, &m.wp_lat, &m.wp_lon, &m.wp_nq, &m.wp_rw);
-  m.wp_pnq = pymod360(m.wp_nq);
-  sincos_t(m.wp_lat * kD2R, &m.wp_sin, &m.wp_cos);
-  m.wp_lonr = m.wp_lon * kD2R;
+  rt.get_t(k, &m.wp_sin, &m.wp_cos, &m.wp_lonr, &m.wp_pnq);
 }
 
 // the LNAV longitude gap's trig evaluated in full (launch start, a new active waypoint)
@@ -544,7 +549,7 @@ __device__ __forceinline__ void substep(AC& s, Memo& m, double dt, const RouteRe
   // update_airspeed (traf.cas is evaluated after the last substep, see step_kernel)
   const double delta_spd = allow_tas - s.tas;
   const bool need_ax = fabs(delta_spd) > fabs(dt * axmax);
-  s.ax = (double)need_ax * sgn(delta_spd) * axmax;
+  s.ax = sgnmul(need_ax, delta_spd, axmax);
   s.tas = need_ax ? s.tas + s.ax * dt : allow_tas;
   m.turnrad = turnrad_of(s.tas);              // for the next substep's LNAV (off the chain)
   BSG_SUBSTEP_MARK(2);
@@ -567,7 +572,7 @@ __device__ __forceinline__ void substep(AC& s, Memo& m, double dt, const RouteRe
       turnrate = (G0 * TAN_BANKDEF / npmax(s.tas, EPS_SPD)) * kR2D;
       swhdgsel = fabs(delhdg) > fabs(dt * turnrate);
     }
-    const double ha = swhdgsel ? s.hdg + dt * turnrate * sgn(delhdg) : hdg_cmd;
+    const double ha = swhdgsel ? s.hdg + sgnmul(true, delhdg, dt * turnrate) : hdg_cmd;
     s.hdg = F ? pymod360_r(ha) : pymod360(ha);
   };
   if (!WIND && fh) turn(std::true_type{});
@@ -575,10 +580,10 @@ __device__ __forceinline__ void substep(AC& s, Memo& m, double dt, const RouteRe
   m.phdg = s.hdg >= 360.0 ? s.hdg - 360.0 : s.hdg;   // pymod360 of a [0, 360] value
   const double delta_alt = allow_h - s.alt;
   const bool swaltsel = fabs(delta_alt) > npmax(10 * FT, fabs(2 * fabs(dt * s.vs)));
-  const double target_vs = (double)swaltsel * sgn(delta_alt) * fabs(vs_cmd);
+  const double target_vs = sgnmul(swaltsel, delta_alt, fabs(vs_cmd));
   const double delta_vs = target_vs - s.vs;
   const bool need_az = fabs(delta_vs) > 300 * FPM;
-  const double az = (double)need_az * sgn(delta_vs) * (300 * FPM);
+  const double az = sgnmul(need_az, delta_vs, 300 * FPM);
   s.vs = need_az ? s.vs + az * dt : target_vs;
   if (!isfinite(s.vs)) s.vs = 0.0;
   // update_groundspeed + update_pos
@@ -1604,15 +1609,15 @@ __device__ __forceinline__ bool vert_own_fast(AC& s, int S, double dt, Atmos* at
     // update_airspeed
     const double delta_spd = allow_tas - s.tas;
     const bool need_ax = fabs(delta_spd) > fabs(dt * axmax);
-    s.ax = (double)need_ax * sgn(delta_spd) * axmax;
+    s.ax = sgnmul(need_ax, delta_spd, axmax);
     s.tas = need_ax ? s.tas + s.ax * dt : allow_tas;
     // (heading on its command: unchanged)  vertical speed
     const double delta_alt = allow_h - s.alt;
     const bool swaltsel = fabs(delta_alt) > npmax(10 * FT, fabs(2 * fabs(dt * s.vs)));
-    const double target_vs = (double)swaltsel * sgn(delta_alt) * fabs(vs_cmd);
+    const double target_vs = sgnmul(swaltsel, delta_alt, fabs(vs_cmd));
     const double delta_vs = target_vs - s.vs;
     const bool need_az = fabs(delta_vs) > 300 * FPM;
-    const double az = (double)need_az * sgn(delta_vs) * (300 * FPM);
+    const double az = sgnmul(need_az, delta_vs, 300 * FPM);
     s.vs = need_az ? s.vs + az * dt : target_vs;
     if (!isfinite(s.vs)) s.vs = 0.0;
     // update_groundspeed + update_pos
@@ -1706,7 +1711,7 @@ __device__ __forceinline__ void propagate(const KParams& p, int e, int j, size_t
     if (mcache) memo_load(m, mc, s0);
     if (j == 0 && mcache) { m.alt_bits = bits(oat[0]); m.at = Atmos{oat[1], oat[2], oat[3]}; }
     RouteRegs rt;
-    rt.load(p.route);
+    rt.load(p.route, p.route_t);
     memo_lnav(m, s, rt);
     const double dt = p.cfg.simdt;
     // substep's fast heading block (fh): every stepping lane of the wave has |ap_trk| < 360
@@ -2091,12 +2096,9 @@ __global__ __launch_bounds__(64 * CDW) BSG_WPE void step_kernel(KParams p) {
     BSG_STAMP(4, stamp_clock() | ((unsigned long long)total << 48));
 #endif
     // phase 2: dense exact StateBased over the surviving pairs, both orders per lane
-    for (int t = lane; t < total; t += 64) {
-      const int pr = cd_list[t];
+    auto commit = [&](int pr, const CdOut* r) {
       const int li = pr >> 6, lk = pr & 63;
       const int gb = (li / GS) * GS;
-      CdOut r[2];
-      cd_pair2(L, li, lk, &r[0], &r[1]);
 #pragma unroll
       for (int o = 0; o < 2; ++o) {
         const int row = o ? lk : li, col = (o ? li : lk) - gb;
@@ -2107,6 +2109,12 @@ __global__ __launch_bounds__(64 * CDW) BSG_WPE void step_kernel(KParams p) {
           if (r[o].confl && r[o].tcpa > 0.0) atomicMax(&L.tmax[row], bits(r[o].tcpa));
         }
       }
+    };
+    for (int t = lane; t < total; t += 64) {
+      const int pr = cd_list[t];
+      CdOut r[2];
+      cd_pair2(L, pr >> 6, pr & 63, &r[0], &r[1]);
+      commit(pr, r);
     }
     __syncthreads();
     cmask = L.cm[lane];

@@ -12,7 +12,7 @@
 
 constexpr int NF = 12;
 
-__global__ void probe(bsg::Route route, const double* st, int S, double dt, long long* cyc,
+__global__ void probe(bsg::Route route, bsg::RouteTrig rtrig, const double* st, int S, double dt, long long* cyc,
                       int* okc, double* out_fast, double* out_gen) {
   using namespace bsg;
   const int l = threadIdx.x;
@@ -36,7 +36,7 @@ __global__ void probe(bsg::Route route, const double* st, int S, double dt, long
   Memo m;
   memo_init(m, b);
   RouteRegs rt;
-  rt.load(route);
+  rt.load(route, rtrig);
   memo_lnav(m, b, rt);
   WindDev w{};
   long long t2 = __builtin_amdgcn_s_memtime();
@@ -71,7 +71,7 @@ int main(int argc, char** argv) {
   (void)hipMemcpy(dst, st.data(), st.size() * 8, hipMemcpyHostToDevice);
   long long best[2] = {1LL << 62, 1LL << 62};
   for (int rep = 0; rep < 5; ++rep) {
-    hipLaunchKernelGGL(probe, dim3(1), dim3(64), 0, 0, route, dst, 30, 1.0, dcyc, dok, dfa, dgb);
+    hipLaunchKernelGGL(probe, dim3(1), dim3(64), 0, 0, route, bsg::RouteTrig{}, dst, 30, 1.0, dcyc, dok, dfa, dgb);
     long long c[2];
     (void)hipMemcpy(c, dcyc, 16, hipMemcpyDeviceToHost);
     for (int i = 0; i < 2; ++i) best[i] = c[i] < best[i] ? c[i] : best[i];

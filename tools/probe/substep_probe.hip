@@ -23,7 +23,7 @@ __device__ long long g_mark[8];
 constexpr int NF = 12;       // lat lon alt hdg tas cas vs ax ap_trk selspd selalt selvs, + nav
 constexpr int SMAX = 32;
 
-__global__ void probe(bsg::Route route, const double* st, int S, double dt, long long* cyc, double* out) {
+__global__ void probe(bsg::Route route, bsg::RouteTrig rtrig, const double* st, int S, double dt, long long* cyc, double* out) {
   using namespace bsg;
   const int l = threadIdx.x;
   AC s{};
@@ -41,7 +41,7 @@ __global__ void probe(bsg::Route route, const double* st, int S, double dt, long
   Memo m;
   memo_init(m, s);
   RouteRegs rt;
-  rt.load(route);
+  rt.load(route, rtrig);
   memo_lnav(m, s, rt);
   const bool trk_ok = __ballot(!(fabs(s.ap_trk) < 360.0)) == 0;        // as propagate
   const bool fh0 = trk_ok && __ballot(!(s.hdg >= 0.0 && s.hdg <= 360.0)) == 0;
@@ -71,10 +71,15 @@ int main(int argc, char** argv) {
       std::fread(st.data(), 8, st.size(), fp) != st.size()) return 2;
   std::fclose(fp);
   bsg::Route route{};
+  bsg::RouteTrig rtrig{};
   route.len = (int)hdr[0];
   for (int k = 0; k < BSG_MAX_ROUTE; ++k) {
     route.lat[k] = hdr[1 + k]; route.lon[k] = hdr[1 + BSG_MAX_ROUTE + k];
     route.next_qdr[k] = hdr[1 + 2 * BSG_MAX_ROUTE + k];
+    // (rwgs is only a bound's centre; the per-waypoint LNAV terms as bsg_create fills them)
+    bsg::sincos_t(route.lat[k] * bsg::kD2R, &rtrig.sinlat[k], &rtrig.coslat[k]);
+    rtrig.lonr[k] = route.lon[k] * bsg::kD2R;
+    rtrig.pnq[k] = bsg::pymod360(route.next_qdr[k]);
   }
   double *dst, *dout;
   long long* dcyc;
@@ -86,7 +91,7 @@ int main(int argc, char** argv) {
   if (S < 2 || S > SMAX) return 2;
   std::vector<long long> best(S, 1LL << 62);
   for (int rep = 0; rep < 7; ++rep) {
-    hipLaunchKernelGGL(probe, dim3(1), dim3(64), 0, 0, route, dst, S, dt, dcyc, dout);
+    hipLaunchKernelGGL(probe, dim3(1), dim3(64), 0, 0, route, rtrig, dst, S, dt, dcyc, dout);
     std::vector<long long> c(S);
     (void)hipMemcpy(c.data(), dcyc, S * 8, hipMemcpyDeviceToHost);
     for (int i = 0; i < S; ++i) best[i] = c[i] < best[i] ? c[i] : best[i];

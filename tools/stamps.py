@@ -22,7 +22,9 @@ gs = 1
 while gs < N:
     gs <<= 1
 grid = (E + 64 // gs - 1) // (64 // gs)
-st = torch.zeros((grid, 8), dtype=torch.int64, device="cuda")
+# (x2: with the lookahead on (E <= 2048) its extra workgroups, blockIdx >= grid, stamp
+# slots 0-1 before they branch off; their rows are ignored below)
+st = torch.zeros((2 * grid, 8), dtype=torch.int64, device="cuda")
 nat.check(b.lib.bsg_set_stamps(b._ctx, C.c_void_p(st.data_ptr())), "bsg_set_stamps")
 act = torch.rand((8, E, 2), dtype=torch.float64, device="cuda") * 2 - 1
 for k in range(30):
@@ -37,7 +39,7 @@ for k in range(5):
     flags = b.envs["flags"].cpu().numpy().copy()
     b.step(act[k % 8])
     torch.cuda.synchronize()
-    recs.append(st.cpu().numpy().astype(np.uint64))
+    recs.append(st[:grid].cpu().numpy().astype(np.uint64))
     post = {f: b.state[f].cpu().numpy() for f in ("lat", "lon", "hdg", "tas", "nav")}
     # per-lane features of this step, folded per wave (64/gs envs per wave)
     wp = np.where(((pre["nav"] >> 8) & 255) == 0, FIX[0], config.RWY_LAT)
@@ -140,3 +142,26 @@ print("  start(second) - start(first) ns", pct(np.array(start_gap) * 1000))
 print("  slot pairs (first,second) most common:",
       sorted(zip(*np.unique(np.stack([first_s, second_s], 1), axis=0, return_counts=True)),
              key=lambda t: -t[1])[:6])
+
+# what sets the kernel span: per-SIMD finish times (last wave's end - kernel start) and the
+# phases / features of the waves on the latest-finishing SIMDs
+print("per-SIMD finish (us after the first wave start), percentiles 50/90/99/99.9/100, and the "
+      "5 latest SIMDs' waves (A, B, CD1, CD2 kcycles; near, switch, turning, speed, resetting lanes; "
+      "CD candidates):")
+for run in range(1, 5):
+    s = np.arange(run * grid, (run + 1) * grid)
+    key = (((xcc[s] * 8 + se[s]) * 2 + sh[s]) * 16 + cu[s]) * 4 + simd[s]
+    t0k = rt0[s].min()
+    uk, inv = np.unique(key, return_inverse=True)
+    fin = np.zeros(len(uk), np.int64)
+    np.maximum.at(fin, inv, rt1[s] - t0k)
+    fin_us = fin * 10 / 1000
+    q = " ".join(f"{np.percentile(fin_us, p):6.1f}" for p in (50, 90, 99, 99.9, 100))
+    print(f" run {run}: {q}")
+    for j in np.argsort(fin)[-5:][::-1]:
+        ws = s[inv == j]
+        desc = []
+        for w in ws:
+            desc.append(f"[A {(c2[w]-c1[w])/1e3:5.1f} B {(c3[w]-c2[w])/1e3:4.1f} CD1 {(c4[w]-c3[w])/1e3:4.1f} "
+                        f"CD2 {(c5[w]-c4[w])/1e3:4.1f} | {' '.join(str(int(v)) for v in F[w, :5])} | cand {tot[w]}]")
+        print(f"   SIMD fin {fin_us[j]:5.1f} us: " + " ".join(desc))
