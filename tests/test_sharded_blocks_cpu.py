@@ -1,0 +1,127 @@
+"""ShardedVectorEnv's block bookkeeping on the CPU (no GPU): world-size-2 gloo processes
+drive it over a stand-in local env whose "kernel" writes known values into the learner
+slot it is pointed at, so the test sees exactly which slot each step wrote and where the
+gathered block puts it -- per step (k = 1) and per block (k = 3, with a partial block
+flushed), overlapped and not.  The GPU tests (tests/test_gpu_sharded.py) check the same
+path bit-exact against one device batch."""
+import os
+import socket
+
+import pytest
+import torch
+
+D = 4                    # row width (obs 1 + reward, terminated, truncated)
+N_LOCAL = 5
+T = 10
+
+
+class _Batch:
+    def __init__(self, n):
+        self.obs_dim = D - 3
+        self.device = torch.device("cpu")
+        self.learner = torch.zeros((n, D))
+        self.n = n
+
+    def set_learner(self, rows):
+        assert rows.is_contiguous() and tuple(rows.shape) == (self.n, D)
+        self.learner = rows
+
+
+class _Local:
+    """Writes value = 1000 * rank + 10 * step + column-independent env index into the
+    learner rows (step -1 = reset)."""
+
+    def __init__(self, num_envs, env_offset, learner):
+        assert learner
+        self.batch = _Batch(num_envs)
+        self.rank = env_offset // num_envs
+        self.t = -1
+
+    def _write(self):
+        env = torch.arange(self.batch.n, dtype=torch.float32)[:, None].expand(self.batch.n, D)
+        self.batch.learner.copy_(1000.0 * self.rank + 10.0 * self.t + env)
+
+    def reset(self, **kw):
+        self.t = -1
+        self._write()
+        return {}, {}
+
+    def step_tensors(self, actions):
+        self.t += 1
+        self._write()
+
+    def close(self):
+        pass
+
+
+def _expected(world, t):
+    env = torch.arange(N_LOCAL, dtype=torch.float32)
+    return torch.cat([1000.0 * r + 10.0 * t + env for r in range(world)])   # [total]
+
+
+def _worker(rank, world, port, k, overlap, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from bluesky_gym.parallel import ShardedVectorEnv
+        env = ShardedVectorEnv(_Local, world * N_LOCAL, overlap=overlap, steps_per_gather=k)
+        got = {}
+
+        def take(first_t, rows, ready):
+            ready.wait()
+            if rows.dim() == 2:
+                got[first_t] = rows[:, 0].clone()
+            else:
+                for i in range(rows.shape[0]):
+                    got[first_t + i] = rows[i].reshape(world * N_LOCAL, D)[:, 0].clone()
+
+        rows, ready = env.reset()
+        take(-1, rows, ready)
+        block_start = 0
+        for t in range(T):
+            rows, ready = env.step(None)
+            if rows is not None:
+                take(block_start, rows, ready)
+                block_start = t + 1
+        rows, ready = env.flush()
+        if rows is not None:
+            take(block_start, rows, ready)
+        env.close()
+        q.put((rank, {t: v.tolist() for t, v in got.items()}, None))
+    except Exception as ex:  # pragma: no cover - reported to the parent
+        q.put((rank, None, repr(ex)))
+    finally:
+        dist.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.parametrize("k,overlap", [(1, True), (1, False), (3, True), (3, False)])
+def test_blocks_deliver_every_step_in_order(k, overlap):
+    import torch.multiprocessing as mp
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, k, overlap, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        r, got, err = q.get(timeout=120)
+        assert err is None, f"rank {r}: {err}"
+        res[r] = got
+    for p in procs:
+        p.join(timeout=30)
+    for r in range(world):
+        got = res[r]
+        assert sorted(got) == list(range(-1, T)), sorted(got)     # reset + every step, once
+        for t, v in got.items():
+            assert v == _expected(world, t).tolist(), (r, t)
