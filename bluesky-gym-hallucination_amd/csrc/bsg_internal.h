@@ -68,6 +68,7 @@ struct KParams {
   int no_fastpath;           // BSG_NO_FASTPATH=1 at bsg_create: the general substep only
                              // (tests compare the specialised paths against it)
   RouteTrig route_t;         // (last: see RouteTrig)
+  int prio_sw_num, prio_sw_den;  // substep priority switch point (set by the launcher)
 };
 
 hipError_t launch_step(const KParams& p, hipStream_t stream);

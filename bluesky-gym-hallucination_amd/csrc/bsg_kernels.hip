@@ -1749,11 +1749,10 @@ __device__ __forceinline__ void propagate(const KParams& p, int e, int j, size_t
       // partners now finish ~5 us apart (-7 % kernel time).  Scheduling only: no effect on
       // results.
       const int slot = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (3 << 11)) & 15;  // HW_ID wave id
-#ifndef BSG_PRIO_SW_NUM
-#define BSG_PRIO_SW_NUM 3                  // switch after 3/4 of the substeps (swept:
-#define BSG_PRIO_SW_DEN 4                  // 1/2, 2/3, 9/10 measured slower, diag file)
-#endif
-      const int sw = (BSG_PRIO_SW_NUM * S + BSG_PRIO_SW_DEN - 1) / BSG_PRIO_SW_DEN;
+      // switch point: 3/4 of the substeps at two full-propagation waves per SIMD (4096
+      // envs: 1/2, 2/3, 4/5, 9/10 measured slower), 2/3 with the lookahead (2,048 envs:
+      // -1.8 %, profiles/r03/ab_prio_balance.txt); set per launch (launch_kind_w)
+      const int sw = (p.prio_sw_num * S + p.prio_sw_den - 1) / p.prio_sw_den;
       for (int it = 0; it < S; ++it) {
         if ((slot & 1) ? (it < sw) : (it >= sw)) __builtin_amdgcn_s_setprio(1);
         else __builtin_amdgcn_s_setprio(0);
@@ -1887,6 +1886,9 @@ __global__ __launch_bounds__(64 * CDW) BSG_WPE void step_kernel(KParams p) {
   if constexpr (kLA) {
     if (p.la && (int)blockIdx.x >= p.la_grid0) {
       lookahead_role<KIND, GS, WIND>(p);
+#if defined(BSG_STAMPS) && BSG_STAMPS
+      BSG_STAMP(6, __builtin_amdgcn_s_memrealtime());
+#endif
       return;                                  // the whole workgroup: no barrier below
     }
   }
@@ -2351,6 +2353,8 @@ static hipError_t launch_kind_w(const KParams& p0, hipStream_t st) {
   KParams p = p0;
   p.la_grid0 = grid0;
   if (!(KIND == BSG_ENV_MERGE && !WIND)) p.la = nullptr;
+  p.prio_sw_num = p.la ? 2 : 3;
+  p.prio_sw_den = p.la ? 3 : 4;
   const int grid = p.la ? 2 * grid0 : grid0;
 #define BSG_CASE(G) \
   case G: hipLaunchKernelGGL((step_kernel<KIND, G, WIND>), dim3(grid), dim3(64), p.lds_pad, st, p); break;

@@ -117,27 +117,40 @@ class _DelayedGather:
     semantics: the collective's stream waits for the caller's stream at enqueue, then (here)
     spins for a long delay before it reads the rows; Work.wait() makes the caller's
     current stream wait for the copy's completion event (the host never blocks).
-    honour_wait=False is the negative control: a Work whose wait() orders nothing."""
+    honour_wait=False is the negative control, made deterministic: a collective that reads
+    its rows only when the NEXT collective is enqueued -- after the kernels in between, so
+    whatever they rewrote is what it gathers -- with a wait() that orders nothing.  (A
+    delayed copy alone is not a reliable control: when the side stream shares a hardware
+    queue with the compute stream the two serialise and the hazard never shows.)"""
 
     def __init__(self, delay_cycles, honour_wait=True):
         self.side = torch.cuda.Stream()
         self.delay = delay_cycles
         self.honour = honour_wait
+        self.pending = None
 
     def __call__(self, out, rows):
         cur = torch.cuda.current_stream()
+        if not self.honour:
+            if self.pending is not None:
+                po, pr = self.pending
+                po[: pr.shape[0]].copy_(pr)          # on the compute stream, one call late
+            self.pending = (out, rows)
+
+            class NoWork:
+                def wait(self):
+                    pass
+            return NoWork()
         self.side.wait_stream(cur)
         with torch.cuda.stream(self.side):
             torch.cuda._sleep(self.delay)
             out[: rows.shape[0]].copy_(rows)
             done = torch.cuda.Event()
             done.record(self.side)
-        honour = self.honour
 
         class Work:
             def wait(self):
-                if honour:
-                    torch.cuda.current_stream().wait_event(done)
+                torch.cuda.current_stream().wait_event(done)
         return Work()
 
 

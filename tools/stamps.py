@@ -31,6 +31,7 @@ for k in range(30):
     b.step(act[k % 8])
 torch.cuda.synchronize()
 recs = []
+la_recs = []
 feats = []
 FIX = (config.FIX_LAT, config.FIX_LON)
 for k in range(5):
@@ -40,6 +41,7 @@ for k in range(5):
     b.step(act[k % 8])
     torch.cuda.synchronize()
     recs.append(st[:grid].cpu().numpy().astype(np.uint64))
+    la_recs.append(st[grid:].cpu().numpy().astype(np.uint64))
     post = {f: b.state[f].cpu().numpy() for f in ("lat", "lon", "hdg", "tas", "nav")}
     # per-lane features of this step, folded per wave (64/gs envs per wave)
     wp = np.where(((pre["nav"] >> 8) & 255) == 0, FIX[0], config.RWY_LAT)
@@ -165,3 +167,18 @@ for run in range(1, 5):
             desc.append(f"[A {(c2[w]-c1[w])/1e3:5.1f} B {(c3[w]-c2[w])/1e3:4.1f} CD1 {(c4[w]-c3[w])/1e3:4.1f} "
                         f"CD2 {(c5[w]-c4[w])/1e3:4.1f} | {' '.join(str(int(v)) for v in F[w, :5])} | cand {tot[w]}]")
         print(f"   SIMD fin {fin_us[j]:5.1f} us: " + " ".join(desc))
+
+# lookahead workgroups (E <= 2048: blockIdx >= grid), if any ran: their life against the
+# main waves' (realtime stamps, 100 MHz)
+la = np.concatenate(la_recs)
+ran = la[:, 0] != 0
+if ran.any():
+    lr0 = la[ran, 0].astype(np.int64); lr1 = la[ran, 6].astype(np.int64)
+    print("lookahead waves: n per launch", int(ran.sum()) // 5, " life (us)", pct((lr1 - lr0) * 10 / 1000 * 1000))
+    for run in range(1, 5):
+        s_ = slice(run * grid, (run + 1) * grid)
+        t0k = rt0[s_].min()
+        lm = la[run * grid:(run + 1) * grid]
+        lm = lm[lm[:, 0] != 0]
+        print(f" run {run}: main waves end {(rt1[s_].max() - t0k) * 10 / 1000:.1f} us, "
+              f"lookahead waves end {(lm[:, 6].astype(np.int64).max() - t0k) * 10 / 1000:.1f} us after the first start")
