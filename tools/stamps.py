@@ -137,7 +137,8 @@ for run in range(5):
 first_l = np.array(first_l); second_l = np.array(second_l)
 print("2-wave SIMDs:", len(first_l))
 if len(first_l) == 0:
-    sys.exit(0)
+    first_l = second_l = np.zeros(1)
+    start_gap, first_s, second_s = [0.0], [0], [0]
 print("  first-finishing wave life ns ", pct(first_l * 1000))
 print("  second-finishing wave life ns", pct(second_l * 1000))
 print("  start(second) - start(first) ns", pct(np.array(start_gap) * 1000))
