@@ -1635,6 +1635,91 @@ __device__ __forceinline__ bool vert_own_fast(AC& s, int S, double dt, Atmos* at
   return ok & (S > 0);
 }
 
+// ---- Merge ownship with the lookahead on: the substep loop for level HDG/SPD flight ------
+// With the lookahead (C4's per-GPU shards) a main wave propagates only its two ownships, and
+// their ten substeps were ~40 k of the main wave's ~58 k cycles at 512 envs
+// (profiles/r03/stamps_la512_before_fastown.txt).  After the HDG/SPD commands
+// (merge_env.py:286-293) the ownship flies without LNAV at its selected altitude, so the
+// speed target (ap_tas and the PerfModel.limits clamp) is one value for the whole step and
+// the vertical branch is never taken: this is substep<false> for exactly that case, every
+// value by the same expression in the same order, with none of substep()'s memo-key
+// branches.  The conditions it assumes (LNAV off, altitude on its selection) are checked up
+// front; the caller otherwise runs substep().  The first substep takes the general
+// pymod360 (a spawned ownship's heading is bearing - 180, possibly negative), later ones
+// the range-limited form (hdg in [0, 360)); bit-identical either way
+// (tests/test_gpu_fastpath.py against BSG_NO_FASTPATH=1, tests/test_gpu_lookahead.py
+// against the inline path).
+//   at: vatmos(alt) -- the ownship atmosphere memo's entry when its key matches
+__device__ __forceinline__ bool merge_own_fast(AC& s, int S, double dt, const Atmos& at,
+                                               double* ap_tas_out, double* allow_out) {
+  const double allow_h = s.selalt > HMAX ? HMAX : s.selalt;
+  if (!(((s.nav & 1) == 0) & (bits(s.alt) == bits(allow_h)) & (S > 0))) return false;
+  // the speed schedule at the constant altitude (substep's memo-miss path with hb == ab)
+  const bool gd = ground_phase(s.alt);
+  const double axmax = gd ? AXMAX_GD : AXMAX;
+  const double ap_tas = casormach2tas_at(s.selspd, at);
+  double allow_tas;
+  {
+    const double vmin = gd ? 0.0 : VMIN_CAS, vmax = gd ? VMAX_GD : VMAX_CAS;
+    const double intent_cas = tas2cas_at(ap_tas, at);
+    double allow_cas = intent_cas < vmin ? vmin : intent_cas;
+    allow_cas = intent_cas > vmax ? vmax : allow_cas;
+    allow_tas = cas2tas_at(allow_cas, at);
+    const double snd_h = sound_at(at);
+    if (allow_tas / snd_h > MMO) allow_tas = MMO * snd_h;
+  }
+  *ap_tas_out = ap_tas;
+  *allow_out = allow_tas;
+  const double hdg_cmd = pymod360(s.ap_trk);
+  const double adt = fabs(dt * axmax);
+  double latr = s.lat * kD2R;
+  SinCos lsc = sincos_dd(latr);
+  uint64_t hkey = kNoKey;
+  double shdg = 0.0, chdg = 0.0;
+  auto sub = [&](auto first_tag) {
+    constexpr bool F = decltype(first_tag)::value;
+    // update_airspeed
+    const double delta_spd = allow_tas - s.tas;
+    const bool need_ax = fabs(delta_spd) > adt;
+    s.ax = sgnmul(need_ax, delta_spd, axmax);
+    s.tas = need_ax ? s.tas + s.ax * dt : allow_tas;
+    // the heading (after the first substep hdg and hdg_cmd are in [0, 360]: pymod360_r is
+    // pymod360 on the arguments below)
+    const double da = hdg_cmd - s.hdg + 180.0;
+    const double delhdg = (F ? pymod360(da) : pymod360_r(da)) - 180.0;
+    bool swhdgsel = false;
+    double turnrate = 0.0;
+    if (delhdg != 0.0) {
+      turnrate = (G0 * TAN_BANKDEF / npmax(s.tas, EPS_SPD)) * kR2D;
+      swhdgsel = fabs(delhdg) > fabs(dt * turnrate);
+    }
+    const double ha = swhdgsel ? s.hdg + sgnmul(true, delhdg, dt * turnrate) : hdg_cmd;
+    s.hdg = F ? pymod360(ha) : pymod360_r(ha);
+    // the vertical speed: delta_alt = +0, so swaltsel is false and target_vs = +0
+    const double delta_vs = 0.0 - s.vs;
+    const bool need_az = fabs(delta_vs) > 300 * FPM;
+    const double az = sgnmul(need_az, delta_vs, 300 * FPM);
+    s.vs = need_az ? s.vs + az * dt : 0.0;
+    if (!isfinite(s.vs)) s.vs = 0.0;
+    // update_groundspeed + update_pos (the altitude stays allow_h)
+    if (bits(s.hdg) != hkey) {
+      sincos_t(s.hdg * kD2R, &shdg, &chdg);
+      hkey = bits(s.hdg);
+    }
+    const double gsnorth = s.tas * chdg;
+    const double gseast = s.tas * shdg;
+    s.lat = s.lat + divk_f(dt * gsnorth, Rearth) * kR2D;
+    const double nlr = s.lat * kD2R;
+    sincos_add(lsc, nlr - latr);
+    latr = nlr;
+    s.lon = s.lon + divk_f(dt * gseast / lsc.c, Rearth) * kR2D;
+  };
+  sub(std::true_type{});
+  for (int it = 1; it < S; ++it) sub(std::false_type{});
+  s.alt = allow_h;
+  return true;
+}
+
 // One RL step of aircraft (e, j) whose state is in s: the ownship's action decode (j == 0),
 // ACTION_FREQUENCY substeps with the cross-step memo, the deferred cas.  StaticObstacle also
 // evaluates its per-substep reward here (sub_reward / sub_done).
@@ -1702,6 +1787,33 @@ __device__ __forceinline__ void propagate(const KParams& p, int e, int j, size_t
     }
     // leave on a wave-uniform condition: a uniform loop below would otherwise still issue
     // every straight-line instruction of its 30 substeps with an empty exec mask
+    if (__ballot(!fast_ok) == 0) return;
+    if (fast_ok) return;
+  }
+  if constexpr (KIND == BSG_ENV_MERGE && !WIND) {
+    // the lookahead's main waves propagate only the ownships: merge_own_fast
+    bool fast_ok = false;
+    if (j == 0 && p.la && !p.no_fastpath) {
+      const bool hit = bits(oat[0]) == bits(s.alt);     // (no memo cache: oat holds no key)
+      const Atmos at = hit ? Atmos{oat[1], oat[2], oat[3]} : vatmos(s.alt);
+      const AC saved = s;
+      double ap_tas, allow_tas;
+      fast_ok = merge_own_fast(s, S, p.cfg.simdt, at, &ap_tas, &allow_tas);
+      if (fast_ok) {
+        s.cas = tas2cas_at(s.tas, at);     // memo_final_cas (the altitude did not change)
+        if (mcache) {
+          // the entries memo_store would leave: level flight, limits keyed by this state
+          const double v[MC_FIELDS] = {ap_tas, allow_tas > 0.0 ? allow_tas : key_as_double(kNoKey)};
+#pragma unroll
+          for (int f = 0; f < MC_FIELDS; ++f)
+            if (bits(mc[f]) != bits(v[f])) mcache[(size_t)f * p.E * N + a] = v[f];
+          double* t = mcache + (size_t)MC_FIELDS * p.E * N + (size_t)e * 4;
+          if (!hit) { t[0] = s.alt; t[1] = at.p; t[2] = at.rho; t[3] = at.T; }
+        }
+      } else {
+        s = saved;
+      }
+    }
     if (__ballot(!fast_ok) == 0) return;
     if (fast_ok) return;
   }

@@ -69,3 +69,41 @@ def test_vertical_ownship_fastpath_bit_identical(kind, autoreset):
         _same(_snap(gen), _snap(fast), t)
         ends += int((gen.terminated | gen.truncated).sum())
     assert ends >= E                                     # episodes ended inside the window
+
+
+@pytest.mark.parametrize("memo", [True, False])
+def test_merge_ownship_fastpath_bit_identical(memo):
+    """merge_own_fast (the lookahead's main waves: level HDG/SPD ownships) against
+    substep(): both batches run the lookahead; one with BSG_NO_FASTPATH=1.  Turns both
+    ways, speed commands into the envelope clamps, NEXT_STEP autoresets (a spawned ownship's
+    first step runs substep(): its heading is bearing - 180), and with the memo cache off."""
+    from bluesky_gym import config, core
+    cfg = config.merge_config(num_ac=32, max_episode_steps=40)
+    E = 512
+    bs = []
+    for general in (True, False):
+        old = os.environ.get("BSG_NO_FASTPATH")
+        os.environ["BSG_NO_FASTPATH"] = "1" if general else "0"
+        try:
+            bs.append(core.DeviceBatch(cfg, E, compute_cd=True, seed=8, learner=True,
+                                       memo_cache=memo, lookahead=True))
+        finally:
+            if old is None:
+                os.environ.pop("BSG_NO_FASTPATH")
+            else:
+                os.environ["BSG_NO_FASTPATH"] = old
+    gen, fast = bs
+    assert gen.lookahead and fast.lookahead
+    g = torch.Generator(device="cuda").manual_seed(6)
+    gen.reset()
+    fast.reset()
+    ends = 0
+    for t in range(120):
+        a = torch.rand((E, 2), dtype=torch.float64, device="cuda", generator=g) * 2.4 - 1.2
+        a = a.clamp(-1, 1)
+        a[::5] = 0.0                                     # straight and steady: no turn, no speed change
+        gen.step(a)
+        fast.step(a)
+        _same(_snap(gen), _snap(fast), t)
+        ends += int((gen.terminated | gen.truncated).sum())
+    assert ends >= 2 * E
