@@ -1862,11 +1862,16 @@ __device__ __forceinline__ void propagate(const KParams& p, int e, int j, size_t
       // results.
       const int slot = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (3 << 11)) & 15;  // HW_ID wave id
       // switch point: 3/4 of the substeps at two full-propagation waves per SIMD (4096
-      // envs: 1/2, 2/3, 4/5, 9/10 measured slower), 2/3 with the lookahead (2,048 envs:
-      // -1.8 %, profiles/r03/ab_prio_balance.txt); set per launch (launch_kind_w)
+      // envs: 1/2, 2/3, 4/5, 9/10 measured slower; profiles/r03/ab_prio_balance.txt); set per
+      // launch (launch_kind_w)
+      // With the lookahead on, the waves that run this loop are the lookahead waves (the main
+      // waves' ownships take merge_own_fast): they end a shard's launch, so they run at the
+      // top priority over the main and CD helper waves they share SIMDs with (512 / 1,024 /
+      // 2,048 envs: -2 / -1 / -3 %, profiles/r03/ab29.txt).
       const int sw = (p.prio_sw_num * S + p.prio_sw_den - 1) / p.prio_sw_den;
       for (int it = 0; it < S; ++it) {
-        if ((slot & 1) ? (it < sw) : (it >= sw)) __builtin_amdgcn_s_setprio(1);
+        if (p.la) __builtin_amdgcn_s_setprio(3);
+        else if ((slot & 1) ? (it < sw) : (it >= sw)) __builtin_amdgcn_s_setprio(1);
         else __builtin_amdgcn_s_setprio(0);
         substep<WIND, KIND != BSG_ENV_MERGE>(s, m, dt, rt, p.wind, it == 0 ? fh0 : trk_ok);
       }
@@ -1935,34 +1940,41 @@ __device__ __forceinline__ void lookahead_role(const KParams& p) {
   const size_t a = (size_t)e * N + j;
   double* memo = p.la + 2 * LA_F * EN;
   uint64_t* tags = reinterpret_cast<uint64_t*>(p.la + (2 * LA_F + MC_FIELDS) * EN);
+  // every read of the common case is issued here, before any decision needs it, so the
+  // wave pays one memory round trip instead of three (env scalars -> slot tag -> state):
+  // the env scalars, the slot's tag and entry, the state (selspd / selalt / selvs) and the
+  // lookahead memo entries
   EnvScalars ev = {};
   load_env(b, e, ev);
+  const double* rslot = p.la + (size_t)p.la_par * LA_F * EN;
+  const uint64_t tag_in = p.mode == MODE_STEP ? tags[(size_t)p.la_par * p.E + e] : 0;
+  AC s = {};
+  load_ac<false>(b, a, s);
+  AC s_slot = s;
+  if (p.mode == MODE_STEP) la_load(rslot, a, EN, s_slot);
+  double mc[MC_FIELDS];
+  memo_fetch(mc, memo, a, EN);
   bool resetting;
   if (p.mode == MODE_RESET) resetting = p.env_mask ? (p.env_mask[e] != 0) : true;
   else resetting = (p.cfg.autoreset_mode == BSG_AUTORESET_NEXT_STEP) && (ev.flags & 1);
   if (!resetting && p.mode != MODE_STEP) return;            // untouched by a masked reset
   const double act[2] = {0.0, 0.0};
   const double oat[4] = {0.0, 0.0, 0.0, 0.0};
-  double mc[MC_FIELDS];
   double sub_reward = 0.0;
   bool sub_done = false;
-  AC s = {};
   uint64_t tag_out;
   if (resetting) {
     double aux[4] = {ev.target_alt, 0.0, 0.0, 0.0};
+    s = AC{};
     spawn<KIND>(p, e, j, ev.episode, s, aux, false);
     memo_invalidate(memo, a, EN);
 #pragma unroll
     for (int f = 0; f < MC_FIELDS; ++f) mc[f] = key_as_double(kNoKey);
     tag_out = la_tag(ev.episode + 1u, 0, p.la_gen);
   } else {
-    const double* rslot = p.la + (size_t)p.la_par * LA_F * EN;
-    if (tags[(size_t)p.la_par * p.E + e] == la_tag(ev.episode, ev.step_count, p.la_gen)) {
-      load_ac<false>(b, a, s);                   // selspd / selalt / selvs
-      la_load(rslot, a, EN, s);
-      memo_fetch(mc, memo, a, EN);
+    if (tag_in == la_tag(ev.episode, ev.step_count, p.la_gen)) {
+      s = s_slot;
     } else {
-      load_ac<false>(b, a, s);
       memo_invalidate(memo, a, EN);
 #pragma unroll
       for (int f = 0; f < MC_FIELDS; ++f) mc[f] = key_as_double(kNoKey);
@@ -2465,8 +2477,8 @@ static hipError_t launch_kind_w(const KParams& p0, hipStream_t st) {
   KParams p = p0;
   p.la_grid0 = grid0;
   if (!(KIND == BSG_ENV_MERGE && !WIND)) p.la = nullptr;
-  p.prio_sw_num = p.la ? 2 : 3;
-  p.prio_sw_den = p.la ? 3 : 4;
+  p.prio_sw_num = 3;                         // (the lookahead's waves: fixed priority)
+  p.prio_sw_den = 4;
   const int grid = p.la ? 2 * grid0 : grid0;
 #define BSG_CASE(G) \
   case G: hipLaunchKernelGGL((step_kernel<KIND, G, WIND>), dim3(grid), dim3(64), p.lds_pad, st, p); break;
