@@ -28,7 +28,7 @@ class DeviceBatch:
     def __init__(self, cfg: EnvKindConfig, num_envs: int, *, autoreset=nat.AUTORESET_NEXT_STEP,
                  compute_cd=True, seed=0, device=None, learner=False, env_offset=0,
                  memo_cache=True, lookahead=None):
-        """lookahead: propagate Merge's intruders one RL step ahead in extra workgroups
+        """lookahead: propagate the intruders (Merge, Vertical) one RL step ahead in extra workgroups
         (bsg_set_lookahead; bit-identical results).  None = on where the library supports
         it and the batch is small enough to leave SIMDs idle (LOOKAHEAD_MAX_ENVS); True /
         False force it."""
@@ -72,7 +72,8 @@ class DeviceBatch:
                                                  nbytes), "bsg_set_lookahead")
             self.lookahead = True
         elif lookahead:
-            raise nat.BsgError("lookahead: MergeEnv with NEXT_STEP (or no) autoreset only")
+            raise nat.BsgError("lookahead: MergeEnv / VerticalCREnv with NEXT_STEP (or no) "
+                               "autoreset only")
 
     # ------------------------------------------------------------------ buffers
     def _alloc(self):

@@ -392,7 +392,8 @@ int32_t bsg_bind(bsg_ctx* c, const bsg_buffers* b) {
 
 int64_t bsg_lookahead_bytes(const bsg_ctx* c) {
   if (!c) return fail(BSG_E_INVALID_ARG, "bsg_lookahead_bytes: null ctx%s%lld");
-  if (c->cfg.env_kind != BSG_ENV_MERGE || c->cfg.autoreset_mode == BSG_AUTORESET_SAME_STEP)
+  if ((c->cfg.env_kind != BSG_ENV_MERGE && c->cfg.env_kind != BSG_ENV_VERTICAL_CR) ||
+      c->cfg.autoreset_mode == BSG_AUTORESET_SAME_STEP)
     return 0;
   return (int64_t)la_bytes(c->cfg);
 }
@@ -401,8 +402,8 @@ int32_t bsg_set_lookahead(bsg_ctx* c, void* scratch, int64_t bytes) {
   if (!c) return fail(BSG_E_INVALID_ARG, "bsg_set_lookahead: null ctx%s%lld");
   if (scratch) {
     if (bsg_lookahead_bytes(c) == 0)
-      return fail(BSG_E_UNSUPPORTED, "bsg_set_lookahead: MergeEnv with NEXT_STEP or no autoreset "
-                  "only%s%lld");
+      return fail(BSG_E_UNSUPPORTED, "bsg_set_lookahead: MergeEnv / VerticalCREnv with NEXT_STEP "
+                  "or no autoreset only%s%lld");
     if (bytes < (int64_t)la_bytes(c->cfg))
       return fail(BSG_E_INVALID_ARG, "bsg_set_lookahead: scratch too small%s (need %lld bytes)", "",
                   (long long)la_bytes(c->cfg));

@@ -1758,11 +1758,12 @@ __device__ __forceinline__ void propagate(const KParams& p, int e, int j, size_t
     }
   }
   const int S = p.cfg.action_frequency;
-  // (Vertical's intruders would run substep() after the ownship's loop in the same wave:
-  // the union measured slower than substep() alone, 121.7 against 90.6 us at 2,048 envs)
-  if constexpr (KIND == BSG_ENV_DESCENT && !WIND) {
+  // Vertical: only with the lookahead, whose main waves propagate the ownships alone (inline,
+  // the intruders would run substep() after the ownship's loop in the same wave: the union
+  // measured slower than substep() alone, 121.7 against 90.6 us at 2,048 envs)
+  if constexpr ((KIND == BSG_ENV_DESCENT || KIND == BSG_ENV_VERTICAL_CR) && !WIND) {
     bool fast_ok = false;
-    if (j == 0 && S > 0 && !p.no_fastpath) {
+    if (j == 0 && S > 0 && !p.no_fastpath && (KIND == BSG_ENV_DESCENT || p.la)) {
       const AC saved = s;
       Atmos at;
       double alt_last;
@@ -2006,7 +2007,7 @@ __global__ __launch_bounds__(64 * CDW) BSG_WPE void step_kernel(KParams p) {
   BSG_STAMP(0, __builtin_amdgcn_s_memrealtime());
   BSG_STAMP(1, stamp_clock());
 #endif
-  constexpr bool kLA = KIND == BSG_ENV_MERGE && !WIND;
+  constexpr bool kLA = (KIND == BSG_ENV_MERGE || KIND == BSG_ENV_VERTICAL_CR) && !WIND;
   if constexpr (kLA) {
     if (p.la && (int)blockIdx.x >= p.la_grid0) {
       lookahead_role<KIND, GS, WIND>(p);
@@ -2476,7 +2477,7 @@ static hipError_t launch_kind_w(const KParams& p0, hipStream_t st) {
   const int grid0 = (p0.E + epb - 1) / epb;
   KParams p = p0;
   p.la_grid0 = grid0;
-  if (!(KIND == BSG_ENV_MERGE && !WIND)) p.la = nullptr;
+  if (!((KIND == BSG_ENV_MERGE || KIND == BSG_ENV_VERTICAL_CR) && !WIND)) p.la = nullptr;
   p.prio_sw_num = 3;                         // (the lookahead's waves: fixed priority)
   p.prio_sw_den = 4;
   const int grid = p.la ? 2 * grid0 : grid0;

@@ -220,9 +220,10 @@ int32_t bsg_bind(bsg_ctx* ctx, const bsg_buffers* bufs);
  * stable_baselines3 common/vec_env/subproc_vec_env.py). */
 int32_t bsg_set_learner(bsg_ctx* ctx, float* learner_rows);
 
-/* Lookahead (MergeEnv-v0 only; NEXT_STEP or no autoreset; inactive while a wind field is
- * set).  Merge's intruders fly their LNAV route independently of the ownship and the
- * action (merge_env.py:155-157, RESO OFF), so with a caller-owned scratch of
+/* Lookahead (MergeEnv-v0 and VerticalCREnv-v0; NEXT_STEP or no autoreset; inactive while a
+ * wind field is set).  Merge's intruders fly their LNAV route, Vertical's their creconfs
+ * straight line, independently of the ownship and the action (merge_env.py:155-157,
+ * vertical_cr_env.py:183-200; RESO OFF), so with a caller-owned scratch of
  * bsg_lookahead_bytes() bytes bound, every launch also propagates the intruders one RL
  * step ahead in extra workgroups, and the next step consumes that state instead of
  * integrating the intruders on its critical path.  Results are bit-identical to the
@@ -230,7 +231,8 @@ int32_t bsg_set_learner(bsg_ctx* ctx, float* learner_rows);
  * bsg_set_lookahead(ctx, NULL, 0) turns it off.  Binding, a wind change or calling
  * bsg_set_lookahead again restarts it from the state buffers (call it again after
  * writing aircraft state directly, as for memo_cache).  Replaces nothing in the reference
- * (a scheduling device: merge_env.py:136-137 runs the substeps of all aircraft). */
+ * (a scheduling device: merge_env.py:136-137 / vertical_cr_env.py:287-289 run the substeps of
+ * all aircraft). */
 int64_t bsg_lookahead_bytes(const bsg_ctx* ctx);
 int32_t bsg_set_lookahead(bsg_ctx* ctx, void* scratch, int64_t bytes);
 

@@ -1,6 +1,7 @@
-"""The Merge lookahead (bsg_set_lookahead; csrc/bsg_kernels.hip lookahead_role): extra
-workgroups propagate the intruders one RL step ahead (their LNAV flight does not depend
-on the ownship or the action, merge_env.py:155-157) and the next step consumes that state.
+"""The lookahead (bsg_set_lookahead; csrc/bsg_kernels.hip lookahead_role): extra
+workgroups propagate the intruders one RL step ahead (Merge's LNAV flight and Vertical's
+creconfs straight lines do not depend on the ownship or the action, merge_env.py:155-157,
+vertical_cr_env.py:183-200) and the next step consumes that state.
 It must be invisible: every output and every state buffer bit-identical to the inline
 path, step by step, through NEXT_STEP autoresets, explicit masked resets, host-supplied
 spawn rows, a direct state write (invalidate_caches) and turning it off and on."""
@@ -14,10 +15,11 @@ OUTS = ("obs", "reward", "terminated", "truncated", "topk", "intr_mask", "conf_m
         "los_mask", "tcpamax", "min_sep", "ep_info", "learner")
 
 
-def _batch(E, N, la, seed=5, maxep=20):
+def _batch(E, N, la, seed=5, maxep=20, kind="merge"):
     from bluesky_gym import config, core
-    return core.DeviceBatch(config.merge_config(num_ac=N, max_episode_steps=maxep), E,
-                            compute_cd=True, seed=seed, learner=True, lookahead=la)
+    cfg = (config.merge_config(num_ac=N, max_episode_steps=maxep) if kind == "merge" else
+           config.vertical_config(num_intruders=N - 1, max_episode_steps=maxep))
+    return core.DeviceBatch(cfg, E, compute_cd=True, seed=seed, learner=True, lookahead=la)
 
 
 def _snap(b):
@@ -40,9 +42,12 @@ def _same(x, y, t):
             raise AssertionError(f"step {t}: {k} differs at {idx}")
 
 
-@pytest.mark.parametrize("E,N", [(512, 32), (100, 20), (256, 16)])
-def test_lookahead_bit_identical_to_inline(E, N):
-    ref, la = _batch(E, N, False), _batch(E, N, True)
+@pytest.mark.parametrize("kind,E,N", [("merge", 512, 32), ("merge", 100, 20), ("merge", 256, 16),
+                                      ("vertical", 512, 32), ("vertical", 100, 6)])
+def test_lookahead_bit_identical_to_inline(kind, E, N):
+    """Vertical's main waves also run the ownship's fast loop (vert_own_fast) under the
+    lookahead: compared here with the inline general substep()."""
+    ref, la = _batch(E, N, False, kind=kind), _batch(E, N, True, kind=kind)
     assert la.lookahead and not ref.lookahead
     g = torch.Generator(device="cuda").manual_seed(2)
     ref.reset()
@@ -50,7 +55,7 @@ def test_lookahead_bit_identical_to_inline(E, N):
     _same(_snap(ref), _snap(la), -1)
     dones = 0
     for t in range(90):
-        a = torch.rand((E, 2), dtype=torch.float64, device="cuda", generator=g) * 2 - 1
+        a = torch.rand((E, la.act_dim), dtype=torch.float64, device="cuda", generator=g) * 2 - 1
         ref.step(a)
         la.step(a)
         _same(_snap(ref), _snap(la), t)
@@ -68,25 +73,27 @@ def test_lookahead_bit_identical_to_inline(E, N):
     assert dones >= E * 3                               # autoresets in the window
 
 
-def test_lookahead_with_host_spawn_rows_and_toggle():
+@pytest.mark.parametrize("kind", ["merge", "vertical"])
+def test_lookahead_with_host_spawn_rows_and_toggle(kind):
     """Parity mode (host spawn rows for the NEXT_STEP resets) and switching the lookahead
     off and on mid-run keep the outputs bit-identical."""
     import ctypes as C
     from bluesky_gym import _native as nat
-    from bluesky_gym.spawn import merge_spawn
+    from bluesky_gym.spawn import merge_spawn, vertical_spawn
     E, N = 128, 32
-    ref, la = _batch(E, N, False, seed=9), _batch(E, N, True, seed=9)
+    ref, la = _batch(E, N, False, seed=9, kind=kind), _batch(E, N, True, seed=9, kind=kind)
     rs = np.random.RandomState(4)
     g = torch.Generator(device="cuda").manual_seed(8)
 
     def rows():
-        return torch.from_numpy(np.stack([merge_spawn(N, rs) for _ in range(E)])).cuda()
+        one = (lambda: merge_spawn(N, rs)) if kind == "merge" else (lambda: vertical_spawn(N - 1, rs))
+        return torch.from_numpy(np.stack([one() for _ in range(E)])).cuda()
 
     sp = rows()
     ref.reset(spawn=sp)
     la.reset(spawn=sp)
     for t in range(70):
-        a = torch.rand((E, 2), dtype=torch.float64, device="cuda", generator=g) * 2 - 1
+        a = torch.rand((E, la.act_dim), dtype=torch.float64, device="cuda", generator=g) * 2 - 1
         sp = rows()
         ref.step(a, spawn=sp)
         la.step(a, spawn=sp)
@@ -101,7 +108,10 @@ def test_lookahead_with_host_spawn_rows_and_toggle():
 def test_lookahead_refused_where_unsupported():
     from bluesky_gym import _native as nat, config, core
     with pytest.raises(nat.BsgError):
-        core.DeviceBatch(config.vertical_config(), 64, lookahead=True)
+        core.DeviceBatch(config.descent_config(), 64, lookahead=True)
+    with pytest.raises(nat.BsgError):
+        core.DeviceBatch(config.vertical_config(), 64, autoreset=nat.AUTORESET_SAME_STEP,
+                         lookahead=True)
     with pytest.raises(nat.BsgError):
         core.DeviceBatch(config.merge_config(num_ac=16), 64,
                          autoreset=nat.AUTORESET_SAME_STEP, lookahead=True)

@@ -51,6 +51,10 @@ for spec in [
     ("merge32_full_1024_nola", config.merge_config(num_ac=32), 1024, True, False),
     ("merge32_full_2048_nola", config.merge_config(num_ac=32), 2048, True, False),
     ("merge32_full_la", config.merge_config(num_ac=32), 4096, True, True),
+    # Vertical (C3) with the lookahead forced off (DeviceBatch's default: on up to 2048 envs)
+    ("vert32_full_2048_nola", config.vertical_config(num_intruders=31), 2048, True, False),
+    ("vert32_full_1024", config.vertical_config(num_intruders=31), 1024, True),
+    ("vert32_full_1024_nola", config.vertical_config(num_intruders=31), 1024, True, False),
 ]:
     name, cfg, E, cd = spec[:4]
     la = spec[4] if len(spec) > 4 else None

@@ -16,7 +16,10 @@ from bluesky_gym import _native as nat
 
 E = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
 N = int(sys.argv[2]) if len(sys.argv) > 2 else 32
-b = core.DeviceBatch(config.merge_config(num_ac=N), E, compute_cd=True, seed=1234)
+KIND = os.environ.get("STAMPS_KIND", "merge")      # merge | vertical
+cfg = (config.merge_config(num_ac=N) if KIND == "merge"
+       else config.vertical_config(num_intruders=N - 1))
+b = core.DeviceBatch(cfg, E, compute_cd=True, seed=1234)
 b.reset()
 gs = 1
 while gs < N:
@@ -26,7 +29,7 @@ grid = (E + 64 // gs - 1) // (64 // gs)
 # slots 0-1 before they branch off; their rows are ignored below)
 st = torch.zeros((2 * grid, 8), dtype=torch.int64, device="cuda")
 nat.check(b.lib.bsg_set_stamps(b._ctx, C.c_void_p(st.data_ptr())), "bsg_set_stamps")
-act = torch.rand((8, E, 2), dtype=torch.float64, device="cuda") * 2 - 1
+act = torch.rand((8, E, b.act_dim), dtype=torch.float64, device="cuda") * 2 - 1
 for k in range(30):
     b.step(act[k % 8])
 torch.cuda.synchronize()
