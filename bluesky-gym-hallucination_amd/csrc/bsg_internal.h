@@ -36,12 +36,15 @@ struct WindDev {
 };
 
 // Lookahead scratch layout (bsg_set_lookahead; bsg_kernels.hip lookahead_role), in doubles
-// for EN = E*N: two slots of LA_F fields x EN, the lookahead blocks' memo [LA_MC][EN], two
-// tag rows [E] (u64).
-constexpr int LA_F = 10;
+// for EN = E*N: two slots of LA_F fields x EN (LA_STATE state fields, then -- Vertical, la_cd
+// -- the intruder pairs' StateBased rows as u64 bits: conflict row, LoS row, tcpamax), the
+// lookahead blocks' memo [LA_MC][EN], two tag rows [E] (u64), two rows [E] of the intruder
+// pairs' minimum separation (bits of a double).
+constexpr int LA_STATE = 10;
+constexpr int LA_F = LA_STATE + 3;
 constexpr int LA_MC = 2;           // = MC_FIELDS (bsg_kernels.hip)
 __host__ __device__ constexpr size_t la_doubles(size_t E, size_t N) {
-  return (2 * LA_F + LA_MC) * E * N + 2 * E;
+  return (2 * LA_F + LA_MC) * E * N + 4 * E;
 }
 
 // Passed by value to every launch (kernarg segment).
@@ -69,6 +72,8 @@ struct KParams {
                              // (tests compare the specialised paths against it)
   RouteTrig route_t;         // (last: see RouteTrig)
   int prio_sw_num, prio_sw_den;  // substep priority switch point (set by the launcher)
+  int la_cd;                 // the lookahead waves also run the intruder pairs' StateBased CD
+                             // (set by the launcher: VerticalCREnv with compute_cd)
 };
 
 hipError_t launch_step(const KParams& p, hipStream_t stream);

@@ -642,6 +642,7 @@ struct Lds : LdsWind<WIND> {
   // longitude in deg, StateBased velocity components
   float4 fpk[64];                  // (lat rad, lon deg, u, v): one ds_read_b128 per pair
   int done[64];
+  int cdsel[64];                   // [g]: which pairs of env group g the CD runs (cd_pairs)
   // StateBased assembly (LDS atomics)
   unsigned long long cm[64], lm[64], tmax[64], gmin[64];
 };
@@ -830,6 +831,109 @@ __device__ __forceinline__ void cd_pair2(const LT& L, int i, int k, CdOut* rik, 
   // the sign of a zero)
   *rki = cd_order((lati - latk) * kD2R, dlon_ki, cavelat, cd_u(L, i) - cd_u(L, k),
                   cd_v(L, i) - cd_v(L, k), dv2, vrel, horizon, alti - altk + 0.0, vsi - vsk);
+}
+
+// The StateBased pairs of one env group that a cd_pairs call covers:
+//   CD_ALL  every unordered pair of its nac aircraft;
+//   CD_OWN  the pairs with aircraft 0 only (the intruder pairs' rows came with the
+//           lookahead slot: Vertical's intruders do not depend on the ownship);
+//   CD_INTR the pairs without aircraft 0 (the lookahead waves, one RL step ahead);
+//   CD_NONE none.
+enum { CD_ALL = 0, CD_OWN = 1, CD_INTR = 2, CD_NONE = 3 };
+
+// offsets 1..n_sft(i, M) of member i on a ring of M members: each unordered pair once, the
+// count balanced (M odd: (M-1)/2 each; M even: M/2 for the first half, M/2 - 1 after)
+__device__ __forceinline__ int ring_sft(int i, int M) {
+  return (M & 1) ? M / 2 : (i < M / 2 ? M / 2 : M / 2 - 1);
+}
+
+// StateBased.detect over the pairs `sel` selects, wave-compacted (oracle: statebased_detect;
+// see cd_candidate_f / cd_pair2).  Phase 1 tests candidate pairs (no transcendentals); phase 2
+// runs the exact arithmetic on the survivors from a dense per-wave LDS work list, both
+// orders of a pair per lane, and assembles the row masks / tcpamax / per-env min separation
+// with LDS atomics (order-independent: or / u64 max of positive doubles / min).  The caller
+// initialises L.cm / L.lm / L.tmax / L.gmin and staged L before the call, ahead of a
+// barrier; the rows are final after it returns (its last barrier).  Every lane of every wave
+// of the workgroup calls it (two barriers).  Pair (i, k) is tested on lane i; the candidate
+// bound and cd_pair2 are symmetric in the pair bit for bit, so which lane takes a pair
+// never changes a result.
+template <int GS, int CDW, class LT>
+__device__ __forceinline__ void cd_pairs(LT& L, unsigned short* cd_list, int lane, int wv, int j,
+                                         int base, int nac, bool cd_on, int sel,
+                                         unsigned long long* st4 = nullptr) {
+  // ring of member lanes r0..nac-1 (ring index i = j - r0); this lane's offsets lo..hi
+  int r0 = 0, M = nac, lo = 1, hi = 0;
+  if (cd_on) {
+    if (sel == CD_ALL) {
+      hi = ring_sft(j, nac);
+    } else if (sel == CD_INTR) {
+      if (j > 0) { r0 = 1; M = nac - 1; hi = ring_sft(j - 1, M); }
+    } else if (sel == CD_OWN) {
+      if (j > 0) { lo = nac - j; hi = lo; }          // (j, j + nac - j mod nac) = (j, 0)
+    }
+  }
+  uint64_t mine = 0;                   // bit sft - lo: pair (j, member at ring offset sft)
+  {
+    const float4 pi = L.fpk[lane];
+    const float flati = pi.x, floni = pi.y, fui = pi.z, fvi = pi.w;
+    const float fali = fabsf(flati);
+    // loads and tests only (unrolled so the LDS reads of several offsets are in flight
+    // together); helper waves (wv > 0) take every CDW-th offset
+#pragma unroll 4
+    for (int sft = lo + wv; sft <= hi; sft += CDW) {
+      int k = j - r0 + sft;
+      if (k >= M) k -= M;
+      const float4 pk = L.fpk[base + r0 + k];
+      const float dlat = fabsf(pk.x - flati);
+      float dl = fabsf(pk.y - floni);
+      dl = dl > 180.0f ? 360.0f - dl : dl;
+      const float x = fmaxf(fali, fabsf(pk.x));
+      const float du = pk.z - fui, dv = pk.w - fvi;
+      if (cd_candidate_f(dlat, dl, x, du * du + dv * dv)) mine |= 1ull << (sft - lo);
+    }
+  }
+  // work list of the candidate pairs: exclusive prefix sum of the per-lane counts (< 64)
+  // from one ballot per bit -- each lane counts the set bits below it (mbcnt), no cross-lane
+  // data movement
+  const int cnt = __popcll(mine);
+  int pos = 0, total = 0;
+#pragma unroll
+  for (int bit = 0; bit < 7; ++bit) {
+    const uint64_t bm = __ballot((cnt >> bit) & 1);
+    pos += (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32),
+                                          __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u)) << bit;
+    total += __popcll(bm) << bit;
+  }
+  for (uint64_t c = mine; c; c &= c - 1) {
+    int k = j - r0 + lo + __builtin_ctzll(c);
+    if (k >= M) k -= M;
+    cd_list[pos++] = (unsigned short)((lane << 6) | (base + r0 + k));
+  }
+  __syncthreads();
+  if (st4 && threadIdx.x == 0) {         // diagnostic stamps (tools/stamps.py): phase-1 end
+    __builtin_amdgcn_sched_barrier(0);
+    *st4 = __builtin_amdgcn_s_memtime() | ((unsigned long long)total << 48);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  // phase 2: dense exact StateBased over the surviving pairs, both orders per lane
+  for (int t = lane; t < total; t += 64) {
+    const int pr = cd_list[t];
+    const int li = pr >> 6, lk = pr & 63;
+    CdOut r[2];
+    cd_pair2(L, li, lk, &r[0], &r[1]);
+    const int gb = (li / GS) * GS;
+#pragma unroll
+    for (int o = 0; o < 2; ++o) {
+      const int row = o ? lk : li, col = (o ? li : lk) - gb;
+      if (r[o].inside) {
+        atomicMin(&L.gmin[li / GS], bits(r[o].dist));
+        if (r[o].confl) atomicOr(&L.cm[row], 1ull << col);
+        if (r[o].lossep) atomicOr(&L.lm[row], 1ull << col);
+        if (r[o].confl && r[o].tcpa > 0.0) atomicMax(&L.tmax[row], bits(r[o].tcpa));
+      }
+    }
+  }
+  __syncthreads();
 }
 
 template <int GS>
@@ -1928,66 +2032,94 @@ __device__ __forceinline__ void la_store(double* slot, size_t a, size_t EN, cons
 // slot the main workgroups read (valid tag), or -- priming, after the scratch was (re)bound
 // -- this launch's step computed here too; then one more step into the other slot (a reset
 // launch writes the slot the next step reads).
-template <int KIND, int GS, bool WIND>
-__device__ __forceinline__ void lookahead_role(const KParams& p) {
-  if (threadIdx.x >= 64) return;
+template <int KIND, int GS, bool WIND, int CDW, class LT>
+__device__ __forceinline__ void lookahead_role(const KParams& p, LT& L, unsigned short* cd_lists) {
+  if (threadIdx.x >= 64) return;              // (la_cd: Vertical, one wave per workgroup)
   const int lane = threadIdx.x;
   const int g = lane / GS, j = lane % GS;
   const int e = ((int)blockIdx.x - p.la_grid0) * (64 / GS) + g;
   const int N = p.N;
-  if (e >= p.E || j == 0 || j >= N) return;
   const Buffers& b = p.b;
   const size_t EN = (size_t)p.E * N;
   const size_t a = (size_t)e * N + j;
   double* memo = p.la + 2 * LA_F * EN;
   uint64_t* tags = reinterpret_cast<uint64_t*>(p.la + (2 * LA_F + MC_FIELDS) * EN);
-  // every read of the common case is issued here, before any decision needs it, so the
-  // wave pays one memory round trip instead of three (env scalars -> slot tag -> state):
-  // the env scalars, the slot's tag and entry, the state (selspd / selalt / selvs) and the
-  // lookahead memo entries
-  EnvScalars ev = {};
-  load_env(b, e, ev);
-  const double* rslot = p.la + (size_t)p.la_par * LA_F * EN;
-  const uint64_t tag_in = p.mode == MODE_STEP ? tags[(size_t)p.la_par * p.E + e] : 0;
-  AC s = {};
-  load_ac<false>(b, a, s);
-  AC s_slot = s;
-  if (p.mode == MODE_STEP) la_load(rslot, a, EN, s_slot);
-  double mc[MC_FIELDS];
-  memo_fetch(mc, memo, a, EN);
-  bool resetting;
-  if (p.mode == MODE_RESET) resetting = p.env_mask ? (p.env_mask[e] != 0) : true;
-  else resetting = (p.cfg.autoreset_mode == BSG_AUTORESET_NEXT_STEP) && (ev.flags & 1);
-  if (!resetting && p.mode != MODE_STEP) return;            // untouched by a masked reset
-  const double act[2] = {0.0, 0.0};
-  const double oat[4] = {0.0, 0.0, 0.0, 0.0};
-  double sub_reward = 0.0;
-  bool sub_done = false;
-  uint64_t tag_out;
-  if (resetting) {
-    double aux[4] = {ev.target_alt, 0.0, 0.0, 0.0};
-    s = AC{};
-    spawn<KIND>(p, e, j, ev.episode, s, aux, false);
-    memo_invalidate(memo, a, EN);
-#pragma unroll
-    for (int f = 0; f < MC_FIELDS; ++f) mc[f] = key_as_double(kNoKey);
-    tag_out = la_tag(ev.episode + 1u, 0, p.la_gen);
-  } else {
-    if (tag_in == la_tag(ev.episode, ev.step_count, p.la_gen)) {
-      s = s_slot;
-    } else {
-      memo_invalidate(memo, a, EN);
-#pragma unroll
-      for (int f = 0; f < MC_FIELDS; ++f) mc[f] = key_as_double(kNoKey);
-      propagate<KIND, WIND>(p, e, j, a, s, ev, sub_reward, sub_done, act, mc, oat, memo);
-      memo_fetch(mc, memo, a, EN);
-    }
-    tag_out = la_tag(ev.episode, ev.step_count + 1, p.la_gen);
-  }
-  propagate<KIND, WIND>(p, e, j, a, s, ev, sub_reward, sub_done, act, mc, oat, memo);
   const int wslot = p.mode == MODE_STEP ? 1 - p.la_par : p.la_par;
-  la_store(p.la + (size_t)wslot * LA_F * EN, a, EN, s);
-  if (j == 1) tags[(size_t)wslot * p.E + e] = tag_out;
+  // this lane propagates intruder (e, j) (and, with la_cd, takes part in its env's pairs)
+  bool run = e < p.E && j > 0 && j < N;
+  AC s = {};
+  if (run) {
+    // every read of the common case is issued here, before any decision needs it, so the
+    // wave pays one memory round trip instead of three (env scalars -> slot tag -> state):
+    // the env scalars, the slot's tag and entry, the state (selspd / selalt / selvs) and the
+    // lookahead memo entries
+    EnvScalars ev = {};
+    load_env(b, e, ev);
+    const double* rslot = p.la + (size_t)p.la_par * LA_F * EN;
+    const uint64_t tag_in = p.mode == MODE_STEP ? tags[(size_t)p.la_par * p.E + e] : 0;
+    load_ac<false>(b, a, s);
+    AC s_slot = s;
+    if (p.mode == MODE_STEP) la_load(rslot, a, EN, s_slot);
+    double mc[MC_FIELDS];
+    memo_fetch(mc, memo, a, EN);
+    bool resetting;
+    if (p.mode == MODE_RESET) resetting = p.env_mask ? (p.env_mask[e] != 0) : true;
+    else resetting = (p.cfg.autoreset_mode == BSG_AUTORESET_NEXT_STEP) && (ev.flags & 1);
+    run = resetting || p.mode == MODE_STEP;               // untouched by a masked reset
+    if (run) {
+      const double act[2] = {0.0, 0.0};
+      const double oat[4] = {0.0, 0.0, 0.0, 0.0};
+      double sub_reward = 0.0;
+      bool sub_done = false;
+      uint64_t tag_out;
+      if (resetting) {
+        double aux[4] = {ev.target_alt, 0.0, 0.0, 0.0};
+        s = AC{};
+        spawn<KIND>(p, e, j, ev.episode, s, aux, false);
+        memo_invalidate(memo, a, EN);
+#pragma unroll
+        for (int f = 0; f < MC_FIELDS; ++f) mc[f] = key_as_double(kNoKey);
+        tag_out = la_tag(ev.episode + 1u, 0, p.la_gen);
+      } else {
+        if (tag_in == la_tag(ev.episode, ev.step_count, p.la_gen)) {
+          s = s_slot;
+        } else {
+          memo_invalidate(memo, a, EN);
+#pragma unroll
+          for (int f = 0; f < MC_FIELDS; ++f) mc[f] = key_as_double(kNoKey);
+          propagate<KIND, WIND>(p, e, j, a, s, ev, sub_reward, sub_done, act, mc, oat, memo);
+          memo_fetch(mc, memo, a, EN);
+        }
+        tag_out = la_tag(ev.episode, ev.step_count + 1, p.la_gen);
+      }
+      propagate<KIND, WIND>(p, e, j, a, s, ev, sub_reward, sub_done, act, mc, oat, memo);
+      la_store(p.la + (size_t)wslot * LA_F * EN, a, EN, s);
+      if (j == 1) tags[(size_t)wslot * p.E + e] = tag_out;
+    }
+  }
+  if (!p.la_cd) return;
+  // The intruder pairs' StateBased rows of the state just stored (the next launch's), for
+  // the main waves that take this slot (cd_pairs CD_OWN adds the ownship's pairs)
+  if (run) stage(L, lane, s);
+  if (j == 1) L.cdsel[g] = run ? CD_INTR : CD_NONE;     // every group has a lane j == 1
+  L.cm[lane] = 0ull;
+  L.lm[lane] = 0ull;
+  L.tmax[lane] = 0ull;                                   // bits of +0.0
+  if (j == 0) L.gmin[g] = bits(__builtin_inf());
+  __syncthreads();
+  const bool cd_on = L.cdsel[g] == CD_INTR && j < N;
+  constexpr int kList = 64 * (GS > 1 ? GS - 1 : 1);
+  cd_pairs<GS, 1>(L, cd_lists, lane, 0, j, g * GS, N, cd_on, CD_INTR);
+  if (run) {
+    double* slot = p.la + (size_t)wslot * LA_F * EN;
+    slot[(size_t)LA_STATE * EN + a] = __longlong_as_double((long long)L.cm[lane]);
+    slot[(size_t)(LA_STATE + 1) * EN + a] = __longlong_as_double((long long)L.lm[lane]);
+    slot[(size_t)(LA_STATE + 2) * EN + a] = __longlong_as_double((long long)L.tmax[lane]);
+    if (j == 1)
+      p.la[(2 * LA_F + MC_FIELDS) * EN + 2 * (size_t)p.E + (size_t)wslot * p.E + e] =
+          __longlong_as_double((long long)L.gmin[g]);
+  }
+  (void)kList;
 }
 
 // CDW: waves per workgroup.  Wave 0 owns the workgroup's 64/GS envs as always; waves 1..CDW-1
@@ -2008,16 +2140,18 @@ __global__ __launch_bounds__(64 * CDW) BSG_WPE void step_kernel(KParams p) {
   BSG_STAMP(1, stamp_clock());
 #endif
   constexpr bool kLA = (KIND == BSG_ENV_MERGE || KIND == BSG_ENV_VERTICAL_CR) && !WIND;
+  __shared__ Lds<WIND> L;
+  constexpr int kList = 64 * (GS > 1 ? GS - 1 : 1);
+  __shared__ unsigned short cd_lists[CDW * kList];   // per-wave CD work lists (cd_pairs)
   if constexpr (kLA) {
     if (p.la && (int)blockIdx.x >= p.la_grid0) {
-      lookahead_role<KIND, GS, WIND>(p);
+      lookahead_role<KIND, GS, WIND, CDW>(p, L, cd_lists);
 #if defined(BSG_STAMPS) && BSG_STAMPS
       BSG_STAMP(6, __builtin_amdgcn_s_memrealtime());
 #endif
       return;                                  // the whole workgroup: no barrier below
     }
   }
-  __shared__ Lds<WIND> L;
   const int lane = threadIdx.x & 63;
   const int wv = CDW > 1 ? (int)(threadIdx.x >> 6) : 0;   // CD helper waves: wv > 0
   const int ws = (WIND && p.wind.augment) ? 2 : 0;   // obs carries wind_u / wind_v
@@ -2051,11 +2185,25 @@ __global__ __launch_bounds__(64 * CDW) BSG_WPE void step_kernel(KParams p) {
   double* const mcache = la_intr ? nullptr : b.memo_cache;
   AC s_la = {};
   uint64_t la_tag_in = 0;
+  // (la_cd: the intruder pairs' rows of that state, and the env's min separation over them
+  // on the ownship lane; used only when the tag matches)
+  unsigned long long la_cd_in[4] = {0ull, 0ull, 0ull, 0ull};
   if (la_intr && ok && p.mode == MODE_STEP) {
     const size_t EN = (size_t)p.E * N;
-    la_load(p.la + (size_t)p.la_par * LA_F * EN, a, EN, s_la);
+    const double* rs = p.la + (size_t)p.la_par * LA_F * EN;
+    la_load(rs, a, EN, s_la);
     la_tag_in = reinterpret_cast<const uint64_t*>(p.la + (2 * LA_F + MC_FIELDS) * EN)
         [(size_t)p.la_par * p.E + e];
+    if (p.la_cd) {
+#pragma unroll
+      for (int f = 0; f < 3; ++f)
+        la_cd_in[f] = (unsigned long long)__double_as_longlong(rs[(size_t)(LA_STATE + f) * EN + a]);
+    }
+  }
+  if (kLA && p.la && p.la_cd && ok && j == 0 && p.mode == MODE_STEP) {
+    const size_t EN = (size_t)p.E * N;
+    la_cd_in[3] = (unsigned long long)__double_as_longlong(
+        p.la[(2 * LA_F + MC_FIELDS) * EN + 2 * (size_t)p.E + (size_t)p.la_par * p.E + e]);
   }
   double mc[MC_FIELDS];
 #pragma unroll
@@ -2122,6 +2270,12 @@ __global__ __launch_bounds__(64 * CDW) BSG_WPE void step_kernel(KParams p) {
       if (ev.over) ev.flags |= BSG_FLAG_SPAWN_OVERFLOW;
     }
     if (wv == 0) stage(L, lane, s);
+    if constexpr (kLA) {
+      // the CD of this env takes the lookahead's intruder rows when its intruders' state did
+      if (wv == 0 && j == 1)
+        L.cdsel[g] = (stepping && la_intr && la_tag_in == la_tag(ev.episode, ev.step_count, p.la_gen))
+                         ? CD_OWN : CD_ALL;
+    }
   }
   __syncthreads();
 #if defined(BSG_STAMPS) && BSG_STAMPS
@@ -2164,86 +2318,26 @@ __global__ __launch_bounds__(64 * CDW) BSG_WPE void step_kernel(KParams p) {
   uint64_t cmask = 0, lmask = 0;
   double tmax = 0.0, msep = __builtin_inf();
   if (kLaneObs && p.cfg.compute_cd) {
-    constexpr int kList = 64 * (GS > 1 ? GS - 1 : 1);
-    __shared__ unsigned short cd_lists[CDW * kList];
     unsigned short* cd_list = cd_lists + wv * kList;   // this wave's work list
+    // CD_OWN (the lookahead's slot brought the intruder pairs' rows): start from them
+    int sel = CD_ALL;
+    if constexpr (kLA) sel = (p.la && p.la_cd) ? L.cdsel[g] : CD_ALL;
     if (wv == 0) {
-    L.cm[lane] = 0ull;
-    L.lm[lane] = 0ull;
-    L.tmax[lane] = 0ull;                                   // bits of +0.0
-    L.gmin[lane] = bits(__builtin_inf());
+      const bool oo = sel == CD_OWN;
+      L.cm[lane] = oo ? la_cd_in[0] : 0ull;
+      L.lm[lane] = oo ? la_cd_in[1] : 0ull;
+      L.tmax[lane] = oo ? la_cd_in[2] : 0ull;              // bits of +0.0
+      if (j == 0) L.gmin[g] = oo ? la_cd_in[3] : bits(__builtin_inf());
     }
-    // phase 1: candidate pairs (no transcendentals).  The bound is symmetric in (i, k)
-    // bit for bit, so each unordered pair is tested once: lane j takes the ring offsets
-    // 1..nac/2 (16 per lane at N = 32, balanced).  (The LDS rows above are first touched
-    // by phase 2's atomics, after the work-list barrier.)
-    // helper waves test wave 0's aircraft (fixed count N: CDW > 1 only for Merge)
+    // every unordered pair once (ring offsets, cd_pairs); helper waves test wave 0's
+    // aircraft (fixed count N: CDW > 1 only for Merge)
     const int nac = CDW > 1 ? N : ev.nac;
     const bool cd_on = CDW > 1 ? ((int)blockIdx.x * (64 / GS) + g < p.E && j < N) : on;
-    uint64_t mine = 0;                   // bit sft-1: pair (j, j + sft) is a candidate
-    if (cd_on) {
-      const float4 pi = L.fpk[lane];
-      const float flati = pi.x, floni = pi.y, fui = pi.z, fvi = pi.w;
-      const float fali = fabsf(flati);
-      // loads and tests only (unrolled so the LDS reads of several offsets are in flight
-      // together)
-      const int nsft = (nac & 1) ? nac / 2 : (j < nac / 2 ? nac / 2 : nac / 2 - 1);
-#pragma unroll 4
-      for (int sft = 1 + wv; sft <= nsft; sft += CDW) {
-        int k = j + sft;
-        if (k >= nac) k -= nac;
-        const float4 pk = L.fpk[base + k];
-        const float dlat = fabsf(pk.x - flati);
-        float dl = fabsf(pk.y - floni);
-        dl = dl > 180.0f ? 360.0f - dl : dl;
-        const float x = fmaxf(fali, fabsf(pk.x));
-        const float du = pk.z - fui, dv = pk.w - fvi;
-        if (cd_candidate_f(dlat, dl, x, du * du + dv * dv)) mine |= 1ull << (sft - 1);
-      }
-    }
-    // work list of the unordered candidate pairs: exclusive prefix sum of the per-lane
-    // counts (< 64) from one ballot per bit -- each lane counts the set bits below it
-    // (mbcnt), no cross-lane data movement
-    const int cnt = __popcll(mine);
-    int pos = 0, total = 0;
-#pragma unroll
-    for (int bit = 0; bit < 7; ++bit) {
-      const uint64_t bm = __ballot((cnt >> bit) & 1);
-      pos += (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32),
-                                            __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u)) << bit;
-      total += __popcll(bm) << bit;
-    }
-    for (uint64_t c = mine; c; c &= c - 1) {
-      int k = j + 1 + __builtin_ctzll(c);
-      if (k >= nac) k -= nac;
-      cd_list[pos++] = (unsigned short)((lane << 6) | (base + k));
-    }
-    __syncthreads();
+    unsigned long long* st4 = nullptr;
 #if defined(BSG_STAMPS) && BSG_STAMPS
-    BSG_STAMP(4, stamp_clock() | ((unsigned long long)total << 48));
+    if (p.stamps) st4 = p.stamps + (size_t)blockIdx.x * 8 + 4;
 #endif
-    // phase 2: dense exact StateBased over the surviving pairs, both orders per lane
-    auto commit = [&](int pr, const CdOut* r) {
-      const int li = pr >> 6, lk = pr & 63;
-      const int gb = (li / GS) * GS;
-#pragma unroll
-      for (int o = 0; o < 2; ++o) {
-        const int row = o ? lk : li, col = (o ? li : lk) - gb;
-        if (r[o].inside) {
-          atomicMin(&L.gmin[li / GS], bits(r[o].dist));
-          if (r[o].confl) atomicOr(&L.cm[row], 1ull << col);
-          if (r[o].lossep) atomicOr(&L.lm[row], 1ull << col);
-          if (r[o].confl && r[o].tcpa > 0.0) atomicMax(&L.tmax[row], bits(r[o].tcpa));
-        }
-      }
-    };
-    for (int t = lane; t < total; t += 64) {
-      const int pr = cd_list[t];
-      CdOut r[2];
-      cd_pair2(L, pr >> 6, pr & 63, &r[0], &r[1]);
-      commit(pr, r);
-    }
-    __syncthreads();
+    cd_pairs<GS, CDW>(L, cd_list, lane, wv, j, base, nac, cd_on, sel, st4);
     cmask = L.cm[lane];
     lmask = L.lm[lane];
     tmax = __longlong_as_double((long long)L.tmax[lane]);
@@ -2480,6 +2574,10 @@ static hipError_t launch_kind_w(const KParams& p0, hipStream_t st) {
   if (!((KIND == BSG_ENV_MERGE || KIND == BSG_ENV_VERTICAL_CR) && !WIND)) p.la = nullptr;
   p.prio_sw_num = 3;                         // (the lookahead's waves: fixed priority)
   p.prio_sw_den = 4;
+  // Vertical: the lookahead waves also take the intruder pairs' CD (they end well before the
+  // main waves there, whose phase 2 runs ~4 rounds of ~230 candidate pairs); Merge: not (its
+  // lookahead waves are the critical path, profiles/r03/fastown/README.md)
+  p.la_cd = (KIND == BSG_ENV_VERTICAL_CR && p.la && p.cfg.compute_cd) ? 1 : 0;
   const int grid = p.la ? 2 * grid0 : grid0;
 #define BSG_CASE(G) \
   case G: hipLaunchKernelGGL((step_kernel<KIND, G, WIND>), dim3(grid), dim3(64), p.lds_pad, st, p); break;
