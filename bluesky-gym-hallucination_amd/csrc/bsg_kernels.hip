@@ -1992,20 +1992,27 @@ __device__ __forceinline__ void propagate(const KParams& p, int e, int j, size_t
   }
 }
 
-// ---- lookahead: the Merge intruders one RL step ahead ------------------------------------
+// ---- lookahead: the intruders one RL step ahead (Merge, Vertical) -------------------------
 // Merge's intruders fly LNAV to FIX then RWY at constant speed and altitude (RESO OFF,
-// merge_env.py:155-157): their next step depends neither on the ownship nor on the
-// action.  With a lookahead scratch bound (bsg_set_lookahead), a step launch has twice the
-// workgroups: the main ones consume the intruders' post-step states the previous launch
-// computed and propagate only the ownship before the observation/CD phases, while the
-// lookahead ones (blockIdx >= la_grid0, one wave each) propagate the intruders one step
-// further.  So the intruders' ten substeps leave the launch's critical path (a C4 shard of
-// 512 envs runs one wave per SIMD: its time is that path).  The same substep() runs on the
-// same inputs: the states are bit-identical to the inline path (tests/test_gpu_lookahead.py).
-// Scratch (doubles, EN = E*N): two slots of LA_F fields x EN (lat lon alt hdg tas cas vs ax
-// ap_trk, nav bits; selspd/selalt/selvs never change for an intruder), the lookahead
-// blocks' own memo [MC_FIELDS][EN], then two tag rows [E] (u64).  A slot entry is valid for
-// the launch whose env scalars give the same tag (episode, step_count, generation).
+// merge_env.py:155-157), Vertical's a creconfs straight line (vertical_cr_env.py:183-200):
+// their next step depends neither on the ownship nor on the action.  With a lookahead
+// scratch bound (bsg_set_lookahead), a step launch has twice the workgroups: the main ones
+// consume the intruders' post-step states the previous launch computed and propagate only
+// the ownship before the observation/CD phases, while the lookahead ones (blockIdx >=
+// la_grid0, one working wave each) propagate the intruders one step further.  So the
+// intruders' substeps leave the launch's critical path (a C4 shard of 512 envs runs one
+// wave per SIMD: its time is that path).  The same substep() runs on the same inputs: the
+// states are bit-identical to the inline path (tests/test_gpu_lookahead.py).
+// Scratch (doubles, EN = E*N; bsg_internal.h la_doubles): two slots of LA_F fields x EN (lat
+// lon alt hdg tas cas vs ax ap_trk, nav bits -- selspd/selalt/selvs never change for an
+// intruder -- then, with la_cd, the intruder pairs' conflict / LoS rows and tcpamax), the
+// lookahead blocks' own memo [MC_FIELDS][EN], two tag rows [E] (u64) and two rows [E] of the
+// intruder pairs' min separation.  A slot entry is valid for the launch whose env scalars
+// give the same tag (episode, step_count, generation).  la_cd (Vertical): the lookahead wave
+// also runs the StateBased CD over the intruder pairs of the state it stores, and the main
+// waves that take the slot add only the ownship's pairs (cd_pairs CD_OWN) -- a pair's result
+// depends on its two aircraft alone and the rows are an or / u64 max / min over pairs, so
+// the outputs are the inline path's bit for bit.
 static_assert(LA_MC == MC_FIELDS, "lookahead memo layout");
 
 __device__ __forceinline__ uint64_t la_tag(uint32_t episode, int step, uint32_t gen) {
