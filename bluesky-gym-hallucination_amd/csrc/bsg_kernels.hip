@@ -2104,7 +2104,7 @@ __device__ __forceinline__ void lookahead_role(const KParams& p, LT& L, unsigned
       if (j == 1) tags[(size_t)wslot * p.E + e] = tag_out;
     }
   }
-  if (!p.la_cd) return;
+  if (KIND != BSG_ENV_VERTICAL_CR || !p.la_cd) return;
   // The intruder pairs' StateBased rows of the state just stored (the next launch's), for
   // the main waves that take this slot (cd_pairs CD_OWN adds the ownship's pairs)
   if (run) stage(L, lane, s);
@@ -2147,6 +2147,9 @@ __global__ __launch_bounds__(64 * CDW) BSG_WPE void step_kernel(KParams p) {
   BSG_STAMP(1, stamp_clock());
 #endif
   constexpr bool kLA = (KIND == BSG_ENV_MERGE || KIND == BSG_ENV_VERTICAL_CR) && !WIND;
+  // (la_cd is Vertical's only: compiled out of the other kinds, whose registers it would
+  // otherwise hold across the substep loop)
+  constexpr bool kLaCd = KIND == BSG_ENV_VERTICAL_CR && !WIND;
   __shared__ Lds<WIND> L;
   constexpr int kList = 64 * (GS > 1 ? GS - 1 : 1);
   __shared__ unsigned short cd_lists[CDW * kList];   // per-wave CD work lists (cd_pairs)
@@ -2201,13 +2204,13 @@ __global__ __launch_bounds__(64 * CDW) BSG_WPE void step_kernel(KParams p) {
     la_load(rs, a, EN, s_la);
     la_tag_in = reinterpret_cast<const uint64_t*>(p.la + (2 * LA_F + MC_FIELDS) * EN)
         [(size_t)p.la_par * p.E + e];
-    if (p.la_cd) {
+    if (kLaCd && p.la_cd) {
 #pragma unroll
       for (int f = 0; f < 3; ++f)
         la_cd_in[f] = (unsigned long long)__double_as_longlong(rs[(size_t)(LA_STATE + f) * EN + a]);
     }
   }
-  if (kLA && p.la && p.la_cd && ok && j == 0 && p.mode == MODE_STEP) {
+  if (kLaCd && p.la && p.la_cd && ok && j == 0 && p.mode == MODE_STEP) {
     const size_t EN = (size_t)p.E * N;
     la_cd_in[3] = (unsigned long long)__double_as_longlong(
         p.la[(2 * LA_F + MC_FIELDS) * EN + 2 * (size_t)p.E + (size_t)p.la_par * p.E + e]);
@@ -2277,7 +2280,7 @@ __global__ __launch_bounds__(64 * CDW) BSG_WPE void step_kernel(KParams p) {
       if (ev.over) ev.flags |= BSG_FLAG_SPAWN_OVERFLOW;
     }
     if (wv == 0) stage(L, lane, s);
-    if constexpr (kLA) {
+    if constexpr (kLaCd) {
       // the CD of this env takes the lookahead's intruder rows when its intruders' state did
       if (wv == 0 && j == 1)
         L.cdsel[g] = (stepping && la_intr && la_tag_in == la_tag(ev.episode, ev.step_count, p.la_gen))
@@ -2328,9 +2331,9 @@ __global__ __launch_bounds__(64 * CDW) BSG_WPE void step_kernel(KParams p) {
     unsigned short* cd_list = cd_lists + wv * kList;   // this wave's work list
     // CD_OWN (the lookahead's slot brought the intruder pairs' rows): start from them
     int sel = CD_ALL;
-    if constexpr (kLA) sel = (p.la && p.la_cd) ? L.cdsel[g] : CD_ALL;
+    if constexpr (kLaCd) sel = (p.la && p.la_cd) ? L.cdsel[g] : CD_ALL;
     if (wv == 0) {
-      const bool oo = sel == CD_OWN;
+      const bool oo = kLaCd && sel == CD_OWN;
       L.cm[lane] = oo ? la_cd_in[0] : 0ull;
       L.lm[lane] = oo ? la_cd_in[1] : 0ull;
       L.tmax[lane] = oo ? la_cd_in[2] : 0ull;              // bits of +0.0
