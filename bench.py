@@ -9,7 +9,9 @@ split over the N GPUs (strong scaling, SURVEY C4: 4096/N envs per rank; `--weak`
 StateBased all-pairs CPA on every step, Gymnasium NEXT_STEP autoreset inside the timed
 region.  Spawns are drawn on the device (Philox); actions come from a bank of U(-1,1)
 batches resident in HBM before timing starts.  With N>1 every step also all-gathers the
-[E, obs+3] fp32 learner rows over RCCL (the north-star's learner hand-off).
+[E, obs+3] fp32 learner rows over RCCL (the north-star's learner hand-off, one per RL
+step); the block-gather variant (one all_gather per 8 steps) is timed afterwards and
+reported in the `gather_block` object.
 """
 from __future__ import annotations
 
@@ -135,10 +137,14 @@ def main():
     ap.add_argument("--weak", action="store_true", help="weak scaling: --envs-per-gpu on every GPU")
     ap.add_argument("--envs-per-gpu", type=int, default=4096)
     ap.add_argument("--num-ac", type=int, default=32)
-    ap.add_argument("--steps-per-gather", type=int, default=8,
+    ap.add_argument("--steps-per-gather", type=int, default=1,
                     help="N>1: learner rows all-gathered once per block of this many steps "
                          "(one RCCL all_gather of [k, E, obs+3] fp32; the last partial block is "
-                         "flushed inside the timed region); 1 = one all_gather per step")
+                         "flushed inside the timed region); 1 (default, SURVEY §8(e), BASELINE C4) "
+                         "= one all_gather per RL step")
+    ap.add_argument("--gather-block", type=int, default=8,
+                    help="N>1: also time the block-gather variant (one all_gather per this many "
+                         "steps) after the headline, reported in the `gather_block` object; 0 = skip")
     ap.add_argument("--no-cd", action="store_true")
     ap.add_argument("--no-gather", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
@@ -259,6 +265,9 @@ def main():
         t = torch.tensor([el, kern_avg_ms, samp_ms, step_avg_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el, kern_avg_ms, samp_ms, step_avg_ms = (float(x) for x in t)
+    blk = None
+    if gather and args.gather_block > 1 and args.gather_block != args.steps_per_gather:
+        blk = bench_gather_block(args, make_local, world, E, acts, backend, dev)
     c5 = None
     if world == 1 and not args.no_c5:
         c5 = bench_c5_quick(args, dev)
@@ -344,10 +353,50 @@ def main():
             out["cpu_baseline"] = cpu
         if c5 is not None:
             out["c5"] = c5
+        if blk is not None:
+            out["gather_block"] = blk
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def bench_gather_block(args, make_local, world, E, acts, backend, dev):
+    """N > 1: the same workload with the learner rows gathered once per block of k steps
+    (one all_gather of [k, E, obs+3] per k steps: fewer, larger collectives; the learner
+    sees each step's rows up to k - 1 steps late).  Not the headline: BASELINE C4 and SURVEY
+    §8(e) gather every step.  Same timing rules (barrier + synchronize on both sides, max
+    over ranks), own env instance."""
+    import torch
+    import torch.distributed as dist
+    from bluesky_gym.parallel import ShardedVectorEnv
+    k = args.gather_block
+    env = ShardedVectorEnv(make_local, world * E, overlap=(backend == "nccl"), steps_per_gather=k)
+    env.reset()
+    for i in range(args.warmup):
+        env.step(acts[i % 16])
+    env.flush()
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        env.step(acts[i % 16])
+    _, ready = env.flush()
+    if ready is not None:
+        ready.wait()
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    t = torch.tensor([el], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    el = float(t[0])
+    env.close()
+    return {"steps_per_gather": k, "value": world * E * args.steps / el,
+            "ms_per_step": el * 1e3 / args.steps, "unit": "env_steps/s",
+            "note": f"one all_gather of [{k}, E, obs+3] fp32 per {k} steps (the learner sees a "
+                    f"step's rows up to {k - 1} steps late); not the C4 contract"}
 
 
 def bench_c5_quick(args, dev):

@@ -97,9 +97,14 @@ class EnvKindConfig:
 
 
 def merge_config(num_ac=20, num_ac_state=5, action_frequency=10, simdt=5.0,
-                 max_episode_steps=50):
+                 max_episode_steps=50, ac_spd=None):
+    """ac_spd: creation CAS [m/s] of every aircraft; None = merge_env.py:30's AC_SPD = 100.
+    Another value is a test hook (the logged revision of DESIGN.md §5), not the reference."""
+    opt = 0 if ac_spd is None or int(ac_spd) == 100 else int(ac_spd)
+    if ac_spd is not None and float(ac_spd) != int(ac_spd):
+        raise ValueError("ac_spd must be a whole number of m/s")
     return EnvKindConfig(nat.ENV_MERGE, num_ac, num_ac_state, action_frequency, simdt,
-                         max_episode_steps)
+                         max_episode_steps, opt)
 
 
 def vertical_config(num_intruders=5, action_frequency=30, simdt=1.0, max_episode_steps=300):

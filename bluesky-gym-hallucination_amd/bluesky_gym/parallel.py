@@ -111,10 +111,12 @@ class ShardedVectorEnv:
         """Resets the local shard and gathers every rank's reset rows (obs, reward 0,
         terminated 0, truncated 0) at once, as a block of one step: returns (rows, Ready)
         shaped as step() does (k = 1: [total_envs, obs+3]; k > 1: [1, world, n_local,
-        obs+3]).  A partial block of earlier steps is flushed (gathered) first.  The local
-        shard's Dict observation stays available as self.local_obs."""
+        obs+3]).  The local shard's Dict observation stays available as self.local_obs.
+        k > 1: a block still open (steps taken since the last gather) raises -- call flush()
+        first and keep its (block, Ready), or those steps' rows would never reach the caller."""
         if self._i:
-            self.flush()
+            raise RuntimeError(f"reset() with {self._i} step(s) of an open gather block: "
+                               "call flush() first and consume its rows")
         blk, _ = self._slot()
         # (a reset(seed=) that rebuilds the batch keeps the learner buffer: vector.py)
         self.local_obs, self.local_info = self.local.reset(**kw)

@@ -143,6 +143,9 @@ class BlueSkyVectorEnv(_gym.VectorEnv):
         """Gymnasium reset.  reset(seed=s) always restarts from s -- fresh host RNG streams
         and episode counters (the Philox key) -- so two resets with the same seed give the
         same episodes; reset() without a seed continues the streams."""
+        # an overflow flagged by step_tensors() calls since the last check raises here at the
+        # latest (the rebuild below would drop the sticky mask)
+        self._check_overflow()
         if seed is not None:
             self._seed = seed
             self._host_rngs = None
@@ -160,7 +163,13 @@ class BlueSkyVectorEnv(_gym.VectorEnv):
 
     def step_tensors(self, actions):
         """Device path: actions [E, A] (torch, any device) -> device views
-        (obs fp32 [E, O], reward fp32 [E], terminated u8 [E], truncated u8 [E])."""
+        (obs fp32 [E, O], reward fp32 [E], terminated u8 [E], truncated u8 [E]).
+
+        SectorCR capacity overflow (an episode drawing more than num_ac aircraft): this
+        path adds no host sync, so the flag is read back only every OVERFLOW_CHECK_EVERY
+        calls -- an overflowed episode can run up to that many steps with missing aircraft
+        before the RuntimeError.  step(), reset() and close() check the sticky flag, so the
+        error is never lost."""
         sp = None
         if self.spawn_mode == "host":
             pend = self.batch.envs["flags"].cpu().numpy() & 1
@@ -227,7 +236,11 @@ class BlueSkyVectorEnv(_gym.VectorEnv):
         return out
 
     def close(self):
-        self.batch.close()
+        try:
+            if getattr(self.batch, "_ctx", None) is not None and self.batch._ctx.value:
+                self._check_overflow()
+        finally:
+            self.batch.close()
 
 
 class MergeVectorEnv(BlueSkyVectorEnv):

@@ -42,7 +42,12 @@ struct bsg_ctx {
   double* la = nullptr;
   int la_par = 0;
   uint32_t la_gen = 0;
+  uint32_t la_seq = 0;              // launches since the last re-arm (snapshot parity)
   bool la_dirty = false, memo_dirty = false, la_was_active = false;
+  bool la_prime = false;            // the next launch runs the priming pass first
+  // a launch was captured into a HIP graph: the host-side slot / snapshot parities cannot
+  // follow the graph's replays, so this ctx runs without the lookahead from then on
+  bool la_captured = false;
   int no_fastpath = 0;
 };
 
@@ -112,13 +117,17 @@ bsg::KParams make_params(const bsg_ctx* c, int mode) {
   p.la = la_active(c) ? c->la : nullptr;
   p.la_par = c->la_par;
   p.la_gen = c->la_gen;
+  p.la_seq = c->la_seq;
   p.no_fastpath = c->no_fastpath;
   return p;
 }
 
-// the lookahead runs for a bound Merge scratch without a wind field (bsg_set_lookahead
-// refuses the configurations it cannot serve: other kinds, SAME_STEP autoreset)
-bool la_active(const bsg_ctx* c) { return c->la != nullptr && c->wind.np == 0; }
+// the lookahead runs for a bound Merge / Vertical scratch without a wind field
+// (bsg_set_lookahead refuses the configurations it cannot serve: other kinds, SAME_STEP
+// autoreset) and never for a ctx whose launches were captured into a graph
+bool la_active(const bsg_ctx* c) {
+  return c->la != nullptr && c->wind.np == 0 && !c->la_captured;
+}
 
 size_t la_bytes(const bsg_config& cfg) {
   return 8 * bsg::la_doubles((size_t)cfg.num_envs, (size_t)cfg.num_ac);
@@ -145,7 +154,9 @@ int la_prepare(bsg_ctx* c, hipStream_t st) {
     if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(lookahead)");
     c->la_gen = (c->la_gen % 0x7ffe) + 1;
     c->la_par = 0;
+    c->la_seq = 0;
     c->la_dirty = false;
+    c->la_prime = true;
   }
   return BSG_OK;
 }
@@ -199,11 +210,32 @@ int launch(bsg_ctx* c, int mode, const double* actions, const double* spawn,
   hipError_t e = hipSetDevice(c->cfg.device);
   if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (c->la && !c->la_captured) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    e = hipStreamIsCapturing(st, &cs);
+    if (e != hipSuccess) return hip_fail(e, "hipStreamIsCapturing");
+    if (cs != hipStreamCaptureStatusNone) c->la_captured = true;
+  }
   if (int r = la_prepare(c, st)) return r;
   bsg::KParams p = make_params(c, mode);
   p.actions = actions;
   p.spawn = spawn;
   p.env_mask = env_mask;
+#if defined(BSG_LA_LEGACY) && BSG_LA_LEGACY
+  c->la_prime = false;                // negative-control debug builds: round 3 had no priming pass
+#endif
+  if (p.la && c->la_prime) {
+    // after a re-arm: from the state the previous launch finished writing, the slot and the
+    // env-scalar snapshot this launch's lookahead waves read (bsg_kernels.hip lookahead_role)
+    bsg::KParams q = p;
+    q.mode = bsg::MODE_PRIME;
+    q.actions = nullptr;
+    q.spawn = nullptr;
+    q.env_mask = nullptr;
+    e = bsg::launch_step(q, st);
+    if (e != hipSuccess) return hip_fail(e, "lookahead priming launch");
+    c->la_prime = false;
+  }
   hipEvent_t t0 = nullptr, t1 = nullptr;
   const bool timed = c->timing > 0 && (c->launch_count++ % c->timing) == 0;
   if (timed) {
@@ -234,7 +266,10 @@ int launch(bsg_ctx* c, int mode, const double* actions, const double* spawn,
     }
     c->pending.emplace_back(t0, t1);
   }
-  if (p.la && mode == bsg::MODE_STEP) c->la_par ^= 1;   // this step wrote the other slot
+  if (p.la) {
+    if (mode == bsg::MODE_STEP) c->la_par ^= 1;   // this step wrote the other slot
+    ++c->la_seq;                                   // and the other snapshot
+  }
   return BSG_OK;
 }
 
@@ -314,7 +349,8 @@ int32_t bsg_create(const bsg_config* cfg, bsg_ctx** out) {
   if (cfg->route_len < 0 || cfg->route_len > BSG_MAX_ROUTE)
     return fail(BSG_E_INVALID_ARG, "bsg_create: route_len out of range%s%lld");
   if (cfg->env_offset < 0) return fail(BSG_E_INVALID_ARG, "bsg_create: env_offset < 0%s%lld");
-  if (cfg->kind_option != 0 && !(cfg->env_kind == BSG_ENV_SECTOR_CR && cfg->kind_option == 1))
+  if (cfg->kind_option != 0 && !(cfg->env_kind == BSG_ENV_SECTOR_CR && cfg->kind_option == 1) &&
+      !(cfg->env_kind == BSG_ENV_MERGE && cfg->kind_option > 0 && cfg->kind_option <= 400))
     return fail(BSG_E_INVALID_ARG, "bsg_create: invalid kind_option%s (%lld)", "", cfg->kind_option);
   if (cfg->env_kind == BSG_ENV_MERGE && cfg->route_len < 1)
     return fail(BSG_E_INVALID_ARG, "bsg_create: Merge needs the FIX/RWY route%s%lld");

@@ -32,9 +32,10 @@ constexpr double P0 = 101325.0;
 constexpr double RHO0 = 1.225;
 constexpr double TSTRAT = 216.65;
 
-// frozen A320 envelope / autopilot defaults (docs/BLUESKY_SUBSET_SPEC.md §A.3).  VMAX_CAS,
-// VSMAX and the phase-GD envelope are fitted to the reference's SAC training logs
-// (oracle/bluesky_subset.py, tests/test_sac_logs.py)
+// frozen A320 envelope / autopilot defaults (docs/BLUESKY_SUBSET_SPEC.md §A.3).  VMAX_CAS
+// and the phase-GD envelope are fitted to the reference's SAC training logs
+// (oracle/bluesky_subset.py, tests/test_ref_logs.py); VSMAX is 4000 fpm, non-binding (the
+// round-2 fit was withdrawn in round 4: the held-out actors rejected it)
 constexpr double TAN_BANKDEF = 0.4663076581549986;    // tan(radians(25)), frozen literal
 constexpr double APVSDEF = 1500.0 * FPM;
 constexpr double EPS_SPD = 0.01;
@@ -43,8 +44,8 @@ constexpr double VMIN_CAS = 140.0 * KTS;
 constexpr double VMAX_CAS = 163.0;
 constexpr double MMO = 0.82;
 constexpr double HMAX = 39800.0 * FT;
-constexpr double VSMAX = 12.1;
-constexpr double VSMIN = -12.1;          // unreachable: the limits see |ap.vs|
+constexpr double VSMAX = 4000.0 * FPM;
+constexpr double VSMIN = -4000.0 * FPM;  // unreachable: the limits see |ap.vs|
 constexpr double GD_ALT_FT = 75.0;       // OpenAP phase GD: alt / ft <= 75
 constexpr double VMAX_GD = 88.5;         // phase GD: CAS in [0, VMAX_GD], axmax AXMAX_GD
 constexpr double AXMAX_GD = 2.0;

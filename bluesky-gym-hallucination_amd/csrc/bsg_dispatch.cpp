@@ -12,7 +12,14 @@ hipError_t launch_step(const KParams& p, hipStream_t st) {
 #if defined(BSG_ONLY_MERGE) && BSG_ONLY_MERGE
   // experiment builds (tools/flag_sweep.sh, tools/variants.sh): Merge only, for fast sweeps
   return p.cfg.env_kind == BSG_ENV_MERGE ? launch_kind_0(p, st) : hipErrorInvalidValue;
-#endif
+#elif defined(BSG_ONLY_LA) && BSG_ONLY_LA
+  // lookahead debug builds (Makefile la-debug): the two kinds with a lookahead
+  switch (p.cfg.env_kind) {
+    case BSG_ENV_MERGE: return launch_kind_0(p, st);
+    case BSG_ENV_VERTICAL_CR: return launch_kind_1(p, st);
+    default: return hipErrorInvalidValue;
+  }
+#else
   switch (p.cfg.env_kind) {
     case BSG_ENV_MERGE: return launch_kind_0(p, st);
     case BSG_ENV_VERTICAL_CR: return launch_kind_1(p, st);
@@ -23,6 +30,7 @@ hipError_t launch_step(const KParams& p, hipStream_t st) {
     case BSG_ENV_PLAN_WAYPOINT: return launch_kind_6(p, st);
     default: return hipErrorInvalidValue;
   }
+#endif
 }
 
 }  // namespace bsg

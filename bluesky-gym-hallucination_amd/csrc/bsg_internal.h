@@ -9,7 +9,8 @@ namespace bsg {
 
 using Buffers = bsg_buffers;
 
-enum { MODE_STEP = 0, MODE_RESET = 1 };
+// MODE_PRIME: the lookahead's priming pass (bsg_abi.cpp launch), lookahead workgroups only
+enum { MODE_STEP = 0, MODE_RESET = 1, MODE_PRIME = 2 };
 
 struct Route {
   int len;
@@ -39,12 +40,19 @@ struct WindDev {
 // for EN = E*N: two slots of LA_F fields x EN (LA_STATE state fields, then -- Vertical, la_cd
 // -- the intruder pairs' StateBased rows as u64 bits: conflict row, LoS row, tcpamax), the
 // lookahead blocks' memo [LA_MC][EN], two tag rows [E] (u64), two rows [E] of the intruder
-// pairs' minimum separation (bits of a double).
+// pairs' minimum separation (bits of a double), then the env-scalar snapshot the lookahead
+// waves read instead of the live env scalars: [2 launch parities][E][2] u64 (bsg_kernels.hip
+// la_snap).  Debug builds with -DBSG_LA_WAIT=1 append [E] u64 phase-A flags (tests only).
 constexpr int LA_STATE = 10;
 constexpr int LA_F = LA_STATE + 3;
 constexpr int LA_MC = 2;           // = MC_FIELDS (bsg_kernels.hip)
+#if defined(BSG_LA_WAIT) && BSG_LA_WAIT
+constexpr size_t LA_WAIT_E = 1;
+#else
+constexpr size_t LA_WAIT_E = 0;
+#endif
 __host__ __device__ constexpr size_t la_doubles(size_t E, size_t N) {
-  return (2 * LA_F + LA_MC) * E * N + 4 * E;
+  return (2 * LA_F + LA_MC) * E * N + (8 + LA_WAIT_E) * E;
 }
 
 // Passed by value to every launch (kernarg segment).
@@ -74,6 +82,9 @@ struct KParams {
   int prio_sw_num, prio_sw_den;  // substep priority switch point (set by the launcher)
   int la_cd;                 // the lookahead waves also run the intruder pairs' StateBased CD
                              // (set by the launcher: VerticalCREnv with compute_cd)
+  uint32_t la_seq;           // launches since the lookahead scratch was (re)armed: its parity
+                             // picks the env-scalar snapshot a launch reads (the main waves
+                             // write the other one for the next launch)
 };
 
 hipError_t launch_step(const KParams& p, hipStream_t stream);

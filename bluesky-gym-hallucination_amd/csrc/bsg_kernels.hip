@@ -969,7 +969,8 @@ __device__ __forceinline__ void spawn_merge(const KParams& p, int e, int j, uint
   }
   double lat, lon;
   get_point_at_distance(p.cfg.wpt_lat[0], p.cfg.wpt_lon[0], dist, brg, &lat, &lon);
-  cre(s, lat, lon, brg - 180, 10000.0, 100.0);               // merge_env.py:119,154
+  // merge_env.py:119,154 (AC_SPD = 100, :30; kind_option > 0: another creation CAS, bsg.h)
+  cre(s, lat, lon, brg - 180, 10000.0, p.cfg.kind_option > 0 ? (double)p.cfg.kind_option : 100.0);
   if (j > 0) s.nav = 1;                                      // ADDWPT FIX; DEST RWY -> LNAV on
 }
 
@@ -2034,11 +2035,60 @@ __device__ __forceinline__ void la_store(double* slot, size_t a, size_t EN, cons
   slot[9 * EN + a] = __longlong_as_double((long long)s.nav);
 }
 
+// The env scalars a lookahead wave needs (episode, step count, the NEXT_STEP reset flag) as
+// they were when its launch started, double-buffered by launch parity: the main waves of
+// launch seq write entry (seq + 1) & 1 at their end (and the priming pass writes seq & 1), a
+// lookahead wave of launch seq reads seq & 1.  So no lookahead wave ever reads a word a main
+// wave of its own launch writes (the live env scalars and
+// state are written by the main waves while the lookahead waves run).  Word 0: episode |
+// step_count << 32; word 1: generation | reset flag << 32 (0xFF.. after the re-arm memset:
+// no generation matches, the entry is unknown).
+__device__ __forceinline__ uint64_t* la_snap(const KParams& p, size_t EN, int par) {
+  return reinterpret_cast<uint64_t*>(p.la + (2 * LA_F + MC_FIELDS) * EN) + 4 * (size_t)p.E +
+         (size_t)par * 2 * p.E;
+}
+
+__device__ __forceinline__ void la_snap_store(const KParams& p, size_t EN, int par, int e,
+                                              const EnvScalars& ev) {
+  uint64_t* sn = la_snap(p, EN, par) + 2 * (size_t)e;
+  const bool rst = p.cfg.autoreset_mode == BSG_AUTORESET_NEXT_STEP && (ev.flags & 1);
+  sn[0] = (uint64_t)ev.episode | ((uint64_t)(uint32_t)ev.step_count << 32);
+  sn[1] = (uint64_t)p.la_gen | ((uint64_t)rst << 32);
+}
+
+#if defined(BSG_LA_WAIT) && BSG_LA_WAIT
+// Debug builds (tests/test_gpu_lookahead.py race test): the main wave of env e publishes the
+// end of its phase-A stores (state and, through the fence, everything before) as the launch
+// sequence number; the lookahead waves of e wait for it before their first read, so every
+// read a lookahead wave makes happens after its main wave wrote the state -- the order that
+// exposes a lookahead that reads what the main waves write.  Bounded spin (~10 ms): a wave
+// never waits forever, whatever the dispatch order.
+__device__ __forceinline__ uint64_t* la_wait_flags(const KParams& p, size_t EN) {
+  return reinterpret_cast<uint64_t*>(p.la + (2 * LA_F + MC_FIELDS) * EN) + 8 * (size_t)p.E;
+}
+__device__ __forceinline__ void la_wait_for_main(const KParams& p, size_t EN, int e) {
+  if (e >= p.E || p.mode == MODE_PRIME) return;
+  const uint64_t want = (uint64_t)p.la_seq + 1;
+  uint64_t* f = la_wait_flags(p, EN) + e;
+  for (int it = 0; it < (1 << 17); ++it) {
+    if (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == want) return;
+    __builtin_amdgcn_s_sleep(8);
+  }
+}
+#endif
+
 // One lookahead wave: the intruders of the same 64/GS envs as main workgroup
-// (blockIdx - la_grid0).  Post-step state of this launch: a spawn (resetting env), the
-// slot the main workgroups read (valid tag), or -- priming, after the scratch was (re)bound
-// -- this launch's step computed here too; then one more step into the other slot (a reset
-// launch writes the slot the next step reads).
+// (blockIdx - la_grid0).  It reads only words no main wave of its launch writes: the
+// env-scalar snapshot (la_snap), the slot and tag row the main waves read too (slots are
+// written only by lookahead waves, the other slot), its own memo region, the intruders'
+// selspd / selalt / selvs (constant after the spawn: no main wave of a stepping env stores
+// them) and the launch inputs (spawn rows, reset mask).  Post-step state of this launch: a
+// spawn (resetting env) or the slot the main workgroups read (valid tag); then one more step
+// into the slot the next launch reads.  A tag that does not match leaves that slot invalid
+// (the next launch's main waves propagate the env inline): after a re-arm (bind, wind,
+// toggle, direct state write) the host runs the priming pass first (MODE_PRIME: no main
+// waves; from the state the previous launch finished writing, one step into the slot the
+// next launch reads), so in a run the tags always match.
 template <int KIND, int GS, bool WIND, int CDW, class LT>
 __device__ __forceinline__ void lookahead_role(const KParams& p, LT& L, unsigned short* cd_lists) {
   if (threadIdx.x >= 64) return;              // (la_cd: Vertical, one wave per workgroup)
@@ -2051,17 +2101,49 @@ __device__ __forceinline__ void lookahead_role(const KParams& p, LT& L, unsigned
   const size_t a = (size_t)e * N + j;
   double* memo = p.la + 2 * LA_F * EN;
   uint64_t* tags = reinterpret_cast<uint64_t*>(p.la + (2 * LA_F + MC_FIELDS) * EN);
+  // the slot this wave writes: a step writes the one the next step reads; a reset or the
+  // priming pass writes the one the next step reads, which is the one this launch would read
   const int wslot = p.mode == MODE_STEP ? 1 - p.la_par : p.la_par;
+#if defined(BSG_LA_WAIT) && BSG_LA_WAIT
+  la_wait_for_main(p, EN, e);
+#endif
   // this lane propagates intruder (e, j) (and, with la_cd, takes part in its env's pairs)
   bool run = e < p.E && j > 0 && j < N;
   AC s = {};
   if (run) {
     // every read of the common case is issued here, before any decision needs it, so the
-    // wave pays one memory round trip instead of three (env scalars -> slot tag -> state):
-    // the env scalars, the slot's tag and entry, the state (selspd / selalt / selvs) and the
-    // lookahead memo entries
-    EnvScalars ev = {};
-    load_env(b, e, ev);
+    // wave pays one memory round trip: the snapshot, the slot's tag and entry, the state
+    // (selspd / selalt / selvs) and the lookahead memo entries
+    uint32_t episode;
+    int step;
+    bool known, rst;
+    if (p.mode == MODE_PRIME) {
+      // no main waves in this launch: the live env scalars are the next launch's start
+      EnvScalars ev = {};
+      load_env(b, e, ev);
+      episode = ev.episode;
+      step = ev.step_count;
+      known = true;
+      rst = p.cfg.autoreset_mode == BSG_AUTORESET_NEXT_STEP && (ev.flags & 1);
+      if (j == 1) la_snap_store(p, EN, (int)(p.la_seq & 1u), e, ev);
+    } else {
+#if defined(BSG_LA_LEGACY) && BSG_LA_LEGACY
+      // negative control (debug builds only): round 3's reads, the live env scalars
+      EnvScalars ev = {};
+      load_env(b, e, ev);
+      episode = ev.episode;
+      step = ev.step_count;
+      known = true;
+      rst = p.cfg.autoreset_mode == BSG_AUTORESET_NEXT_STEP && (ev.flags & 1);
+#else
+      const uint64_t* sn = la_snap(p, EN, (int)(p.la_seq & 1u)) + 2 * (size_t)e;
+      const uint64_t w0 = sn[0], w1 = sn[1];
+      episode = (uint32_t)w0;
+      step = (int)(uint32_t)(w0 >> 32);
+      known = (uint32_t)w1 == p.la_gen;
+      rst = (w1 >> 32) & 1u;
+#endif
+    }
     const double* rslot = p.la + (size_t)p.la_par * LA_F * EN;
     const uint64_t tag_in = p.mode == MODE_STEP ? tags[(size_t)p.la_par * p.E + e] : 0;
     load_ac<false>(b, a, s);
@@ -2071,38 +2153,63 @@ __device__ __forceinline__ void lookahead_role(const KParams& p, LT& L, unsigned
     memo_fetch(mc, memo, a, EN);
     bool resetting;
     if (p.mode == MODE_RESET) resetting = p.env_mask ? (p.env_mask[e] != 0) : true;
-    else resetting = (p.cfg.autoreset_mode == BSG_AUTORESET_NEXT_STEP) && (ev.flags & 1);
-    run = resetting || p.mode == MODE_STEP;               // untouched by a masked reset
-    if (run) {
+    else if (p.mode == MODE_PRIME) resetting = false;
+    else resetting = rst;
+    // MODE_PRIME: every env not resetting at the next launch (that launch spawns the others);
+    // MODE_RESET: the masked envs; MODE_STEP: every env, from a spawn or a valid slot
+    bool valid;
+    if (p.mode == MODE_PRIME) valid = !rst;
+    else if (!known) valid = false;
+    else if (resetting) valid = true;
+    else valid = p.mode == MODE_STEP && tag_in == la_tag(episode, step, p.la_gen);
+    const bool touch = p.mode == MODE_STEP || (p.mode == MODE_RESET ? resetting : valid);
+#if defined(BSG_LA_LEGACY) && BSG_LA_LEGACY
+    // round 3's priming: on a tag mismatch, this launch's step from the live state
+    const bool legacy_prime = p.mode == MODE_STEP && known && !resetting && !valid;
+    valid = valid || legacy_prime;
+#else
+    constexpr bool legacy_prime = false;
+#endif
+    if (valid) {
       const double act[2] = {0.0, 0.0};
       const double oat[4] = {0.0, 0.0, 0.0, 0.0};
       double sub_reward = 0.0;
       bool sub_done = false;
+      EnvScalars ev = {};                      // (propagate reads no env scalar for these kinds)
       uint64_t tag_out;
       if (resetting) {
-        double aux[4] = {ev.target_alt, 0.0, 0.0, 0.0};
+        double aux[4] = {0.0, 0.0, 0.0, 0.0};
         s = AC{};
-        spawn<KIND>(p, e, j, ev.episode, s, aux, false);
+        spawn<KIND>(p, e, j, episode, s, aux, false);
         memo_invalidate(memo, a, EN);
 #pragma unroll
         for (int f = 0; f < MC_FIELDS; ++f) mc[f] = key_as_double(kNoKey);
-        tag_out = la_tag(ev.episode + 1u, 0, p.la_gen);
-      } else {
-        if (tag_in == la_tag(ev.episode, ev.step_count, p.la_gen)) {
-          s = s_slot;
-        } else {
-          memo_invalidate(memo, a, EN);
+        tag_out = la_tag(episode + 1u, 0, p.la_gen);
+      } else if (p.mode == MODE_PRIME) {
+        // from the state the previous launch finished writing: the next launch's post-step
+        // state, for the tag that launch starts with
+        memo_invalidate(memo, a, EN);
 #pragma unroll
-          for (int f = 0; f < MC_FIELDS; ++f) mc[f] = key_as_double(kNoKey);
-          propagate<KIND, WIND>(p, e, j, a, s, ev, sub_reward, sub_done, act, mc, oat, memo);
-          memo_fetch(mc, memo, a, EN);
-        }
-        tag_out = la_tag(ev.episode, ev.step_count + 1, p.la_gen);
+        for (int f = 0; f < MC_FIELDS; ++f) mc[f] = key_as_double(kNoKey);
+        tag_out = la_tag(episode, step, p.la_gen);
+      } else if (legacy_prime) {
+        memo_invalidate(memo, a, EN);
+#pragma unroll
+        for (int f = 0; f < MC_FIELDS; ++f) mc[f] = key_as_double(kNoKey);
+        propagate<KIND, WIND>(p, e, j, a, s, ev, sub_reward, sub_done, act, mc, oat, memo);
+        memo_fetch(mc, memo, a, EN);
+        tag_out = la_tag(episode, step + 1, p.la_gen);
+      } else {
+        s = s_slot;
+        tag_out = la_tag(episode, step + 1, p.la_gen);
       }
       propagate<KIND, WIND>(p, e, j, a, s, ev, sub_reward, sub_done, act, mc, oat, memo);
       la_store(p.la + (size_t)wslot * LA_F * EN, a, EN, s);
       if (j == 1) tags[(size_t)wslot * p.E + e] = tag_out;
+    } else if (touch && j == 1) {
+      tags[(size_t)wslot * p.E + e] = ~0ull;   // no generation produces this tag
     }
+    run = valid;
   }
   if (KIND != BSG_ENV_VERTICAL_CR || !p.la_cd) return;
   // The intruder pairs' StateBased rows of the state just stored (the next launch's), for
@@ -2279,6 +2386,15 @@ __global__ __launch_bounds__(64 * CDW) BSG_WPE void step_kernel(KParams p) {
       reset_scalars<KIND>(ev, aux);
       if (ev.over) ev.flags |= BSG_FLAG_SPAWN_OVERFLOW;
     }
+#if defined(BSG_LA_WAIT) && BSG_LA_WAIT
+    if (kLA && p.la && wv == 0) {
+      // debug builds: phase A's stores are out; release the lookahead waves of env e
+      __threadfence();
+      if (j == 0 && env_ok)
+        __hip_atomic_store(la_wait_flags(p, (size_t)p.E * N) + e, (uint64_t)p.la_seq + 1,
+                           __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+#endif
     if (wv == 0) stage(L, lane, s);
     if constexpr (kLaCd) {
       // the CD of this env takes the lookahead's intruder rows when its intruders' state did
@@ -2562,6 +2678,10 @@ __global__ __launch_bounds__(64 * CDW) BSG_WPE void step_kernel(KParams p) {
   }
 
   if (active && j == 0) store_env(b, e, ev);
+  // the next launch's lookahead waves read this env's scalars from the snapshot (la_snap)
+  if constexpr (kLA) {
+    if (p.la && env_ok && j == 0) la_snap_store(p, (size_t)p.E * N, (int)((p.la_seq + 1u) & 1u), e, ev);
+  }
 #if defined(BSG_STAMPS) && BSG_STAMPS
   BSG_STAMP(5, stamp_clock());
   BSG_STAMP(6, __builtin_amdgcn_s_memrealtime());
@@ -2582,13 +2702,17 @@ static hipError_t launch_kind_w(const KParams& p0, hipStream_t st) {
   KParams p = p0;
   p.la_grid0 = grid0;
   if (!((KIND == BSG_ENV_MERGE || KIND == BSG_ENV_VERTICAL_CR) && !WIND)) p.la = nullptr;
+  if (p.mode == MODE_PRIME) {
+    if (!p.la) return hipSuccess;
+    p.la_grid0 = 0;                          // every workgroup takes the lookahead role
+  }
   p.prio_sw_num = 3;                         // (the lookahead's waves: fixed priority)
   p.prio_sw_den = 4;
   // Vertical: the lookahead waves also take the intruder pairs' CD (they end well before the
   // main waves there, whose phase 2 runs ~4 rounds of ~230 candidate pairs); Merge: not (its
   // lookahead waves are the critical path, profiles/r03/fastown/README.md)
   p.la_cd = (KIND == BSG_ENV_VERTICAL_CR && p.la && p.cfg.compute_cd) ? 1 : 0;
-  const int grid = p.la ? 2 * grid0 : grid0;
+  const int grid = (p.la && p.mode != MODE_PRIME) ? 2 * grid0 : grid0;
 #define BSG_CASE(G) \
   case G: hipLaunchKernelGGL((step_kernel<KIND, G, WIND>), dim3(grid), dim3(64), p.lds_pad, st, p); break;
   if constexpr (KIND == BSG_ENV_MERGE && !WIND) {

@@ -81,7 +81,10 @@ typedef struct bsg_config {
   int32_t env_offset;        /* global id of env 0 of this batch (Philox counter); a shard of a
                                 multi-GPU job passes its first global env id */
   int32_t kind_option;       /* SectorCR ac_density_mode: 0 "normal", 1 uniform
-                                (sector_cr_env.py:45,95-100); 0 for the other kinds */
+                                (sector_cr_env.py:45,95-100).  MergeEnv: the creation CAS of
+                                every aircraft in m/s, 0 = the reference's AC_SPD = 100
+                                (merge_env.py:30,119,154); a test hook for the log revision
+                                of DESIGN.md §5.  0 for the other kinds */
   int32_t reserved0;
   double route_lat[BSG_MAX_ROUTE];
   double route_lon[BSG_MAX_ROUTE];

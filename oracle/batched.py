@@ -264,10 +264,13 @@ class MergeOracle(_Base):
 
     def __init__(self, num_envs, num_ac=20, num_ac_state=5, action_frequency=10, simdt=5.0,
                  max_episode_steps=50, autoreset=AUTORESET_NEXT_STEP, seed=0,
-                 compute_cd=True):
+                 compute_cd=True, ac_spd=MERGE_AC_SPD):
+        """ac_spd: creation CAS of every aircraft (merge_env.py:30 AC_SPD = 100; another value
+        restates the logged revision of DESIGN.md §5, tests/test_ref_logs.py)."""
         super().__init__(num_envs, num_ac, action_frequency, simdt, max_episode_steps,
                          autoreset, seed)
         assert num_ac - 1 >= num_ac_state
+        self.ac_spd = float(ac_spd)
         self.K = int(num_ac_state)
         self.compute_cd = compute_cd
         self.wpt_reach = np.zeros(self.E, np.int32)
@@ -305,7 +308,7 @@ class MergeOracle(_Base):
         lat, lon = bsx.get_point_at_distance(FIX_LAT, FIX_LON, dist, brg)
         for j in range(self.N):
             bsx.cre_state(st, (ids, np.full(len(ids), j)), lat[:, j], lon[:, j],
-                          brg[:, j] - 180, MERGE_ALT, MERGE_AC_SPD)
+                          brg[:, j] - 180, MERGE_ALT, self.ac_spd)
         # intruders: ADDWPT FIX ; DEST RWY  -> LNAV on, active waypoint FIX
         st.swlnav[ids, 1:] = True
         st.actwp[ids, 1:] = 0

@@ -54,13 +54,14 @@ T0 = 288.15             # K
 Tstrat = 216.65         # K
 
 # Frozen A320 envelope and autopilot defaults (docs/BLUESKY_SUBSET_SPEC.md §A.3).  The
-# speed / vertical-speed limits and the ground-phase envelope are FITTED to the reference's
-# own SAC training logs (scripts/common/results/logs_backup/*_SAC.csv) by rolling out its
-# saved actors (tests/golden/sac_actors.npz; tests/test_ref_logs.py; the
-# held-out DDPG/PPO actors reject the binding VSMAX, see there):
+# speed limit and the ground-phase envelope are FITTED to the reference's own SAC training
+# logs (scripts/common/results/logs_backup/*_SAC.csv) by rolling out its saved actors
+# (tests/golden/sac_actors.npz; tests/test_ref_logs.py):
 #   VMAX_CAS: Descent + Vertical episode-length distributions (162.5..163.5 bracket)
-#   VSMAX:    Descent final-altitude distribution (the terminal dive runs at the limit)
 #   VMAX_GD:  Horizontal + PlanWaypoint episode lengths (aircraft created at alt 0)
+# VSMAX is NOT fitted (round 4): the round-2 fit (12.1 m/s, from Descent SAC's final
+# altitude) bound below the envs' 12.5 m/s command and the held-out DDPG / PPO actors
+# rejected it; it is 4000 fpm, non-binding for every command the envs issue.
 BANKDEF = math.radians(25.0)          # ap.bankdef
 TAN_BANKDEF = 0.4663076581549986      # tan(BANKDEF), frozen literal shared with the device code
 APVSDEF = 1500.0 * fpm                # ap.apvsdef  (m/s)
@@ -70,8 +71,8 @@ VMIN_CAS = 140.0 * kts                # perf.vmin   (m/s CAS)
 VMAX_CAS = 163.0                      # perf.vmax   (m/s CAS), fitted
 MMO = 0.82                            # perf.mmo
 HMAX = 39800.0 * ft                   # perf.hmax   (m)
-VSMAX = 12.1                          # perf.vsmax  (m/s), fitted
-VSMIN = -12.1                         # perf.vsmin  (m/s); unreachable: the intent is |ap.vs|
+VSMAX = 4000.0 * fpm                  # perf.vsmax  (m/s), non-binding (the fit is withdrawn)
+VSMIN = -4000.0 * fpm                 # perf.vsmin  (m/s); unreachable: the intent is |ap.vs|
 GD_ALT_FT = 75.0                      # OpenAP phase GD: alt <= 75 ft
 VMAX_GD = 88.5                        # perf.vmax in phase GD (m/s CAS), fitted; vmin 0
 AXMAX_GD = 2.0                        # perf.axmax in phase GD (m/s2)

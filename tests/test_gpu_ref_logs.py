@@ -79,3 +79,24 @@ def test_device_reproduces_reference_logs(tag):
     unexpected = [k for k in bad if (tag, k) not in sp.KNOWN_RED]
     assert not unexpected, (f"{tag}: outside its band of the reference log: {unexpected}\n"
                             + "\n".join(lines))
+
+
+@pytest.mark.parametrize("ac_spd", [100, 150])
+def test_device_merge_saturated_policy(ac_spd):
+    """The MergeEnv DDPG / TD3 logs' saturated (+1, +1) policy on 4,096 device envs
+    (tests/test_ref_logs.py::test_merge_saturated_policy for the oracle; num_ac = 20, CD on,
+    the lookahead as DeviceBatch picks it): the same statistics against both logs."""
+    from bluesky_gym import config, core
+    b = core.DeviceBatch(config.merge_config(num_ac=20, ac_spd=ac_spd), E, seed=7)
+    b.reset()
+    act = torch.ones((E, 2), dtype=torch.float64, device=b.device)
+    for _ in range(50):
+        b.step(act)
+    assert bool(b.truncated.bool().all())
+    info = b.ep_info.cpu().numpy()
+    ours = {"total_reward": info[:, 0], "total_intrusions": info[:, 1], "average_drift": info[:, 3]}
+    tag = f"merge_sat_{ac_spd}"
+    lines, bad = sp.merge_sat_compare(tag, ours)
+    print("\n".join(lines))
+    unexpected = [k for k in bad if (tag, k) not in sp.KNOWN_RED]
+    assert not unexpected, f"{tag}: outside its band of the reference logs: {unexpected}\n" + "\n".join(lines)

@@ -112,3 +112,28 @@ def test_actor_forms():
     s = sp.actor_np(W, "static_ppo", x, np.random.default_rng(2))
     assert s.shape == (4096, 2) and s.min() == -1.0 and s.max() == 1.0   # std ~1.8: clipped
     assert np.abs(m).max() <= 1.0
+
+
+@pytest.mark.parametrize("ac_spd", [100, 150])
+def test_merge_saturated_policy(ac_spd):
+    """MergeEnv-v0's own DDPG / TD3 logs: from episode 3 on a constant
+    (+-1, +1) action flew them -- HDG +-15 deg and SPD +20 m/s every RL step
+    (merge_env.py:286-293), a circling ownship, every episode truncated at 50 steps.  The
+    statistics pin the sim layer under the headline env: the intruders' spawn and LNAV
+    stream (merge_env.py:148-158, FIX then RWY), the ownship's speed envelope at 10,000 m
+    and the intrusion count (:275-284).  num_ac = 20, the env's default.  Compared with both
+    logs' last 1,000 episodes: drift mean / spread, intrusions, reward and the intrusion
+    histogram; the known reds (ref_policy.KNOWN_RED) carry the decision that moves them."""
+    E = 2048
+    o = ob.MergeOracle(E, num_ac=20, seed=11, compute_cd=False, ac_spd=ac_spd)
+    o.reset()
+    act = np.tile([1.0, 1.0], (E, 1))
+    for _ in range(50):
+        r = o.step(act)
+    assert r["truncated"].all()
+    info = o.info()
+    tag = f"merge_sat_{ac_spd}"
+    lines, bad = sp.merge_sat_compare(tag, {k: info[k] for k in sp.MERGE_SAT_KEYS})
+    print("\n".join(lines))
+    unexpected = [k for k in bad if (tag, k) not in sp.KNOWN_RED]
+    assert not unexpected, f"{tag}: outside its band of the reference logs: {unexpected}\n" + "\n".join(lines)

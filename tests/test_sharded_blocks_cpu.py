@@ -125,3 +125,54 @@ def test_blocks_deliver_every_step_in_order(k, overlap):
         assert sorted(got) == list(range(-1, T)), sorted(got)     # reset + every step, once
         for t, v in got.items():
             assert v == _expected(world, t).tolist(), (r, t)
+
+
+def _worker_midreset(rank, world, port, q):
+    """k = 3: a reset() while a block is open must raise (it used to flush and
+    drop the block's rows); after flush() the rows of the open block arrive and reset() works."""
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from bluesky_gym.parallel import ShardedVectorEnv
+        env = ShardedVectorEnv(_Local, world * N_LOCAL, overlap=True, steps_per_gather=3)
+        env.reset()
+        for _ in range(4):                       # one full block (t = 0..2), t = 3 opens one
+            env.step(None)
+        raised = False
+        try:
+            env.reset()
+        except RuntimeError:
+            raised = True
+        rows, ready = env.flush()
+        ready.wait()
+        t3 = rows[0].reshape(world * N_LOCAL, D)[:, 0].tolist()
+        rows, ready = env.reset()
+        ready.wait()
+        r = rows[0].reshape(world * N_LOCAL, D)[:, 0].tolist()
+        env.close()
+        q.put((rank, (raised, t3, r), None))
+    except Exception as ex:  # pragma: no cover - reported to the parent
+        q.put((rank, None, repr(ex)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_reset_with_an_open_block_raises_and_loses_nothing():
+    import torch.multiprocessing as mp
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_midreset, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for _ in range(world):
+        r, got, err = q.get(timeout=120)
+        assert err is None, f"rank {r}: {err}"
+        raised, t3, rst = got
+        assert raised
+        assert t3 == _expected(world, 3).tolist()
+        assert rst == _expected(world, -1).tolist()
+    for p in procs:
+        p.join(timeout=30)
