@@ -95,14 +95,17 @@ class BlueSkyVectorEnv(_gym.VectorEnv):
         prev = getattr(self, "_over", None)
         self._over = over if prev is None or prev.shape != over.shape else prev | over
 
-    def _check_overflow(self):
+    def _check_overflow(self, pending_only=False):
         """SectorCR: an episode that drew more aircraft than the capacity raises, as the
-        host-spawn path does (bsg.h BSG_FLAG_SPAWN_OVERFLOW; sector_cr_env.py:95-100)."""
+        host-spawn path does (bsg.h BSG_FLAG_SPAWN_OVERFLOW; sector_cr_env.py:95-100).
+        pending_only: only what step_tensors() noted since the last check (reset / close:
+        the flag of an overflow already raised persists in the env's flags)."""
         if self.kind_cfg.kind != nat.ENV_SECTOR_CR:
             return
-        self._note_overflow()
-        over, self._over = self._over, None
-        if bool(over.any()):
+        if not pending_only:
+            self._note_overflow()
+        over, self._over = getattr(self, "_over", None), None
+        if over is not None and bool(over.any()):
             e = int(torch.nonzero(over)[0, 0])
             raise RuntimeError(f"SectorCR env {e}: the episode drew more aircraft than "
                                f"num_ac={self.kind_cfg.num_ac}; construct with a larger num_ac")
@@ -145,7 +148,7 @@ class BlueSkyVectorEnv(_gym.VectorEnv):
         same episodes; reset() without a seed continues the streams."""
         # an overflow flagged by step_tensors() calls since the last check raises here at the
         # latest (the rebuild below would drop the sticky mask)
-        self._check_overflow()
+        self._check_overflow(pending_only=True)
         if seed is not None:
             self._seed = seed
             self._host_rngs = None
@@ -238,7 +241,7 @@ class BlueSkyVectorEnv(_gym.VectorEnv):
     def close(self):
         try:
             if getattr(self.batch, "_ctx", None) is not None and self.batch._ctx.value:
-                self._check_overflow()
+                self._check_overflow(pending_only=True)
         finally:
             self.batch.close()
 

@@ -257,3 +257,18 @@ def test_sector_overflow_check_is_lazy_on_the_tensor_path():
     with pytest.raises(RuntimeError, match="more aircraft"):
         env.step_tensors(a)
     env.close()
+
+
+def test_sector_overflow_noted_by_step_tensors_is_raised_at_close():
+    """fewer than OVERFLOW_CHECK_EVERY step_tensors() calls after an overflowing
+    reset must still raise -- at close() (or the next reset()) -- never be lost."""
+    import torch
+    from bluesky_gym.vector import SectorCRVectorEnv
+    env = SectorCRVectorEnv(num_envs=64, num_ac=8, seed=1)
+    with pytest.raises(RuntimeError, match="more aircraft"):
+        env.reset()
+    a = torch.zeros((64, 2), dtype=torch.float64, device=env.batch.device)
+    for _ in range(3):
+        env.step_tensors(a)                      # the persisting flag is noted, not raised
+    with pytest.raises(RuntimeError, match="more aircraft"):
+        env.close()

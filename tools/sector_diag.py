@@ -30,9 +30,9 @@ BUCKETS = ((0, 10), (10, 20), (20, 30), (30, 60), (60, 1000))
 HIST = [0, 5, 10, 15, 20, 25, 30, 40, 60, 100, 400]
 
 
-def rollout(tag, E, seed=0, horizon=400):
+def rollout(tag, E, seed=0, horizon=400, spd_scale=1.0, hdg_scale=1.0, flip=(), af=5, dt=1.0):
     W = sp.load()
-    o = oba.SectorOracle(E, seed=5, compute_cd=False)
+    o = oba.SectorOracle(E, seed=5, compute_cd=False, action_frequency=af, simdt=dt)
     rng = None if sp.alg_of(W, tag) == "ddpg" else np.random.default_rng(seed)
     obs = o.reset()["obs"]
     ndone = np.zeros(E, np.int64)
@@ -40,7 +40,11 @@ def rollout(tag, E, seed=0, horizon=400):
     rec = {k: np.full(E, np.nan) for k in sp.LOG_KEYS["sector"]}
     tas, acts = [], []
     for _ in range(horizon):
-        act = sp.actor_np(W, tag, obs, rng)
+        ob_in = obs.copy()
+        for c in flip:
+            ob_in[:, c] = -ob_in[:, c]
+        act = sp.actor_np(W, tag, ob_in, rng)
+        act = act * np.array([hdg_scale, spd_scale])
         tas.append(o.st.tas[:, 0][ndone == 0].copy())
         acts.append(act[ndone == 0].copy())
         r = o.step(act)
@@ -76,13 +80,20 @@ def main():
     ap.add_argument("--tag", default="sector")
     ap.add_argument("--envs", type=int, default=200)
     ap.add_argument("--set", action="append", default=[])
+    ap.add_argument("--spd-scale", type=float, default=1.0, help="scale the actor's speed action")
+    ap.add_argument("--hdg-scale", type=float, default=1.0, help="scale the actor's heading action")
+    ap.add_argument("--flip", default="", help="comma list of obs columns negated for the actor")
+    ap.add_argument("--af", type=int, default=5, help="ACTION_FREQUENCY (sector_cr_env.py:31: 5)")
+    ap.add_argument("--dt", type=float, default=1.0, help="DT (sector_cr_env.py:77: 'DT 1')")
     a = ap.parse_args()
     for s in a.set:
         k, v = s.split("=")
-        setattr(bsx, k, float(v))
+        setattr(oba if k.startswith(("C_", "S_")) else bsx, k, float(v))
         print(f"set {k} = {v}")
     t = time.time()
-    W, rec = rollout(a.tag, a.envs)
+    flip = tuple(int(c) for c in a.flip.split(',') if c)
+    W, rec = rollout(a.tag, a.envs, spd_scale=a.spd_scale, hdg_scale=a.hdg_scale, flip=flip,
+                     af=a.af, dt=a.dt)
     print(f"rollout {a.envs} envs {time.time() - t:.1f} s")
     log = sp.log_stats(W, a.tag)
     report("ours", rec["length"], rec["average_drift"], rec["total_intrusions"])
