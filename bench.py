@@ -142,6 +142,9 @@ def main():
                          "(one RCCL all_gather of [k, E, obs+3] fp32; the last partial block is "
                          "flushed inside the timed region); 1 (default, SURVEY §8(e), BASELINE C4) "
                          "= one all_gather per RL step")
+    ap.add_argument("--transport", default="rccl", choices=("rccl", "torch"),
+                    help="N>1 over RCCL: the learner-row gather as libbsg's direct RCCL calls "
+                         "(default) or torch.distributed.all_gather_into_tensor")
     ap.add_argument("--gather-block", type=int, default=8,
                     help="N>1: also time the block-gather variant (one all_gather per this many "
                          "steps) after the headline, reported in the `gather_block` object; 0 = skip")
@@ -191,9 +194,20 @@ def main():
     gather = world > 1 and not args.no_gather
     make_local = lambda **kw: MergeVectorEnv(num_ac=args.num_ac, seed=1234,  # noqa: E731
                                              compute_cd=not args.no_cd, **kw)
+    transport_note = None
     if gather:
-        env = ShardedVectorEnv(make_local, world * E, overlap=(backend == "nccl"),
-                               steps_per_gather=args.steps_per_gather)
+        # RCCL (backend nccl): libbsg's direct RCCL gather (parallel.RcclGather); torch's
+        # all_gather_into_tensor only if that cannot start (recorded in the JSON line)
+        transport = args.transport if backend == "nccl" else "torch"
+        try:
+            env = ShardedVectorEnv(make_local, world * E, overlap=(backend == "nccl"),
+                                   steps_per_gather=args.steps_per_gather, transport=transport)
+        except Exception as ex:          # noqa: BLE001 - reported, not hidden
+            if transport != "rccl":
+                raise
+            transport_note = f"native RCCL gather failed to start ({ex}); torch.distributed used"
+            env = ShardedVectorEnv(make_local, world * E, overlap=True,
+                                   steps_per_gather=args.steps_per_gather, transport="torch")
         batch = env.local.batch
         env.reset()
     else:
@@ -315,6 +329,8 @@ def main():
                                                           else f" + {backend} all_gather") if gather else ""),
                 "backend": backend if world > 1 else None,
                 "steps_per_gather": args.steps_per_gather if gather else None,
+                "gather_transport": (env.transport if gather else None),
+                "gather_transport_note": transport_note,
             },
             "roofline": {
                 # the binding limit is fp64 VALU dependency latency; `frac`
@@ -371,7 +387,12 @@ def bench_gather_block(args, make_local, world, E, acts, backend, dev):
     import torch.distributed as dist
     from bluesky_gym.parallel import ShardedVectorEnv
     k = args.gather_block
-    env = ShardedVectorEnv(make_local, world * E, overlap=(backend == "nccl"), steps_per_gather=k)
+    transport = args.transport if backend == "nccl" else "torch"
+    try:
+        env = ShardedVectorEnv(make_local, world * E, overlap=(backend == "nccl"), steps_per_gather=k,
+                               transport=transport)
+    except Exception:                    # noqa: BLE001 - the headline line records the failure
+        env = ShardedVectorEnv(make_local, world * E, overlap=True, steps_per_gather=k)
     env.reset()
     for i in range(args.warmup):
         env.step(acts[i % 16])
@@ -393,7 +414,7 @@ def bench_gather_block(args, make_local, world, E, acts, backend, dev):
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     el = float(t[0])
     env.close()
-    return {"steps_per_gather": k, "value": world * E * args.steps / el,
+    return {"steps_per_gather": k, "transport": env.transport, "value": world * E * args.steps / el,
             "ms_per_step": el * 1e3 / args.steps, "unit": "env_steps/s",
             "note": f"one all_gather of [{k}, E, obs+3] fp32 per {k} steps (the learner sees a "
                     f"step's rows up to {k - 1} steps late); not the C4 contract"}

@@ -92,7 +92,11 @@ EXPORTED_SYMBOLS = (
     "bsg_create", "bsg_destroy", "bsg_bind", "bsg_reset", "bsg_step", "bsg_set_timing",
     "bsg_step_timing", "bsg_set_stamps", "bsg_set_wind", "bsg_ctx_obs_dim", "bsg_geom_width",
     "bsg_set_learner", "bsg_policy_sac", "bsg_lookahead_bytes", "bsg_set_lookahead",
+    "bsg_comm_last_error", "bsg_comm_unique_id", "bsg_comm_create", "bsg_comm_destroy",
+    "bsg_comm_all_gather", "bsg_comm_wait",
 )
+COMM_ID_BYTES = 128          # include/bsg.h BSG_COMM_ID_BYTES
+COMM_SLOTS = 2               # BSG_COMM_SLOTS
 
 
 class BsgSacActor(C.Structure):
@@ -161,6 +165,19 @@ def load_library(path: str | None = None):
     lib.bsg_policy_sac.restype = C.c_int32
     lib.bsg_policy_sac.argtypes = [C.POINTER(BsgSacActor), C.c_void_p, C.c_int32, C.c_int32,
                                    C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+    lib.bsg_comm_last_error.restype = C.c_char_p
+    lib.bsg_comm_last_error.argtypes = []
+    lib.bsg_comm_unique_id.restype = C.c_int32
+    lib.bsg_comm_unique_id.argtypes = [C.c_void_p]
+    lib.bsg_comm_create.restype = C.c_int32
+    lib.bsg_comm_create.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.POINTER(C.c_void_p)]
+    lib.bsg_comm_destroy.restype = C.c_int32
+    lib.bsg_comm_destroy.argtypes = [C.c_void_p]
+    lib.bsg_comm_all_gather.restype = C.c_int32
+    lib.bsg_comm_all_gather.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_int32,
+                                        C.c_void_p]
+    lib.bsg_comm_wait.restype = C.c_int32
+    lib.bsg_comm_wait.argtypes = [C.c_void_p, C.c_int32, C.c_void_p]
     if lib.bsg_abi_version() != ABI_VERSION:
         raise BsgError(f"libbsg ABI {lib.bsg_abi_version()} != expected {ABI_VERSION}")
     if path is None:
@@ -173,3 +190,10 @@ def check(rc: int, what: str):
         lib = load_library()
         msg = lib.bsg_last_error().decode(errors="replace")
         raise BsgError(f"{what} failed ({E_CODES.get(rc, rc)}): {msg}")
+
+
+def check_comm(rc: int, what: str):
+    """Like check() for the bsg_comm_* calls (their own error string)."""
+    if rc != 0:
+        msg = load_library().bsg_comm_last_error().decode(errors="replace")
+        raise BsgError(f"{what} failed ({rc}): {msg}")

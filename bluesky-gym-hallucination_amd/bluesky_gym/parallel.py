@@ -34,6 +34,69 @@ def all_gather_rows(out: torch.Tensor, local: torch.Tensor, group=None, async_op
         return dist.all_gather(parts, local, group=group, async_op=async_op)
 
 
+class RcclGather:
+    """The learner-row all-gather as direct RCCL calls from libbsg (include/bsg.h bsg_comm_*):
+    per gather one C call -- an event on the caller's stream, ncclAllGather on the comm's own
+    stream, a completion event per slot -- instead of torch.distributed's c10d enqueue
+    (~28 us of host time per call, plus ~7 us per Work.wait: profiles/r03/
+    shard_host_breakdown_k1.txt), which made a per-step gather the loop's bottleneck at
+    C4's shard sizes.  The communicator's id is broadcast once over the process group."""
+
+    def __init__(self, device, group=None):
+        import ctypes as C
+        from . import _native as nat
+        self._C, self._nat = C, nat
+        self.lib = nat.load_library()
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        idb = torch.zeros(nat.COMM_ID_BYTES, dtype=torch.uint8)
+        if self.rank == 0:
+            nat.check_comm(self.lib.bsg_comm_unique_id(C.c_void_p(idb.data_ptr())), "bsg_comm_unique_id")
+        if self.world > 1:
+            # the process group's backend decides where the id travels (RCCL: a device tensor)
+            t = idb.to(device) if dist.get_backend(group) == "nccl" else idb
+            dist.broadcast(t, src=dist.get_global_rank(group, 0) if group is not None else 0,
+                           group=group)
+            idb = t.cpu()
+        comm = C.c_void_p()
+        nat.check_comm(self.lib.bsg_comm_create(C.c_void_p(idb.data_ptr()), self.world, self.rank,
+                                                torch.device(device).index or 0, C.byref(comm)),
+                       "bsg_comm_create")
+        self._comm = comm
+        self._dev = torch.device(device).index or 0
+
+    def _stream(self):
+        from .core import _raw_stream        # torch's raw current-stream handle (no Stream object)
+        if _raw_stream is not None:
+            return self._C.c_void_p(_raw_stream(self._dev))
+        return self._C.c_void_p(torch.cuda.current_stream(self._dev).cuda_stream)
+
+    def gather(self, out: torch.Tensor, src: torch.Tensor, slot: int):
+        """out[world * src.numel()] <- every rank's src, on the comm's stream after the
+        current stream's work; returns a handle whose wait() orders the current stream."""
+        self._nat.check_comm(self.lib.bsg_comm_all_gather(
+            self._comm, self._C.c_void_p(src.data_ptr()), self._C.c_void_p(out.data_ptr()),
+            src.numel(), int(slot), self._stream()), "bsg_comm_all_gather")
+        return _RcclWork(self, int(slot))
+
+    def wait(self, slot: int):
+        self._nat.check_comm(self.lib.bsg_comm_wait(self._comm, int(slot), self._stream()),
+                             "bsg_comm_wait")
+
+    def close(self):
+        if self._comm is not None and self._comm.value:
+            self.lib.bsg_comm_destroy(self._comm)
+            self._comm = self._C.c_void_p()
+
+
+class _RcclWork:
+    def __init__(self, g, slot):
+        self._g, self._slot = g, slot
+
+    def wait(self):
+        self._g.wait(self._slot)
+
+
 class Ready:
     """Completion of one step's gathered rows.  wait(): the current stream (RCCL) or the
     host (gloo) waits until every rank's rows of that step are in the gathered buffer."""
@@ -68,11 +131,14 @@ class ShardedVectorEnv:
     gathers a partial block (call it before reading the rows of the last steps)."""
 
     def __init__(self, make_local, total_envs: int, *, overlap=True, group=None, collective=None,
-                 steps_per_gather: int = 1):
+                 steps_per_gather: int = 1, transport="torch"):
         """collective: optional ``f(out, rows) -> Work`` that starts the gather of this
         rank's rows into ``out`` asynchronously (``Work.wait()`` = a stream wait), in place
         of RCCL's all_gather_into_tensor -- another transport, or a test's delayed copy
-        (tests/test_gpu_sharded.py).  With it the overlapped path is used at any world size."""
+        (tests/test_gpu_sharded.py).  With it the overlapped path is used at any world size.
+        transport: "torch" (torch.distributed's all_gather_into_tensor) or "rccl" (RcclGather:
+        libbsg's direct RCCL calls, the low-host-overhead path; overlapped at any world
+        size)."""
         if int(steps_per_gather) < 1:
             raise ValueError("steps_per_gather must be >= 1")
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
@@ -92,7 +158,14 @@ class ShardedVectorEnv:
                                       device=dev) for _ in range(2)]
         self._blk, self._i = 0, 0
         self._collective = collective
-        self.overlap = collective is not None or (overlap and self.world > 1)
+        self._rccl = None
+        if collective is None and transport == "rccl":
+            self._rccl = RcclGather(dev, group)
+        elif transport not in ("torch", "rccl"):
+            raise ValueError(f"unknown transport {transport!r}")
+        self.transport = "rccl" if self._rccl is not None else ("custom" if collective else "torch")
+        self.overlap = (collective is not None or self._rccl is not None
+                        or (overlap and self.world > 1))
         self._work = [None, None]
 
     def _slot(self):
@@ -145,7 +218,9 @@ class ShardedVectorEnv:
         src = self._rows[blk, :n]                       # [n, n_local, d], contiguous
         out = self._gathered[blk][: self.world * n]     # rank-major: out[r * n + i]
         if self.overlap:
-            if self._collective is not None:
+            if self._rccl is not None:
+                work = self._rccl.gather(out, src, blk)
+            elif self._collective is not None:
                 work = self._collective(out, src)
             else:
                 work = all_gather_rows(out, src, self.group, async_op=True)
@@ -167,4 +242,7 @@ class ShardedVectorEnv:
             if w is not None:
                 w.wait()
         self._work = [None, None]
+        if self._rccl is not None:
+            torch.cuda.synchronize(self.local.batch.device)
+            self._rccl.close()
         self.local.close()

@@ -301,6 +301,31 @@ int32_t bsg_policy_sac(const bsg_sac_actor* actor, const float* obs, int32_t num
                        int32_t obs_stride, const float* eps, double* actions, float* log_prob,
                        void* stream);
 
+/* ---- the multi-GPU learner-row all-gather (RCCL over xGMI) -----------------------------
+ * Replaces: the reference's vectorisation is SubprocVecEnv (scripts/multi_processing_example
+ * .py:51-53), one env per process feeding one learner; here every rank's shard of envs
+ * hands its learner rows [n_local, obs+3] fp32 (bsg_set_learner) to every rank by one
+ * all-gather per RL step.  RCCL is resolved at run time (the process's
+ * librccl.so.1 -- torch's -- else ROCm's).  The gather runs on a comm-owned stream after
+ * an event on the caller's stream (overlapping the caller's next kernels); completion is
+ * tracked per slot (a ring of BSG_COMM_SLOTS row buffers), and bsg_comm_wait makes a stream
+ * wait for a slot's gather -- the consumer of the gathered rows, or the step that next
+ * overwrites that slot's rows.  All calls asynchronous; errors in bsg_comm_last_error(). */
+#define BSG_COMM_ID_BYTES 128
+#define BSG_COMM_SLOTS 2
+typedef struct bsg_comm bsg_comm;
+const char* bsg_comm_last_error(void);
+/* rank 0 draws the id (ncclGetUniqueId) and broadcasts it to the other ranks */
+int32_t bsg_comm_unique_id(uint8_t* id /* [BSG_COMM_ID_BYTES] */);
+int32_t bsg_comm_create(const uint8_t* id, int32_t nranks, int32_t rank, int32_t device,
+                        bsg_comm** out);
+int32_t bsg_comm_destroy(bsg_comm* comm);
+/* recv[nranks * count] <- every rank's send[count] (rank-major), on the comm's stream after
+ * everything `stream` has enqueued so far; slot in [0, BSG_COMM_SLOTS) */
+int32_t bsg_comm_all_gather(bsg_comm* comm, const float* send, float* recv, int64_t count,
+                            int32_t slot, void* stream);
+int32_t bsg_comm_wait(bsg_comm* comm, int32_t slot, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

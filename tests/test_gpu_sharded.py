@@ -272,3 +272,49 @@ def test_sector_overflow_noted_by_step_tensors_is_raised_at_close():
         env.step_tensors(a)                      # the persisting flag is noted, not raised
     with pytest.raises(RuntimeError, match="more aircraft"):
         env.close()
+
+
+@pytest.mark.parametrize("k", [1, 4])
+def test_rccl_transport_rows_match_one_batch(k):
+    """The native RCCL gather (parallel.RcclGather: libbsg's bsg_comm_* -- ncclAllGather on
+    a comm-owned stream, events per slot) on a one-rank communicator: the gathered rows are
+    the un-sharded batch's, bit for bit, every step through autoresets, with the gather
+    overlapped and the row ring reused (k = 1: every step; k = 4: per block).  RCCL cannot
+    run two ranks on one GPU; the rank-major layout is the same call torch's
+    all_gather_into_tensor makes (the 2-rank tests above)."""
+    import torch.distributed as dist
+    from bluesky_gym import config, core
+    from bluesky_gym.parallel import ShardedVectorEnv
+    from bluesky_gym.vector import MergeVectorEnv
+    assert not dist.is_initialized()
+    total = E_LOCAL
+    env = ShardedVectorEnv(lambda **kw: MergeVectorEnv(num_ac=32, seed=SEED, compute_cd=True,
+                                                       max_episode_steps=MAXEP, **kw),
+                           total, steps_per_gather=k, transport="rccl")
+    assert env.transport == "rccl" and env.overlap
+    acts = _actions(total)
+    got = []
+    rows, ready = env.reset()
+    ready.wait()
+    got += _rows_list(rows, total)
+    for t in range(T):
+        rows, ready = env.step(acts[t].cuda())
+        if rows is None:
+            continue
+        ready.wait()
+        got += _rows_list(rows, total)    # (.cpu() on the current stream: after the wait)
+    rows, ready = env.flush()
+    if rows is not None:
+        ready.wait()
+        got += _rows_list(rows, total)
+    env.close()
+    b = core.DeviceBatch(config.merge_config(num_ac=32, max_episode_steps=MAXEP), total,
+                         compute_cd=True, seed=SEED, learner=True)
+    b.reset()
+    want = [b.learner.cpu().numpy().copy()]
+    for t in range(T):
+        b.step(acts[t].cuda())
+        want.append(b.learner.cpu().numpy().copy())
+    got, want = np.stack(got), np.stack(want)
+    assert got.shape == want.shape
+    assert np.array_equal(got.view(np.uint32), want.view(np.uint32))

@@ -5,7 +5,8 @@ as on the 8-GPU node.  At 512 envs per GPU (C4's 8-GPU shard) the kernel is ~32 
 the host must enqueue a step in less than that or the node run is host-bound.
 
     python tools/shard_overhead_nccl.py            # E = 512 and 4096
-Prints wall per step and host time per call for batch.step and ShardedVectorEnv.step.
+Prints wall per step and host time per call for batch.step and ShardedVectorEnv.step, with
+torch's all_gather_into_tensor and with libbsg's direct RCCL gather (transport="rccl").
 """
 import os
 import sys
@@ -61,6 +62,28 @@ def main():
             if K == 8:
                 break
             s.close()
+        # libbsg's direct RCCL gather (parallel.RcclGather), one per step and per block of 8
+        for graphs in ("1", "0"):
+            os.environ["BSG_COMM_GRAPHS"] = graphs
+            for K in (1, 8):
+                r = parallel.ShardedVectorEnv(
+                    lambda **kw: MergeVectorEnv(num_ac=32, seed=1, compute_cd=True, **kw), E,
+                    steps_per_gather=K, transport="rccl")
+                r.reset()
+                w, h = timed(lambda k: r.step(bank[k % 16]))
+                print(f"E={E:5d} ShardedVectorEnv.step (bsg_comm RCCL{' graph' if graphs == '1' else ''}, "
+                      f"{K} step(s) per gather) wall/step {w:7.1f} us  host/call {h:6.1f} us", flush=True)
+                if K == 1:
+                    # the gather call alone (the step's rows of slot 0)
+                    src, out = r._rows[0, 0], r._gathered[0][:1]
+                    torch.cuda.synchronize()
+                    t0 = time.perf_counter()
+                    for k in range(T):
+                        r._rccl.gather(out, src, 0)
+                    hg = (time.perf_counter() - t0) / T * 1e6
+                    torch.cuda.synchronize()
+                    print(f"E={E:5d}   bsg_comm_all_gather alone host/call {hg:6.1f} us", flush=True)
+                r.close()
         # the enqueue cost of the collective alone
         out = torch.empty((E, s.local.batch.obs_dim + 3), dtype=torch.float32, device="cuda")
         rows = s._rows[0, 0]
