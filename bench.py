@@ -153,6 +153,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--skip-cpu-baseline", action="store_true")
     ap.add_argument("--no-c5", action="store_true", help="skip the short C5 (Descent + policy) leg")
+    ap.add_argument("--no-c5-learner", action="store_true",
+                    help="skip C5's learner-in-the-loop leg inside the default run")
     ap.add_argument("--workload", default="merge", choices=("merge", "descent-sac"),
                     help="merge: the BASELINE metric (default); descent-sac: BASELINE configs[4], "
                          "DescentEnv-v0 with the SAC learner in the loop")
@@ -478,9 +480,14 @@ def bench_c5_quick(args, dev):
     with torch.cuda.graph(g):
         it()
     wall_pol, ev_pol = timed(lambda k: g.replay())
+    learner = None
+    if not args.no_c5_learner:
+        learner = c5_learner_leg(b, W, dev, steps, warm)
     return {"workload": "DescentEnv-v0 4096 envs, 30 substeps x DT 1 s, SAME_STEP autoreset + "
-                        "final_obs (BASELINE configs[4], one GPU; learner: --workload descent-sac)",
+                        "final_obs (BASELINE configs[4], one GPU; the learner leg as "
+                        "--workload descent-sac's graph)",
             "steps": steps,
+            "env_policy_learner": learner,
             "env_only": {"value": E / wall_env, "ms_per_step": wall_env * 1e3,
                          "kernel_avg_ms": ev_env, "kernel": "bsg::step_kernel<DESCENT,1>"},
             "env_policy": {"value": E / wall_pol, "ms_per_step": wall_pol * 1e3,
@@ -488,6 +495,39 @@ def bench_c5_quick(args, dev):
                            "policy": "reference's saved Descent SAC actor, stochastic, fused HIP "
                                      "kernel bsg_policy_sac, HIP graph of sample + step"},
             "unit": "env_steps/s"}
+
+
+def c5_learner_leg(b, W, dev, steps, warm):
+    """BASELINE configs[4] end to end on this GPU, inside the default run (the
+    learner-in-the-loop figure was never driver-timed): every vector step = the SAC actor's
+    sample (fused kernel) -> bsg_step -> replay insert -> one SAC update (SB3 2.x SAC,
+    scripts/descent_env_sac.py:25-34: batch 256, lr 1e-3, gradient_steps 1; tools/sac_torch.py),
+    the iteration captured as one HIP graph; the learner's GEMMs on rocBLAS."""
+    import torch
+    sys.path.insert(0, os.path.join(REPO, "tools"))
+    import sac_torch
+    torch.backends.cuda.preferred_blas_library("cublas")
+    os.environ["DISABLE_ADDMM_CUDA_LT"] = "1"
+    sac = sac_torch.SAC(b.obs_dim, b.act_dim, dev, group=None, seed=0, lr=1e-3)
+    sac.actor.load_sb3(W, "descent")
+    rl = sac_torch.RLLoop(b, sac, learn=True, fused_policy=True)
+    rl.obs.copy_(b.obs)
+    for _ in range(8):                                # fill the buffer past one batch
+        rl.step()
+    rl.capture()
+    for _ in range(warm):
+        rl.replay()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        rl.replay()
+    torch.cuda.synchronize()
+    wall = (time.perf_counter() - t0) / steps
+    lq, la = sac.update()
+    return {"value": b.E / wall, "ms_per_step": wall * 1e3, "unit": "env_steps/s",
+            "critic_loss": float(lq), "actor_loss": float(la),
+            "learner": "SB3 SAC restated (tools/sac_torch.py): twin critics + actor 256-256, "
+                       "batch 256, one update per vector step, HIP graph"}
 
 
 def bench_descent_sac(args):

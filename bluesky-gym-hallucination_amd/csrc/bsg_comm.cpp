@@ -15,6 +15,7 @@
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
 
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -108,7 +109,18 @@ struct bsg_comm {
   bool use_graphs = true;               // BSG_COMM_GRAPHS=0: plain ncclAllGather per call
   GatherGraph graphs[kGraphCache];
   int next_graph = 0;
+  // BSG_COMM_PROFILE=1: host time of each part of bsg_comm_all_gather, printed at destroy
+  bool prof = false;
+  double t_rec = 0, t_wait = 0, t_coll = 0, t_rec2 = 0;
+  long n_calls = 0;
 };
+
+namespace {
+inline double now_us() {
+  return std::chrono::duration<double, std::micro>(
+             std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+}  // namespace
 
 namespace {
 
@@ -176,6 +188,7 @@ int32_t bsg_comm_create(const uint8_t* id, int32_t nranks, int32_t rank, int32_t
     return comm_fail(BSG_E_HIP, nccl_msg(r, e, "ncclCommInitRank"));
   }
   if (const char* gv = std::getenv("BSG_COMM_GRAPHS")) c->use_graphs = std::atoi(gv) != 0;
+  if (const char* pv = std::getenv("BSG_COMM_PROFILE")) c->prof = std::atoi(pv) != 0;
   he = hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking);
   for (int s = 0; s < BSG_COMM_SLOTS && he == hipSuccess; ++s) {
     he = hipEventCreateWithFlags(&c->step_done[s], hipEventDisableTiming);
@@ -192,6 +205,11 @@ int32_t bsg_comm_create(const uint8_t* id, int32_t nranks, int32_t rank, int32_t
 int32_t bsg_comm_destroy(bsg_comm* c) {
   if (!c) return BSG_OK;
   if (c->side) (void)hipStreamSynchronize(c->side);
+  if (c->prof && c->n_calls > 0)
+    std::fprintf(stderr, "bsg_comm profile: %ld calls, host us/call: event %.2f, stream wait %.2f, "
+                 "collective %.2f (%s), event %.2f\n", c->n_calls, c->t_rec / c->n_calls,
+                 c->t_wait / c->n_calls, c->t_coll / c->n_calls,
+                 c->use_graphs ? "graph launch" : "ncclAllGather", c->t_rec2 / c->n_calls);
   for (auto& g : c->graphs)
     if (g.exec) (void)hipGraphExecDestroy(g.exec);
   for (int s = 0; s < BSG_COMM_SLOTS; ++s) {
@@ -213,9 +231,12 @@ int32_t bsg_comm_all_gather(bsg_comm* c, const float* send, float* recv, int64_t
     return comm_fail(BSG_E_INVALID_ARG, "bsg_comm_all_gather: slot or count out of range");
   Rccl* r = rccl();
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const double t0 = c->prof ? now_us() : 0.0;
   // the gather reads what the caller's stream wrote up to here (the step's learner rows)
   hipError_t he = hipEventRecord(c->step_done[slot], st);
+  const double t1 = c->prof ? now_us() : 0.0;
   if (he == hipSuccess) he = hipStreamWaitEvent(c->side, c->step_done[slot], 0);
+  const double t2 = c->prof ? now_us() : 0.0;
   if (he != hipSuccess) return comm_fail(BSG_E_HIP, std::string("bsg_comm_all_gather: ") + hipGetErrorString(he));
   if (c->use_graphs) {
     std::string err;
@@ -227,8 +248,14 @@ int32_t bsg_comm_all_gather(bsg_comm* c, const float* send, float* recv, int64_t
     ncclResult_t e = r->all_gather(send, recv, (size_t)count, kNcclFloat32, c->nc, c->side);
     if (e != 0) return comm_fail(BSG_E_HIP, nccl_msg(r, e, "ncclAllGather"));
   }
+  const double t3 = c->prof ? now_us() : 0.0;
   he = hipEventRecord(c->gathered[slot], c->side);
   if (he != hipSuccess) return comm_fail(BSG_E_HIP, std::string("bsg_comm_all_gather: ") + hipGetErrorString(he));
+  if (c->prof) {
+    const double t4 = now_us();
+    c->t_rec += t1 - t0; c->t_wait += t2 - t1; c->t_coll += t3 - t2; c->t_rec2 += t4 - t3;
+    ++c->n_calls;
+  }
   c->pending[slot] = true;
   return BSG_OK;
 }

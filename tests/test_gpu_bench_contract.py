@@ -15,7 +15,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def test_bench_json_line():
     out = subprocess.run([sys.executable, "bench.py", "--steps", "5", "--warmup", "2",
                           "--cpu-seconds", "1"], cwd=REPO, capture_output=True, text=True,
-                         timeout=110)
+                         timeout=200)
     assert out.returncode == 0, out.stderr[-2000:]
     lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, out.stdout
@@ -41,4 +41,8 @@ def test_bench_json_line():
     c5 = r["c5"]
     assert c5["env_only"]["value"] > 0 and c5["env_policy"]["value"] > 0
     assert c5["env_policy"]["value"] <= c5["env_only"]["value"] * 1.05
+    # ... and its learner-in-the-loop leg (the whole SAC iteration as one HIP graph)
+    ln = c5["env_policy_learner"]
+    assert 0 < ln["value"] <= c5["env_policy"]["value"] * 1.05
+    assert ln["critic_loss"] == ln["critic_loss"] and ln["actor_loss"] == ln["actor_loss"]
     assert rf["scope"].startswith("per GPU") and rf["step_avg_ms"] == rf["kernel_avg_ms"]

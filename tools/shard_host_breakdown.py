@@ -3,7 +3,8 @@ path (world-size-1 NCCL group on one GPU, as tools/shard_overhead_nccl.py): the 
 of two steps ago, the learner-row pointer swap, the step launch (and its parts), the
 all-gather enqueue.  Finds what to cut so that a C4 shard's host side stays below its
 ~30 us kernel.
-    python tools/shard_host_breakdown.py [E] [steps_per_gather]
+    python tools/shard_host_breakdown.py [E] [steps_per_gather] [torch|rccl]
+(rccl: libbsg's bsg_comm transport; BSG_COMM_PROFILE=1 adds the C call's own breakdown)
 """
 import os
 import sys
@@ -29,8 +30,10 @@ def main():
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
     coll = lambda out, rows: dist.all_gather_into_tensor(out, rows, async_op=True)  # noqa: E731
     K = int(sys.argv[2]) if len(sys.argv) > 2 else 1
+    tr = sys.argv[3] if len(sys.argv) > 3 else "torch"
     s = parallel.ShardedVectorEnv(lambda **kw: MergeVectorEnv(num_ac=32, seed=1, compute_cd=True, **kw),
-                                  E, collective=coll, steps_per_gather=K)
+                                  E, collective=coll if tr == "torch" else None, steps_per_gather=K,
+                                  transport=tr)
     s.reset()
     b = s.local.batch
     bank = torch.rand((16, E, 2), dtype=torch.float64, device="cuda") * 2 - 1
@@ -68,8 +71,8 @@ def main():
     torch.cuda.synchronize()
     wall = (time.perf_counter() - t_all) / T * 1e6
     for n, v in acc.items():
-        print(f"E={E} k={K} {n:32s} {v / T * 1e6:7.2f} us/call", flush=True)
-    print(f"E={E} k={K} wall per step {wall:.1f} us (incl. the instrumentation)", flush=True)
+        print(f"E={E} k={K} {tr} {n:32s} {v / T * 1e6:7.2f} us/call", flush=True)
+    print(f"E={E} k={K} {tr} wall per step {wall:.1f} us (incl. the instrumentation)", flush=True)
     t0 = time.perf_counter()
     for k in range(T):
         b.lib.bsg_abi_version()
