@@ -79,6 +79,23 @@ class RcclGather:
             src.numel(), int(slot), self._stream()), "bsg_comm_all_gather")
         return _RcclWork(self, int(slot))
 
+    def step_gather(self, batch, actions: torch.Tensor, rows: torch.Tensor, out: torch.Tensor,
+                    slot: int):
+        """bsg_step_gather: the wait for rows[slot]'s previous gather, the learner-row pointer,
+        the step launch and this step's gather, in one C call (device spawns only)."""
+        a = actions
+        if a.dtype != torch.float64 or a.device != batch.device or not a.is_contiguous():
+            a = a.to(device=batch.device, dtype=torch.float64).contiguous()
+        batch._keep = (a, None)
+        batch.learner = rows
+        C = self._C
+        rc = self.lib.bsg_step_gather(batch._ctx, self._comm, C.c_void_p(a.data_ptr()), None,
+                                      C.c_void_p(rows.data_ptr()), C.c_void_p(out.data_ptr()),
+                                      int(slot), self._stream())
+        if rc != 0:
+            self._nat.check(rc, "bsg_step_gather")
+        return _RcclWork(self, int(slot))
+
     def wait(self, slot: int):
         self._nat.check_comm(self.lib.bsg_comm_wait(self._comm, int(slot), self._stream()),
                              "bsg_comm_wait")
@@ -164,6 +181,12 @@ class ShardedVectorEnv:
         elif transport not in ("torch", "rccl"):
             raise ValueError(f"unknown transport {transport!r}")
         self.transport = "rccl" if self._rccl is not None else ("custom" if collective else "torch")
+        # the one-call step (bsg_step_gather): the Merge / Vertical / ... kinds with device
+        # spawns (host-spawn rows and SectorCR's overflow note go through step_tensors)
+        from . import _native as nat
+        self._fused = (self._rccl is not None and self.k == 1
+                       and getattr(self.local, "spawn_mode", "device") != "host"
+                       and self.local.kind_cfg.kind != nat.ENV_SECTOR_CR)
         self.overlap = (collective is not None or self._rccl is not None
                         or (overlap and self.world > 1))
         self._work = [None, None]
@@ -200,6 +223,14 @@ class ShardedVectorEnv:
         Ready); they may be read after ready.wait(), until the step after next.  k > 1:
         (None, None) inside a block, (block, Ready) at its last step; a block stays valid
         until the end of the next block."""
+        if self._fused:
+            # transport "rccl", one gather per step, device spawns: one C call per step
+            blk = self._blk
+            out = self._gathered[blk][: self.world]
+            self._work[blk] = self._rccl.step_gather(self.local.batch, local_actions,
+                                                      self._rows[blk, 0], out, blk)
+            self._blk = 1 - blk
+            return out.view(self.total_envs, self.row_dim), Ready(self._work[blk])
         blk, i = self._slot()
         self.local.step_tensors(local_actions)
         if i + 1 < self.k:

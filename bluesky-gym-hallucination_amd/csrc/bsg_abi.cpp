@@ -471,6 +471,22 @@ int32_t bsg_step(bsg_ctx* c, const double* actions, const double* spawn, void* s
   return launch(c, bsg::MODE_STEP, actions, spawn, nullptr, stream);
 }
 
+int32_t bsg_step_gather(bsg_ctx* c, bsg_comm* comm, const double* actions, const double* spawn,
+                        float* rows, float* gathered, int32_t slot, void* stream) {
+  if (!c || !comm) return fail(BSG_E_INVALID_ARG, "bsg_step_gather: null ctx/comm%s%lld");
+  if (!c->bound) return fail(BSG_E_STATE, "bsg_step_gather: buffers not bound%s%lld");
+  if (!actions || !rows || !gathered) return fail(BSG_E_INVALID_ARG, "bsg_step_gather: null buffer%s%lld");
+  // rows[slot] was last read by the gather of two steps ago: the step writes it after that
+  if (bsg_comm_wait(comm, slot, stream) != BSG_OK)
+    return fail(BSG_E_HIP, "bsg_step_gather: %s%lld", bsg_comm_last_error());
+  c->bufs.learner = rows;
+  if (int r = launch(c, bsg::MODE_STEP, actions, spawn, nullptr, stream)) return r;
+  const int64_t count = (int64_t)c->cfg.num_envs * (c->obs_dim + 3);
+  if (bsg_comm_all_gather(comm, rows, gathered, count, slot, stream) != BSG_OK)
+    return fail(BSG_E_HIP, "bsg_step_gather: %s%lld", bsg_comm_last_error());
+  return BSG_OK;
+}
+
 int32_t bsg_set_wind(bsg_ctx* c, const bsg_wind* w) {
   if (!c) return fail(BSG_E_INVALID_ARG, "bsg_set_wind: null ctx%s%lld");
   const int base = bsg_obs_dim(c->cfg.env_kind, c->cfg.num_ac, c->cfg.num_ac_state);

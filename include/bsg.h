@@ -325,6 +325,12 @@ int32_t bsg_comm_destroy(bsg_comm* comm);
 int32_t bsg_comm_all_gather(bsg_comm* comm, const float* send, float* recv, int64_t count,
                             int32_t slot, void* stream);
 int32_t bsg_comm_wait(bsg_comm* comm, int32_t slot, void* stream);
+/* One RL step of a shard and the gather of its learner rows in one call (the host side of
+ * a C4 step: ~one launch instead of a wait, a pointer swap, a launch and a gather):
+ * bsg_comm_wait(slot) [the gather that last read rows[slot]], learner rows <- rows,
+ * bsg_step, bsg_comm_all_gather(rows -> gathered, num_envs * (obs_dim + 3), slot). */
+int32_t bsg_step_gather(bsg_ctx* ctx, bsg_comm* comm, const double* actions, const double* spawn,
+                        float* rows, float* gathered, int32_t slot, void* stream);
 
 #ifdef __cplusplus
 }
