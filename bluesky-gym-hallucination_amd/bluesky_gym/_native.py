@@ -96,7 +96,7 @@ EXPORTED_SYMBOLS = (
     "bsg_comm_all_gather", "bsg_comm_wait", "bsg_step_gather",
 )
 COMM_ID_BYTES = 128          # include/bsg.h BSG_COMM_ID_BYTES
-COMM_SLOTS = 2               # BSG_COMM_SLOTS
+COMM_SLOTS = 16              # BSG_COMM_SLOTS
 
 
 class BsgSacActor(C.Structure):

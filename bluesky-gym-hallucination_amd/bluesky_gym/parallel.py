@@ -82,19 +82,19 @@ class RcclGather:
     def step_gather(self, batch, actions: torch.Tensor, rows: torch.Tensor, out: torch.Tensor,
                     slot: int):
         """bsg_step_gather: the wait for rows[slot]'s previous gather, the learner-row pointer,
-        the step launch and this step's gather, in one C call (device spawns only)."""
+        the step launch and this step's gather, in one C call (device spawns only).  Returns
+        nothing: the caller keeps one handle per slot (ShardedVectorEnv._ready)."""
         a = actions
-        if a.dtype != torch.float64 or a.device != batch.device or not a.is_contiguous():
+        if a.dtype is not torch.float64 or not a.is_contiguous() or a.device != batch.device:
             a = a.to(device=batch.device, dtype=torch.float64).contiguous()
         batch._keep = (a, None)
         batch.learner = rows
         C = self._C
         rc = self.lib.bsg_step_gather(batch._ctx, self._comm, C.c_void_p(a.data_ptr()), None,
                                       C.c_void_p(rows.data_ptr()), C.c_void_p(out.data_ptr()),
-                                      int(slot), self._stream())
+                                      slot, self._stream())
         if rc != 0:
             self._nat.check(rc, "bsg_step_gather")
-        return _RcclWork(self, int(slot))
 
     def wait(self, slot: int):
         self._nat.check_comm(self.lib.bsg_comm_wait(self._comm, int(slot), self._stream()),
@@ -169,11 +169,6 @@ class ShardedVectorEnv:
         d = b.obs_dim + 3
         self.row_dim = d
         dev = b.device
-        # rows[blk, i]: the kernel's learner output of step i of block blk (a ring of 2 blocks)
-        self._rows = torch.zeros((2, self.k, self.n_local, d), dtype=torch.float32, device=dev)
-        self._gathered = [torch.empty((self.world * self.k, self.n_local, d), dtype=torch.float32,
-                                      device=dev) for _ in range(2)]
-        self._blk, self._i = 0, 0
         self._collective = collective
         self._rccl = None
         if collective is None and transport == "rccl":
@@ -189,7 +184,23 @@ class ShardedVectorEnv:
                        and self.local.kind_cfg.kind != nat.ENV_SECTOR_CR)
         self.overlap = (collective is not None or self._rccl is not None
                         or (overlap and self.world > 1))
-        self._work = [None, None]
+        # rows[blk, i]: the kernel's learner output of step i of block blk, a ring of R blocks:
+        # R = BSG_COMM_SLOTS for the fused per-step gather (the step that rewrites a slot comes
+        # R steps after its gather, which a fence the stream already waited for covers: one
+        # stream wait per R/2 steps, bsg_comm.cpp), else 2
+        R = nat.COMM_SLOTS if self._fused else 2
+        self._nslots = R
+        self._rows = torch.zeros((R, self.k, self.n_local, d), dtype=torch.float32, device=dev)
+        self._gathered = torch.empty((R, self.world * self.k, self.n_local, d), dtype=torch.float32,
+                                     device=dev)
+        self._blk, self._i = 0, 0
+        self._work = [None] * R
+        if self._fused:
+            # per slot, made once: the row block the kernel writes, the gathered view step()
+            # returns and its completion handle (the host side of a step is one C call)
+            self._slot_rows = [self._rows[s, 0] for s in range(R)]
+            self._views = [self._gathered[s].view(self.total_envs, d) for s in range(R)]
+            self._ready = [Ready(_RcclWork(self._rccl, s)) for s in range(R)]
 
     def _slot(self):
         """Point the kernel's learner output at the next slot; before the first write into a
@@ -200,6 +211,8 @@ class ShardedVectorEnv:
             if w is not None:
                 w.wait()
                 self._work[blk] = None
+            elif self._fused:
+                self._rccl.wait(blk)     # (a fused step's gather of this slot: no Work object)
         self.local.batch.set_learner(self._rows[blk, i])
         return blk, i
 
@@ -224,13 +237,13 @@ class ShardedVectorEnv:
         (None, None) inside a block, (block, Ready) at its last step; a block stays valid
         until the end of the next block."""
         if self._fused:
-            # transport "rccl", one gather per step, device spawns: one C call per step
+            # transport "rccl", one gather per step, device spawns: one C call per step (the
+            # wait for the slot's previous gather is libbsg's, bsg_step_gather)
             blk = self._blk
-            out = self._gathered[blk][: self.world]
-            self._work[blk] = self._rccl.step_gather(self.local.batch, local_actions,
-                                                      self._rows[blk, 0], out, blk)
-            self._blk = 1 - blk
-            return out.view(self.total_envs, self.row_dim), Ready(self._work[blk])
+            self._rccl.step_gather(self.local.batch, local_actions, self._slot_rows[blk],
+                                   self._gathered[blk], blk)
+            self._blk = blk + 1 if blk + 1 < self._nslots else 0
+            return self._views[blk], self._ready[blk]
         blk, i = self._slot()
         self.local.step_tensors(local_actions)
         if i + 1 < self.k:
@@ -263,7 +276,7 @@ class ShardedVectorEnv:
         else:
             all_gather_rows(out, src, self.group)
             ready = Ready()
-        self._blk, self._i = 1 - blk, 0
+        self._blk, self._i = (blk + 1) % self._nslots, 0
         if self.k == 1:
             return out.view(self.total_envs, self.row_dim), ready
         return out.view(self.world, n, self.n_local, self.row_dim).permute(1, 0, 2, 3), ready
@@ -272,7 +285,7 @@ class ShardedVectorEnv:
         for w in self._work:
             if w is not None:
                 w.wait()
-        self._work = [None, None]
+        self._work = [None] * self._nslots
         if self._rccl is not None:
             torch.cuda.synchronize(self.local.batch.device)
             self._rccl.close()

@@ -143,9 +143,19 @@ int la_prepare(bsg_ctx* c, hipStream_t st) {
     c->la_was_active = act;
   }
   if (c->memo_dirty && c->bufs.memo_cache) {
+    // Not into a graph: a launch being captured turns the lookahead off (la_captured), and
+    // at that on -> off transition the cache needs no reset -- the intruder entries were
+    // invalidated when the lookahead came on and never written since (its blocks keep their
+    // own memo), the ownship entries stayed current.  A reset captured into the graph
+    // measured inexact replays (tests/test_gpu_lookahead.py
+    // ::test_lookahead_off_once_a_launch_is_captured, profiles/r04/capture_replay.txt); the
+    // flag stays set, so the next launch outside a graph resets the cache as before.
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    hipError_t e = hipStreamIsCapturing(st, &cs);
+    if (e != hipSuccess) return hip_fail(e, "hipStreamIsCapturing");
+    if (cs != hipStreamCaptureStatusNone) return BSG_OK;
     const size_t EN = (size_t)c->cfg.num_envs * c->cfg.num_ac;
-    hipError_t e = hipMemsetAsync(c->bufs.memo_cache, 0xFF,
-                                  8 * (2 * EN + 4 * (size_t)c->cfg.num_envs), st);
+    e = hipMemsetAsync(c->bufs.memo_cache, 0xFF, 8 * (2 * EN + 4 * (size_t)c->cfg.num_envs), st);
     if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(memo_cache)");
   }
   c->memo_dirty = false;
@@ -476,7 +486,8 @@ int32_t bsg_step_gather(bsg_ctx* c, bsg_comm* comm, const double* actions, const
   if (!c || !comm) return fail(BSG_E_INVALID_ARG, "bsg_step_gather: null ctx/comm%s%lld");
   if (!c->bound) return fail(BSG_E_STATE, "bsg_step_gather: buffers not bound%s%lld");
   if (!actions || !rows || !gathered) return fail(BSG_E_INVALID_ARG, "bsg_step_gather: null buffer%s%lld");
-  // rows[slot] was last read by the gather of two steps ago: the step writes it after that
+  // rows[slot] was last read by the gather of BSG_COMM_SLOTS steps ago (a ring): the step
+  // writes it after that gather (usually known complete already: no stream wait)
   if (bsg_comm_wait(comm, slot, stream) != BSG_OK)
     return fail(BSG_E_HIP, "bsg_step_gather: %s%lld", bsg_comm_last_error());
   c->bufs.learner = rows;

@@ -6,10 +6,23 @@
 // gather cost ~35 us per step (c10d's enqueue ~28 us + Work.wait ~7 us,
 // profiles/r03/shard_host_breakdown_k1.txt) against a 512-env shard's ~28 us kernel: one
 // gather per step made the loop host-bound.  Here one call records an event on the
-// caller's stream, makes the comm's stream wait for it, enqueues ncclAllGather there and
-// records the gather's completion per slot; bsg_comm_wait makes a stream wait for a slot's
-// gather (the consumer, or the step that next overwrites those rows).  All asynchronous.
-//
+// caller's stream, makes the comm's own stream wait for it and enqueues ncclAllGather there.
+// Completion is tracked by gather sequence number: a fence event is recorded behind every
+// BSG_COMM_SLOTS/2-th gather, and bsg_comm_wait makes a stream wait for the oldest fence that
+// covers the slot's last gather -- with a ring of BSG_COMM_SLOTS row buffers the step that
+// next overwrites a slot finds its gather already covered by a fence its stream waited for,
+// so that stream wait is issued once per BSG_COMM_SLOTS/2 steps instead of every step.
+// The comm's stream has the greatest priority: one of the default priority may share a
+// hardware queue with the caller's stream, which puts each gather between two steps.
+// Measured (tools/probe/hostapi_probe.cpp with a 28 us kernel standing in for the 512-env
+// shard, profiles/r04/comm/): 52.4 us per step with an event pair and a reverse wait every
+// step on a default-priority stream (round 3's scheme), 35.6 us with the fences and the
+// priority, 30.0 us for the launches alone; the product path (tools/shard_flag_sweep.py)
+// 49.4 -> 33.4 us per step at 512 envs, 70.4 -> 55.6 at 4096.  (A completion value published
+// by the step kernel's last workgroup instead of the event pair -- every workgroup counting
+// itself out with a device-scope atomic -- tied at 512 envs and cost +58 us at 4096: the
+// atomics on one address from 2,048 workgroups across eight XCDs serialise.)  All
+// asynchronous.
 // RCCL is resolved at run time: the librccl.so.1 the process already loaded (torch's) if
 // any, else ROCm's.  One copy of RCCL per process, no link-time dependency.
 #include <dlfcn.h>
@@ -99,14 +112,25 @@ struct GatherGraph {
 };
 constexpr int kGraphCache = 8;
 
+constexpr int kFences = 4;              // fence events in flight (a ring)
+constexpr int64_t kFenceEvery = BSG_COMM_SLOTS / 2;
+constexpr int kWaited = 4;              // streams whose waited-for gather is remembered
+
 struct bsg_comm {
   ncclComm_t nc = nullptr;
   int nranks = 0, rank = 0, device = 0;
-  hipStream_t side = nullptr;           // the gathers' stream
-  hipEvent_t step_done[BSG_COMM_SLOTS] = {};
-  hipEvent_t gathered[BSG_COMM_SLOTS] = {};
-  bool pending[BSG_COMM_SLOTS] = {};    // gathered[slot] recorded and not yet waited for
-  bool use_graphs = true;               // BSG_COMM_GRAPHS=0: plain ncclAllGather per call
+  hipStream_t side = nullptr;           // the gathers' stream (greatest priority)
+  hipEvent_t step_done[BSG_COMM_SLOTS] = {};   // caller-stream events (bsg_comm_all_gather)
+  // gather g (1-based, in issue order) is covered by every fence recorded after it
+  int64_t gseq = 0;                     // gathers issued
+  int64_t slot_seq[BSG_COMM_SLOTS] = {};   // the last gather that read each slot (0: none)
+  hipEvent_t fence[kFences] = {};
+  int64_t fence_seq[kFences] = {};      // the gather each fence was recorded behind (0: none)
+  int next_fence = 0;
+  int64_t last_fence = 0;
+  struct Waited { void* stream; int64_t seq; } waited[kWaited] = {};
+  int next_waited = 0;
+  bool use_graphs = false;              // BSG_COMM_GRAPHS=1: the gather as a replayed HIP graph
   GatherGraph graphs[kGraphCache];
   int next_graph = 0;
   // BSG_COMM_PROFILE=1: host time of each part of bsg_comm_all_gather, printed at destroy
@@ -146,6 +170,69 @@ hipGraphExec_t gather_graph(bsg_comm* c, Rccl* r, const void* send, void* recv, 
   g.recv = recv;
   g.count = count;
   return g.exec;
+}
+
+// the gather itself on c->side (a replayed graph or a plain ncclAllGather)
+int enqueue_gather(bsg_comm* c, Rccl* r, const float* send, float* recv, int64_t count,
+                   const char* who) {
+  if (c->use_graphs) {
+    std::string err;
+    hipGraphExec_t ex = gather_graph(c, r, send, recv, count, &err);
+    if (!ex) return comm_fail(BSG_E_HIP, std::string(who) + ": " + err);
+    hipError_t he = hipGraphLaunch(ex, c->side);
+    if (he != hipSuccess) return comm_fail(BSG_E_HIP, std::string("hipGraphLaunch: ") + hipGetErrorString(he));
+    return BSG_OK;
+  }
+  ncclResult_t e = r->all_gather(send, recv, (size_t)count, kNcclFloat32, c->nc, c->side);
+  if (e != 0) return comm_fail(BSG_E_HIP, nccl_msg(r, e, "ncclAllGather"));
+  return BSG_OK;
+}
+
+// a fence event behind everything enqueued on c->side so far
+int record_fence(bsg_comm* c) {
+  const int k = c->next_fence;
+  hipError_t he = hipEventRecord(c->fence[k], c->side);
+  if (he != hipSuccess) return comm_fail(BSG_E_HIP, std::string("hipEventRecord(fence): ") + hipGetErrorString(he));
+  c->fence_seq[k] = c->gseq;
+  c->last_fence = c->gseq;
+  c->next_fence = (k + 1) % kFences;
+  return BSG_OK;
+}
+
+// bookkeeping after gather gseq + 1 read `slot`
+int gathered(bsg_comm* c, int slot) {
+  c->slot_seq[slot] = ++c->gseq;
+  if (c->gseq - c->last_fence >= kFenceEvery) return record_fence(c);
+  return BSG_OK;
+}
+
+int64_t* waited_mark(bsg_comm* c, void* stream) {
+  for (auto& w : c->waited)
+    if (w.stream == stream && w.seq > 0) return &w.seq;
+  auto& w = c->waited[c->next_waited];
+  c->next_waited = (c->next_waited + 1) % kWaited;
+  w.stream = stream;
+  w.seq = 0;
+  return &w.seq;
+}
+
+// `stream` waits until gather `need` is complete: nothing if it already waited for a fence
+// that covers it, else for the oldest fence that does (recorded now if none does yet)
+int wait_for(bsg_comm* c, int64_t need, void* stream) {
+  if (need <= 0) return BSG_OK;
+  int64_t* w = waited_mark(c, stream);
+  if (*w >= need) return BSG_OK;
+  int best = -1;
+  for (int k = 0; k < kFences; ++k)
+    if (c->fence_seq[k] >= need && (best < 0 || c->fence_seq[k] < c->fence_seq[best])) best = k;
+  if (best < 0) {
+    if (int rc = record_fence(c)) return rc;
+    best = (c->next_fence + kFences - 1) % kFences;
+  }
+  hipError_t he = hipStreamWaitEvent(reinterpret_cast<hipStream_t>(stream), c->fence[best], 0);
+  if (he != hipSuccess) return comm_fail(BSG_E_HIP, std::string("hipStreamWaitEvent: ") + hipGetErrorString(he));
+  *w = c->fence_seq[best];
+  return BSG_OK;
 }
 
 }  // namespace
@@ -189,11 +276,13 @@ int32_t bsg_comm_create(const uint8_t* id, int32_t nranks, int32_t rank, int32_t
   }
   if (const char* gv = std::getenv("BSG_COMM_GRAPHS")) c->use_graphs = std::atoi(gv) != 0;
   if (const char* pv = std::getenv("BSG_COMM_PROFILE")) c->prof = std::atoi(pv) != 0;
-  he = hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking);
-  for (int s = 0; s < BSG_COMM_SLOTS && he == hipSuccess; ++s) {
+  int least = 0, greatest = 0;
+  he = hipDeviceGetStreamPriorityRange(&least, &greatest);
+  if (he == hipSuccess) he = hipStreamCreateWithPriority(&c->side, hipStreamNonBlocking, greatest);
+  for (int s = 0; s < BSG_COMM_SLOTS && he == hipSuccess; ++s)
     he = hipEventCreateWithFlags(&c->step_done[s], hipEventDisableTiming);
-    if (he == hipSuccess) he = hipEventCreateWithFlags(&c->gathered[s], hipEventDisableTiming);
-  }
+  for (int k = 0; k < kFences && he == hipSuccess; ++k)
+    he = hipEventCreateWithFlags(&c->fence[k], hipEventDisableTiming);
   if (he != hipSuccess) {
     bsg_comm_destroy(c);
     return comm_fail(BSG_E_HIP, std::string("bsg_comm_create: ") + hipGetErrorString(he));
@@ -207,15 +296,15 @@ int32_t bsg_comm_destroy(bsg_comm* c) {
   if (c->side) (void)hipStreamSynchronize(c->side);
   if (c->prof && c->n_calls > 0)
     std::fprintf(stderr, "bsg_comm profile: %ld calls, host us/call: event %.2f, stream wait %.2f, "
-                 "collective %.2f (%s), event %.2f\n", c->n_calls, c->t_rec / c->n_calls,
-                 c->t_wait / c->n_calls, c->t_coll / c->n_calls,
+                 "collective %.2f (%s), fence bookkeeping %.2f\n", c->n_calls,
+                 c->t_rec / c->n_calls, c->t_wait / c->n_calls, c->t_coll / c->n_calls,
                  c->use_graphs ? "graph launch" : "ncclAllGather", c->t_rec2 / c->n_calls);
   for (auto& g : c->graphs)
     if (g.exec) (void)hipGraphExecDestroy(g.exec);
-  for (int s = 0; s < BSG_COMM_SLOTS; ++s) {
+  for (int s = 0; s < BSG_COMM_SLOTS; ++s)
     if (c->step_done[s]) (void)hipEventDestroy(c->step_done[s]);
-    if (c->gathered[s]) (void)hipEventDestroy(c->gathered[s]);
-  }
+  for (int k = 0; k < kFences; ++k)
+    if (c->fence[k]) (void)hipEventDestroy(c->fence[k]);
   if (c->side) (void)hipStreamDestroy(c->side);
   if (c->nc) {
     if (Rccl* r = rccl()) r->comm_destroy(c->nc);
@@ -238,35 +327,21 @@ int32_t bsg_comm_all_gather(bsg_comm* c, const float* send, float* recv, int64_t
   if (he == hipSuccess) he = hipStreamWaitEvent(c->side, c->step_done[slot], 0);
   const double t2 = c->prof ? now_us() : 0.0;
   if (he != hipSuccess) return comm_fail(BSG_E_HIP, std::string("bsg_comm_all_gather: ") + hipGetErrorString(he));
-  if (c->use_graphs) {
-    std::string err;
-    hipGraphExec_t ex = gather_graph(c, r, send, recv, count, &err);
-    if (!ex) return comm_fail(BSG_E_HIP, "bsg_comm_all_gather: " + err);
-    he = hipGraphLaunch(ex, c->side);
-    if (he != hipSuccess) return comm_fail(BSG_E_HIP, std::string("hipGraphLaunch: ") + hipGetErrorString(he));
-  } else {
-    ncclResult_t e = r->all_gather(send, recv, (size_t)count, kNcclFloat32, c->nc, c->side);
-    if (e != 0) return comm_fail(BSG_E_HIP, nccl_msg(r, e, "ncclAllGather"));
-  }
+  if (int rc = enqueue_gather(c, r, send, recv, count, "bsg_comm_all_gather")) return rc;
   const double t3 = c->prof ? now_us() : 0.0;
-  he = hipEventRecord(c->gathered[slot], c->side);
-  if (he != hipSuccess) return comm_fail(BSG_E_HIP, std::string("bsg_comm_all_gather: ") + hipGetErrorString(he));
+  if (int rc = gathered(c, slot)) return rc;
   if (c->prof) {
     const double t4 = now_us();
     c->t_rec += t1 - t0; c->t_wait += t2 - t1; c->t_coll += t3 - t2; c->t_rec2 += t4 - t3;
     ++c->n_calls;
   }
-  c->pending[slot] = true;
   return BSG_OK;
 }
 
 int32_t bsg_comm_wait(bsg_comm* c, int32_t slot, void* stream) {
   if (!c) return comm_fail(BSG_E_INVALID_ARG, "bsg_comm_wait: null comm");
   if (slot < 0 || slot >= BSG_COMM_SLOTS) return comm_fail(BSG_E_INVALID_ARG, "bsg_comm_wait: slot out of range");
-  if (!c->pending[slot]) return BSG_OK;      // nothing gathered into this slot yet
-  hipError_t he = hipStreamWaitEvent(reinterpret_cast<hipStream_t>(stream), c->gathered[slot], 0);
-  if (he != hipSuccess) return comm_fail(BSG_E_HIP, std::string("bsg_comm_wait: ") + hipGetErrorString(he));
-  return BSG_OK;
+  return wait_for(c, c->slot_seq[slot], stream);
 }
 
 }  // extern "C"

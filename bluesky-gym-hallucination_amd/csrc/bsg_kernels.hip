@@ -412,7 +412,11 @@ __device__ __forceinline__ void substep(AC& s, Memo& m, double dt, const RouteRe
     // cover the squares' rounding.  (Making this block straight-line for every lane --
     // selects instead of the branch -- measured ~170 cycles slower per substep:
     // tools/probe/substep_probe.hip.)
+#if defined(BSG_EXP_NONEED) && BSG_EXP_NONEED
+    const bool need = false && (!far || half > 45.0);   // timing experiment only: wrong results
+#else
     const bool need = !far || half > 45.0;
+#endif
     if (need) {
       bool reached = false;
       const double g = npmax(0.0001, fabs(gsv));
@@ -2376,6 +2380,9 @@ __global__ __launch_bounds__(64 * CDW) BSG_WPE void step_kernel(KParams p) {
           s.tas = s_la.tas; s.cas = s_la.cas; s.vs = s_la.vs; s.ax = s_la.ax;
           s.ap_trk = s_la.ap_trk; s.nav = s_la.nav;
         } else {
+#if defined(BSG_EXP_NOOWN) && BSG_EXP_NOOWN
+          if (j > 0)   // timing experiment only: the ownship does not move (wrong results)
+#endif
           propagate<KIND, WIND>(p, e, j, a, s, ev, sub_reward, sub_done, act, mc, oat, mcache);
         }
       }

@@ -306,13 +306,17 @@ int32_t bsg_policy_sac(const bsg_sac_actor* actor, const float* obs, int32_t num
  * .py:51-53), one env per process feeding one learner; here every rank's shard of envs
  * hands its learner rows [n_local, obs+3] fp32 (bsg_set_learner) to every rank by one
  * all-gather per RL step.  RCCL is resolved at run time (the process's
- * librccl.so.1 -- torch's -- else ROCm's).  The gather runs on a comm-owned stream after
- * an event on the caller's stream (overlapping the caller's next kernels); completion is
- * tracked per slot (a ring of BSG_COMM_SLOTS row buffers), and bsg_comm_wait makes a stream
- * wait for a slot's gather -- the consumer of the gathered rows, or the step that next
- * overwrites that slot's rows.  All calls asynchronous; errors in bsg_comm_last_error(). */
+ * librccl.so.1 -- torch's -- else ROCm's).  The gather runs on a comm-owned stream of the
+ * greatest priority after the caller's work (overlapping the caller's next kernels);
+ * completion is tracked per slot (a ring of BSG_COMM_SLOTS row buffers) through fence
+ * events recorded every BSG_COMM_SLOTS/2 gathers, and bsg_comm_wait makes a stream wait for
+ * a slot's last gather -- the consumer of the gathered rows, or the step that next
+ * overwrites that slot's rows (a no-op when that stream already waited for a fence covering
+ * it).  All calls asynchronous; errors in bsg_comm_last_error().
+ * Environment: BSG_COMM_GRAPHS=1 (the gather as a replayed HIP graph), BSG_COMM_PROFILE=1
+ * (host time per part, printed at destroy). */
 #define BSG_COMM_ID_BYTES 128
-#define BSG_COMM_SLOTS 2
+#define BSG_COMM_SLOTS 16
 typedef struct bsg_comm bsg_comm;
 const char* bsg_comm_last_error(void);
 /* rank 0 draws the id (ncclGetUniqueId) and broadcasts it to the other ranks */

@@ -11,7 +11,7 @@ if [ "$mode" = build ]; then
   for kv in "$@"; do
     k=${kv%%=*}; d=${kv#*=}; x=""
     case "$d" in *:*) x=${d#*:}; d=${d%%:*};; esac
-    ( o=$OUT/obj_$k && mkdir -p $o && /opt/rocm/bin/hipcc $FLAGS $x -DBSG_KIND_TU=0 -c -o $o/k.o $d/bsg_kernels.hip && /opt/rocm/bin/hipcc $FLAGS $x -x hip -c -o $o/d.o $d/bsg_dispatch.cpp && /opt/rocm/bin/hipcc $FLAGS $x -x hip -c -o $o/a.o $d/bsg_abi.cpp && /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o $OUT/libbsg_$k.so $o/k.o $o/d.o $o/a.o ) &
+    ( o=$OUT/obj_$k && mkdir -p $o && /opt/rocm/bin/hipcc $FLAGS $x -DBSG_KIND_TU=0 -c -o $o/k.o $d/bsg_kernels.hip && /opt/rocm/bin/hipcc $FLAGS $x -x hip -c -o $o/d.o $d/bsg_dispatch.cpp && /opt/rocm/bin/hipcc $FLAGS $x -x hip -c -o $o/a.o $d/bsg_abi.cpp && /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o $OUT/libbsg_$k.so $o/k.o $o/d.o $o/a.o build/obj/bsg_comm.o build/obj/bsg_policy.o -ldl ) &
   done
   wait
   ls -la $OUT
