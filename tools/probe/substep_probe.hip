@@ -6,7 +6,13 @@
 //         -mllvm -disable-machine-licm tools/probe/substep_probe.hip -o tools/probe/substep_probe
 // section marks inside substep (bsg_kernels.hip BSG_SUBSTEP_MARK): s_memtime per mark
 __device__ long long g_mark[8];
+#ifdef PROBE_CUT
+// instruction-count builds (tools/probe/pmc_sections.sh): the substep ends at mark PROBE_CUT, so
+// rocprofv3's SQ_INSTS_* of consecutive cuts give each section's dynamic instruction count
+#define BSG_SUBSTEP_MARK(i) do { g_mark[i] = __builtin_amdgcn_s_memtime(); if ((i) == PROBE_CUT) return; } while (0)
+#else
 #define BSG_SUBSTEP_MARK(i) do { g_mark[i] = __builtin_amdgcn_s_memtime(); } while (0)
+#endif
 #include "../../bluesky-gym-hallucination_amd/csrc/bsg_kernels.hip"
 
 #include <cstdio>
