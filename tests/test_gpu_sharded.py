@@ -72,7 +72,7 @@ def _shard_worker(rank, world, port, overlap, k, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("overlap,k", [(True, 1), (False, 1), (True, 4)])
+@pytest.mark.parametrize("overlap,k", [(True, 1), (False, 1), (True, 4), (True, 8)])
 def test_sharded_rows_match_one_batch(overlap, k):
     """k = steps_per_gather: one all-gather per step, or per block of 4 steps."""
     import torch.multiprocessing as mp
@@ -274,7 +274,7 @@ def test_sector_overflow_noted_by_step_tensors_is_raised_at_close():
         env.close()
 
 
-@pytest.mark.parametrize("k", [1, 4])
+@pytest.mark.parametrize("k", [1, 4, 8])
 def test_rccl_transport_rows_match_one_batch(k):
     """The native RCCL gather (parallel.RcclGather: libbsg's bsg_comm_* -- ncclAllGather on
     a comm-owned stream, events per slot) on a one-rank communicator: the gathered rows are

@@ -103,7 +103,7 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("k,overlap", [(1, True), (1, False), (3, True), (3, False)])
+@pytest.mark.parametrize("k,overlap", [(1, True), (1, False), (3, True), (3, False), (8, True)])
 def test_blocks_deliver_every_step_in_order(k, overlap):
     import torch.multiprocessing as mp
     world = 2
