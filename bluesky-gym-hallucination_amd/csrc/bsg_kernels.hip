@@ -364,13 +364,91 @@ __device__ __forceinline__ void memo_lnav(Memo& m, const AC& s, const RouteRegs&
 #define BSG_SUBSTEP_MARK(i) do { } while (0)
 #endif
 
+// The heading update with its three pymod360 (substep).  fh (wave-uniform, propagate):
+// every lane has |ap_trk| < 360 and hdg in [0, 360], so hdg_cmd = pymod360(ap_trk) is one
+// select, and delhdg's and the new heading's arguments lie in [-180, 540] (two selects
+// each; |dt * turnrate| < |delhdg| <= 180 when it is added) -- one uniform branch here
+// instead of three ~150-cycle fmod branches.  WIND: hdg_cmd is the wind-corrected command.
+template <bool WIND>
+__device__ __forceinline__ void turn_update(AC& s, Memo& m, double dt, bool fh, double hdg_cmd) {
+  auto turn = [&](auto fh_tag) {
+    constexpr bool F = decltype(fh_tag)::value;
+    if constexpr (!WIND) hdg_cmd = F ? pymod360_s(s.ap_trk) : pymod360(s.ap_trk);
+    const double da = hdg_cmd - s.hdg + 180.0;
+    const double delhdg = (F ? pymod360_r(da) : pymod360(da)) - 180.0;
+    // |delhdg| > |dt*turnrate| is false at delhdg == 0 whatever turnrate is: a straight
+    // flying aircraft needs no turn rate (whose division would sit on the tas -> heading
+    // -> position chain)
+    bool swhdgsel = false;
+    double turnrate = 0.0;
+    if (delhdg != 0.0) {
+      turnrate = (G0 * TAN_BANKDEF / npmax(s.tas, EPS_SPD)) * kR2D;
+      swhdgsel = fabs(delhdg) > fabs(dt * turnrate);
+    }
+    const double ha = swhdgsel ? s.hdg + sgnmul(true, delhdg, dt * turnrate) : hdg_cmd;
+    s.hdg = F ? pymod360_r(ha) : pymod360(ha);
+  };
+  if (!WIND && fh) turn(std::true_type{});
+  else turn(std::false_type{});
+  m.phdg = s.hdg >= 360.0 ? s.hdg - 360.0 : s.hdg;   // pymod360 of a [0, 360] value
+}
+
+// update_groundspeed + update_pos (substep), with the altitude update of a climbing /
+// descending aircraft (swaltsel; else alt = allow_h -- the cruise substep passes its own
+// altitude)
+template <bool WIND, bool HMEMO>
+__device__ __forceinline__ void position_update(AC& s, Memo& m, double dt, double vwn, double vwe,
+                                                bool swaltsel, double allow_h) {
+  if constexpr (HMEMO) {
+    if (bits(s.hdg) != m.hdg_bits) {      // straight flight keeps its heading trig
+      sincos_t(s.hdg * kD2R, &m.shdg, &m.chdg);
+      m.hdg_bits = bits(s.hdg);
+    }
+  } else {
+    // LNAV lanes re-aim at the waypoint's bearing every substep, so some lane of a wave
+    // always misses the memo: its branch would only add latency
+    sincos_t(s.hdg * kD2R, &m.shdg, &m.chdg);
+  }
+  const double shdg = m.shdg, chdg = m.chdg;
+  double gsnorth = s.tas * chdg;
+  double gseast = s.tas * shdg;
+  if constexpr (WIND) {
+    const bool applywind = s.alt > 50.0 * FT;     // airborne (altitude before update_pos)
+    gsnorth = gsnorth + vwn * (double)applywind;
+    gseast = gseast + vwe * (double)applywind;
+    if (applywind) {
+      s.gs = sqrt(gsnorth * gsnorth + gseast * gseast);
+      s.trk = pymod360_s(atan2(gseast, gsnorth) * kR2D);
+    } else {
+      s.gs = s.tas;
+      s.trk = s.hdg;
+    }
+  }
+  if (swaltsel) s.alt = divk(rint((s.alt + s.vs * dt) * 1e6), 1e6);   // a branch: level flight
+  else s.alt = allow_h;                                            // skips the division
+  BSG_SUBSTEP_MARK(4);
+  // (divk_f: the numerators are finite -- tas is clamped by the envelope, |cos| <= 1)
+  s.lat = s.lat + divk_f(dt * gsnorth, Rearth) * kR2D;
+  const double latr = s.lat * kD2R;          // |latr - m.latr| < 3e-4 rad: angle addition
+  sincos_add(m.lat_sc, latr - m.latr);
+  m.latr = latr;
+  const double ge = dt * gseast / m.lat_sc.c;
+  s.lon = s.lon + divk_f(ge, Rearth) * kR2D;
+}
+
 // ---- one BlueSky substep of one aircraft (Traffic.update, RESO OFF) ------------------
 // oracle/bluesky_subset.py: traffic_update.  WIND: a wind field is set (wrappers/wind.py).
 // HMEMO: keep the heading's sin/cos across substeps keyed by its bits (kinds whose
 // aircraft fly constant headings); Merge's LNAV intruders change heading every substep.
-template <bool WIND, bool HMEMO = true>
+// CRUISE (the caller checked cruise_ok for every lane of the wave, !WIND): the aircraft is
+// level on its selected altitude with vs = 0, at its speed target (tas == the memoised
+// allow_tas, the speed memo valid for this state).  The speed schedule, PerfModel.limits,
+// update_airspeed and the vertical update are then identities -- tas, alt and the memo keys
+// stay, ax and vs become +0 -- so they are compiled out; everything else is the same code.
+template <bool WIND, bool HMEMO = true, bool CRUISE = false>
 __device__ __forceinline__ void substep(AC& s, Memo& m, double dt, const RouteRegs& rt,
                                         const WindDev& w, bool fh = false) {
+  static_assert(!(CRUISE && WIND), "the cruise substep has no wind");
   double vwn = 0.0, vwe = 0.0;
   if constexpr (WIND) wind_at(w, s.lat, s.lon, s.alt, &vwn, &vwe);
   const double gsv = WIND ? s.gs : s.tas;     // without wind gs = tas and trk = hdg
@@ -485,6 +563,18 @@ __device__ __forceinline__ void substep(AC& s, Memo& m, double dt, const RouteRe
     if (s.nav & 1) s.ap_trk = qdr;
   }
   BSG_SUBSTEP_MARK(1);
+  if constexpr (CRUISE) {
+    // (substep's own values on a cruise_ok state: delta_spd = +0 -> ax = +0, tas kept,
+    // turnrad unchanged; delta_alt = +0 -> target_vs = +0, vs = +0, alt = allow_h = alt)
+    m.last_alt = s.alt;
+    s.ax = 0.0;
+    BSG_SUBSTEP_MARK(2);
+    turn_update<false>(s, m, dt, fh, 0.0);
+    s.vs = 0.0;
+    BSG_SUBSTEP_MARK(3);
+    position_update<false, HMEMO>(s, m, dt, 0.0, 0.0, false, s.alt);
+    return;
+  }
   const double ap_vs = fabs(s.selvs) > 0.1 ? s.selvs : APVSDEF;
   const double ap_alt = s.selalt;
   const uint64_t ab = bits(s.alt);
@@ -557,31 +647,7 @@ __device__ __forceinline__ void substep(AC& s, Memo& m, double dt, const RouteRe
   s.tas = need_ax ? s.tas + s.ax * dt : allow_tas;
   m.turnrad = turnrad_of(s.tas);              // for the next substep's LNAV (off the chain)
   BSG_SUBSTEP_MARK(2);
-  // The heading update with its three pymod360.  fh (wave-uniform, propagate): every
-  // lane has |ap_trk| < 360 and hdg in [0, 360], so hdg_cmd = pymod360(ap_trk) is one
-  // select, and delhdg's and the new heading's arguments lie in [-180, 540] (two selects
-  // each; |dt * turnrate| < |delhdg| <= 180 when it is added) -- one uniform branch here
-  // instead of three ~150-cycle fmod branches.
-  auto turn = [&](auto fh_tag) {
-    constexpr bool F = decltype(fh_tag)::value;
-    if constexpr (!WIND) hdg_cmd = F ? pymod360_s(s.ap_trk) : pymod360(s.ap_trk);
-    const double da = hdg_cmd - s.hdg + 180.0;
-    const double delhdg = (F ? pymod360_r(da) : pymod360(da)) - 180.0;
-    // |delhdg| > |dt*turnrate| is false at delhdg == 0 whatever turnrate is: a straight
-    // flying aircraft needs no turn rate (whose division would sit on the tas -> heading
-    // -> position chain)
-    bool swhdgsel = false;
-    double turnrate = 0.0;
-    if (delhdg != 0.0) {
-      turnrate = (G0 * TAN_BANKDEF / npmax(s.tas, EPS_SPD)) * kR2D;
-      swhdgsel = fabs(delhdg) > fabs(dt * turnrate);
-    }
-    const double ha = swhdgsel ? s.hdg + sgnmul(true, delhdg, dt * turnrate) : hdg_cmd;
-    s.hdg = F ? pymod360_r(ha) : pymod360(ha);
-  };
-  if (!WIND && fh) turn(std::true_type{});
-  else turn(std::false_type{});
-  m.phdg = s.hdg >= 360.0 ? s.hdg - 360.0 : s.hdg;   // pymod360 of a [0, 360] value
+  turn_update<WIND>(s, m, dt, fh, hdg_cmd);
   const double delta_alt = allow_h - s.alt;
   const bool swaltsel = fabs(delta_alt) > npmax(10 * FT, fabs(2 * fabs(dt * s.vs)));
   const double target_vs = sgnmul(swaltsel, delta_alt, fabs(vs_cmd));
@@ -592,41 +658,11 @@ __device__ __forceinline__ void substep(AC& s, Memo& m, double dt, const RouteRe
   if (!isfinite(s.vs)) s.vs = 0.0;
   // update_groundspeed + update_pos
   BSG_SUBSTEP_MARK(3);
-  if constexpr (HMEMO) {
-    if (bits(s.hdg) != m.hdg_bits) {      // straight flight keeps its heading trig
-      sincos_t(s.hdg * kD2R, &m.shdg, &m.chdg);
-      m.hdg_bits = bits(s.hdg);
-    }
-  } else {
-    // LNAV lanes re-aim at the waypoint's bearing every substep, so some lane of a wave
-    // always misses the memo: its branch would only add latency
-    sincos_t(s.hdg * kD2R, &m.shdg, &m.chdg);
-  }
-  const double shdg = m.shdg, chdg = m.chdg;
-  double gsnorth = s.tas * chdg;
-  double gseast = s.tas * shdg;
   if constexpr (WIND) {
-    const bool applywind = s.alt > 50.0 * FT;     // airborne (altitude before update_pos)
-    gsnorth = gsnorth + vwn * (double)applywind;
-    gseast = gseast + vwe * (double)applywind;
-    if (applywind) {
-      s.gs = sqrt(gsnorth * gsnorth + gseast * gseast);
-      s.trk = pymod360_s(atan2(gseast, gsnorth) * kR2D);
-    } else {
-      s.gs = s.tas;
-      s.trk = s.hdg;
-    }
+    position_update<true, HMEMO>(s, m, dt, vwn, vwe, swaltsel, allow_h);
+  } else {
+    position_update<false, HMEMO>(s, m, dt, vwn, vwe, swaltsel, allow_h);
   }
-  if (swaltsel) s.alt = divk(rint((s.alt + s.vs * dt) * 1e6), 1e6);   // a branch: level flight
-  else s.alt = allow_h;                                            // skips the division
-  BSG_SUBSTEP_MARK(4);
-  // (divk_f: the numerators are finite -- tas is clamped by the envelope, |cos| <= 1)
-  s.lat = s.lat + divk_f(dt * gsnorth, Rearth) * kR2D;
-  const double latr = s.lat * kD2R;          // |latr - m.latr| < 3e-4 rad: angle addition
-  sincos_add(m.lat_sc, latr - m.latr);
-  m.latr = latr;
-  const double ge = dt * gseast / m.lat_sc.c;
-  s.lon = s.lon + divk_f(ge, Rearth) * kR2D;
 }
 
 // ---- LDS staging (one wave per block; GS lanes per env) -------------------------------
@@ -1839,7 +1875,7 @@ constexpr int kActDim = (KIND == BSG_ENV_MERGE || KIND == BSG_ENV_STATIC_OBSTACL
 // act: the env's action row, mc: its memo-cache entries (both fetched at kernel entry)
 // mcache: the memo-cache buffer this aircraft's entries live in (b.memo_cache; the
 // lookahead blocks' own region; nullptr = no memo -- the same bits, computed in full)
-template <int KIND, bool WIND>
+template <int KIND, bool WIND, bool LA_ROLE = false>
 __device__ __forceinline__ void propagate(const KParams& p, int e, int j, size_t a, AC& s,
                                           EnvScalars& ev, double& sub_reward, bool& sub_done,
                                           const double act[2], const double mc[MC_FIELDS],
@@ -1942,6 +1978,22 @@ __device__ __forceinline__ void propagate(const KParams& p, int e, int j, size_t
     // test, so an env's first step after a reset runs one substep on the fmod path.
     const bool trk_ok = !WIND && __ballot(!(fabs(s.ap_trk) < 360.0)) == 0;
     const bool fh0 = trk_ok && __ballot(!(s.hdg >= 0.0 && s.hdg <= 360.0)) == 0;
+    // Merge intruders in cruise -- the lookahead waves' lanes, whose aircraft fly LNAV level
+    // at their selected altitude on their speed target: if every stepping lane of the wave
+    // is level with vs = 0, at tas == the memoised allow_tas with the speed memo valid for
+    // this state, the whole step stays so and the cruise substep (no speed schedule,
+    // limits, update_airspeed or vertical update: identities there) gives the same bits.
+    // Waves with an ownship lane (the inline path) never qualify.
+    bool cruise = false;
+    if constexpr (LA_ROLE && KIND == BSG_ENV_MERGE && !WIND) {
+      const double allow_h = s.selalt > HMAX ? HMAX : s.selalt;
+      const bool ok_l = j > 0 && !p.no_fastpath && mcache != nullptr &&
+                        bits(s.alt) == bits(allow_h) && s.vs == 0.0 &&
+                        m.spd_bits == bits(s.selspd) && m.spdalt_bits == bits(s.alt) &&
+                        m.lim_tas_bits == bits(m.ap_tas) && m.lim_h_bits == bits(allow_h) &&
+                        m.lim_gd == ground_phase(s.alt) && bits(s.tas) == bits(m.allow_tas);
+      cruise = __ballot(!ok_l) == 0;
+    }
     if constexpr (KIND == BSG_ENV_STATIC_OBSTACLE) {
       // static_obstacle_env.py:132-150: _get_reward after every substep, with the
       // waypoint distance and drift of the previous observation; stop when done
@@ -1979,11 +2031,20 @@ __device__ __forceinline__ void propagate(const KParams& p, int e, int j, size_t
       // top priority over the main and CD helper waves they share SIMDs with (512 / 1,024 /
       // 2,048 envs: -2 / -1 / -3 %, profiles/r03/ab29.txt).
       const int sw = (p.prio_sw_num * S + p.prio_sw_den - 1) / p.prio_sw_den;
-      for (int it = 0; it < S; ++it) {
-        if (p.la) __builtin_amdgcn_s_setprio(3);
-        else if ((slot & 1) ? (it < sw) : (it >= sw)) __builtin_amdgcn_s_setprio(1);
-        else __builtin_amdgcn_s_setprio(0);
-        substep<WIND, KIND != BSG_ENV_MERGE>(s, m, dt, rt, p.wind, it == 0 ? fh0 : trk_ok);
+      auto loop = [&](auto cruise_tag) {
+        constexpr bool CR = decltype(cruise_tag)::value && LA_ROLE && KIND == BSG_ENV_MERGE && !WIND;
+        for (int it = 0; it < S; ++it) {
+          if (p.la) __builtin_amdgcn_s_setprio(3);
+          else if ((slot & 1) ? (it < sw) : (it >= sw)) __builtin_amdgcn_s_setprio(1);
+          else __builtin_amdgcn_s_setprio(0);
+          substep<WIND, KIND != BSG_ENV_MERGE, CR>(s, m, dt, rt, p.wind, it == 0 ? fh0 : trk_ok);
+        }
+      };
+      if constexpr (LA_ROLE && KIND == BSG_ENV_MERGE && !WIND) {
+        if (cruise) loop(std::true_type{});
+        else loop(std::false_type{});
+      } else {
+        loop(std::false_type{});
       }
       __builtin_amdgcn_s_setprio(0);
 #endif
@@ -2200,14 +2261,14 @@ __device__ __forceinline__ void lookahead_role(const KParams& p, LT& L, unsigned
         memo_invalidate(memo, a, EN);
 #pragma unroll
         for (int f = 0; f < MC_FIELDS; ++f) mc[f] = key_as_double(kNoKey);
-        propagate<KIND, WIND>(p, e, j, a, s, ev, sub_reward, sub_done, act, mc, oat, memo);
+        propagate<KIND, WIND, true>(p, e, j, a, s, ev, sub_reward, sub_done, act, mc, oat, memo);
         memo_fetch(mc, memo, a, EN);
         tag_out = la_tag(episode, step + 1, p.la_gen);
       } else {
         s = s_slot;
         tag_out = la_tag(episode, step + 1, p.la_gen);
       }
-      propagate<KIND, WIND>(p, e, j, a, s, ev, sub_reward, sub_done, act, mc, oat, memo);
+      propagate<KIND, WIND, true>(p, e, j, a, s, ev, sub_reward, sub_done, act, mc, oat, memo);
       la_store(p.la + (size_t)wslot * LA_F * EN, a, EN, s);
       if (j == 1) tags[(size_t)wslot * p.E + e] = tag_out;
     } else if (touch && j == 1) {
