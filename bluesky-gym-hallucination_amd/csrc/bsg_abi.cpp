@@ -49,6 +49,11 @@ struct bsg_ctx {
   // follow the graph's replays, so this ctx runs without the lookahead from then on
   bool la_captured = false;
   int no_fastpath = 0;
+  // Merge's creation-state constants (KParams::spawn_k), computed once by the first launch
+  // outside a stream capture: 0 = not yet, 1 = valid, -1 = unavailable
+  int spawn_k_state = 0;
+  double spawn_k[4] = {};
+  double* spawn_k_dev = nullptr;
 };
 
 namespace {
@@ -119,7 +124,36 @@ bsg::KParams make_params(const bsg_ctx* c, int mode) {
   p.la_gen = c->la_gen;
   p.la_seq = c->la_seq;
   p.no_fastpath = c->no_fastpath;
+  p.spawn_k_ok = c->spawn_k_state == 1 ? 1 : 0;
+  for (int k = 0; k < 4; ++k) p.spawn_k[k] = c->spawn_k[k];
   return p;
+}
+
+// KParams::spawn_k (Merge): one small kernel and a read-back, once per ctx, by the first
+// launch that is not being captured into a graph; BSG_NO_FASTPATH=1 leaves it off (the
+// tests compare the two)
+int spawn_k_prepare(bsg_ctx* c, hipStream_t st) {
+  if (c->spawn_k_state != 0) return BSG_OK;
+  if (c->cfg.env_kind != BSG_ENV_MERGE || c->no_fastpath) { c->spawn_k_state = -1; return BSG_OK; }
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  hipError_t e = hipStreamIsCapturing(st, &cs);
+  if (e != hipSuccess) return hip_fail(e, "hipStreamIsCapturing");
+  if (cs != hipStreamCaptureStatusNone) return BSG_OK;          // (a later launch does it)
+  c->spawn_k_state = -1;
+  if (!c->spawn_k_dev && (e = hipMalloc(reinterpret_cast<void**>(&c->spawn_k_dev), 64)) != hipSuccess)
+    return hip_fail(e, "hipMalloc(spawn_k)");
+  double h[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+  const double spd = c->cfg.kind_option > 0 ? (double)c->cfg.kind_option : 100.0;   // spawn_merge
+  if ((e = bsg::spawn_consts_merge(spd, 10000.0, c->spawn_k_dev, st)) != hipSuccess)
+    return hip_fail(e, "spawn constants launch");
+  if ((e = hipMemcpyAsync(h, c->spawn_k_dev, sizeof(h), hipMemcpyDeviceToHost, st)) != hipSuccess)
+    return hip_fail(e, "hipMemcpyAsync(spawn_k)");
+  if ((e = hipStreamSynchronize(st)) != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
+  if (h[4] == 1.0) {
+    for (int k = 0; k < 4; ++k) c->spawn_k[k] = h[k];
+    c->spawn_k_state = 1;
+  }
+  return BSG_OK;
 }
 
 // the lookahead runs for a bound Merge / Vertical scratch without a wind field
@@ -227,6 +261,7 @@ int launch(bsg_ctx* c, int mode, const double* actions, const double* spawn,
     if (cs != hipStreamCaptureStatusNone) c->la_captured = true;
   }
   if (int r = la_prepare(c, st)) return r;
+  if (int r = spawn_k_prepare(c, st)) return r;
   bsg::KParams p = make_params(c, mode);
   p.actions = actions;
   p.spawn = spawn;
@@ -402,6 +437,7 @@ int32_t bsg_destroy(bsg_ctx* c) {
     (void)hipEventDestroy(pr.second);
   }
   for (auto ev : c->ev_pool) (void)hipEventDestroy(ev);
+  if (c->spawn_k_dev) (void)hipFree(c->spawn_k_dev);
   delete c;
   return BSG_OK;
 }

@@ -85,9 +85,20 @@ struct KParams {
   uint32_t la_seq;           // launches since the lookahead scratch was (re)armed: its parity
                              // picks the env-scalar snapshot a launch reads (the main waves
                              // write the other one for the next launch)
+  // Merge: the creation state every aircraft of every env spawns with (same CAS, same
+  // altitude; bsg_abi.cpp computes it once with the kernels' own functions,
+  // spawn_consts_merge): [0] tas, [1] cas of Traffic.cre, [2] the speed memo's ap_tas,
+  // [3] its allow_tas entry (> 0: the 'level' form, bsg_kernels.hip Memo).  spawn_k_ok = 0:
+  // not available (cre and the memo as before).
+  double spawn_k[4];
+  int spawn_k_ok;
 };
 
 hipError_t launch_step(const KParams& p, hipStream_t stream);
+
+// Merge's creation-state constants (KParams::spawn_k) into out[0..4] (device; out[4] = 1.0
+// when valid), one thread, on `stream` (bsg_kernels.hip, the Merge translation unit)
+hipError_t spawn_consts_merge(double spd, double alt, double* out, hipStream_t stream);
 
 // per-kind launchers, one translation unit each (bsg_kernels.hip -DBSG_KIND_TU=<kind>;
 // the suffix is the BSG_ENV_* value)

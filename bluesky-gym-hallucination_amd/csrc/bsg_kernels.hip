@@ -33,6 +33,7 @@
 //     the distance as well.  min_sep is defined over the pairs inside the horizon.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <type_traits>
 
 #include "bsg_areas.h"
@@ -87,6 +88,16 @@ __device__ __forceinline__ void cre(AC& s, double lat, double lon, double hdg, d
   Atmos at = vatmos(alt);
   double tas, cas;
   casormach_at(spd, at, &tas, &cas);
+  s.lat = lat; s.lon = lon; s.alt = alt; s.hdg = hdg; s.tas = tas; s.cas = cas;
+  s.vs = 0.0; s.ax = 0.0; s.ap_trk = hdg; s.selspd = cas; s.selalt = alt; s.selvs = 0.0;
+  s.gs = tas; s.trk = hdg;
+  s.nav = 0;
+}
+
+// cre with the creation speed's tas / cas given (KParams::spawn_k: the same values cre
+// computes for Merge's one creation speed and altitude)
+__device__ __forceinline__ void cre_k(AC& s, double lat, double lon, double hdg, double alt,
+                                      double tas, double cas) {
   s.lat = lat; s.lon = lon; s.alt = alt; s.hdg = hdg; s.tas = tas; s.cas = cas;
   s.vs = 0.0; s.ax = 0.0; s.ap_trk = hdg; s.selspd = cas; s.selalt = alt; s.selvs = 0.0;
   s.gs = tas; s.trk = hdg;
@@ -317,6 +328,19 @@ __device__ __forceinline__ void memo_store(const Memo& m, const AC& s, const dou
 __device__ __forceinline__ void memo_invalidate(double* mc, size_t a, size_t stride) {
 #pragma unroll
   for (int f = 0; f < MC_FIELDS; ++f) mc[f * stride + a] = key_as_double(kNoKey);
+}
+
+// PerfModel.limits' speed clamp at a general atmosphere (substep's limits, the branch that
+// is not one of the two constant limit atmospheres): CAS clamp, back to TAS, Mach cap
+__device__ __forceinline__ double limits_general(double ap_tas, const Atmos& ah, bool gd) {
+  const double vmin = gd ? 0.0 : VMIN_CAS, vmax = gd ? VMAX_GD : VMAX_CAS;
+  const double intent_cas = tas2cas_at(ap_tas, ah);
+  double allow_cas = intent_cas < vmin ? vmin : intent_cas;
+  allow_cas = intent_cas > vmax ? vmax : allow_cas;
+  double allow_tas = cas2tas_at(allow_cas, ah);
+  const double snd_h = sound_at(ah);
+  if (allow_tas / snd_h > MMO) allow_tas = MMO * snd_h;
+  return allow_tas;
 }
 
 // the atmosphere at the current altitude, evaluated only when a memo entry needs it
@@ -605,7 +629,6 @@ __device__ __forceinline__ void substep(AC& s, Memo& m, double dt, const RouteRe
     }
     // PerfModel.limits
     if (bits(m.ap_tas) != m.lim_tas_bits || hb != m.lim_h_bits || gd != m.lim_gd) {
-      const double vmin = gd ? 0.0 : VMIN_CAS, vmax = gd ? VMAX_GD : VMAX_CAS;
       double allow_tas;
       const bool khi = bits(allow_h) == bits(HMAX);
       if (hb != ab && (khi || allow_h == 0.0)) {
@@ -622,12 +645,7 @@ __device__ __forceinline__ void substep(AC& s, Memo& m, double dt, const RouteRe
         if (allow_tas > tmmo) allow_tas = tmmo;
       } else {
         const Atmos ah = (hb == ab) ? memo_at(m, s.alt, ab) : vatmos(allow_h);
-        const double intent_cas = tas2cas_at(m.ap_tas, ah);
-        double allow_cas = intent_cas < vmin ? vmin : intent_cas;
-        allow_cas = intent_cas > vmax ? vmax : allow_cas;
-        allow_tas = cas2tas_at(allow_cas, ah);
-        const double snd_h = sound_at(ah);
-        if (allow_tas / snd_h > MMO) allow_tas = MMO * snd_h;
+        allow_tas = limits_general(m.ap_tas, ah, gd);
       }
       m.allow_tas = allow_tas;
       m.lim_tas_bits = bits(m.ap_tas);
@@ -1010,7 +1028,8 @@ __device__ __forceinline__ void spawn_merge(const KParams& p, int e, int j, uint
   double lat, lon;
   get_point_at_distance(p.cfg.wpt_lat[0], p.cfg.wpt_lon[0], dist, brg, &lat, &lon);
   // merge_env.py:119,154 (AC_SPD = 100, :30; kind_option > 0: another creation CAS, bsg.h)
-  cre(s, lat, lon, brg - 180, 10000.0, p.cfg.kind_option > 0 ? (double)p.cfg.kind_option : 100.0);
+  if (p.spawn_k_ok) cre_k(s, lat, lon, brg - 180, 10000.0, p.spawn_k[0], p.spawn_k[1]);
+  else cre(s, lat, lon, brg - 180, 10000.0, p.cfg.kind_option > 0 ? (double)p.cfg.kind_option : 100.0);
   if (j > 0) s.nav = 1;                                      // ADDWPT FIX; DEST RWY -> LNAV on
 }
 
@@ -1202,6 +1221,23 @@ __device__ __forceinline__ void spawn(const KParams& p, int e, int j, uint32_t e
 // ---------------------------------------------------------------------------------------
 // Per-env scalars
 // ---------------------------------------------------------------------------------------
+// The speed-memo entries of freshly created aircraft: Merge with KParams::spawn_k has the
+// values their first substep would compute (the same functions on the same creation state,
+// bsg_abi.cpp), so that substep starts from a valid memo instead of three speed
+// conversions; other kinds (and Merge without the constants): no entry.  mc (optional):
+// the caller's register copy.
+template <int KIND>
+__device__ __forceinline__ void memo_spawned(const KParams& p, double* mcb, size_t a, size_t stride,
+                                             double* mc) {
+  double v0 = key_as_double(kNoKey), v1 = key_as_double(kNoKey);
+  if constexpr (KIND == BSG_ENV_MERGE) {
+    if (p.spawn_k_ok) { v0 = p.spawn_k[2]; v1 = p.spawn_k[3]; }
+  }
+  mcb[(size_t)MC_AP_TAS * stride + a] = v0;
+  mcb[(size_t)MC_ALLOW_TAS * stride + a] = v1;
+  if (mc) { mc[MC_AP_TAS] = v0; mc[MC_ALLOW_TAS] = v1; }
+}
+
 struct EnvScalars {
   int step_count, flags, wpt_reach, faf_reached, total_intr;
   uint32_t episode;
@@ -2246,9 +2282,7 @@ __device__ __forceinline__ void lookahead_role(const KParams& p, LT& L, unsigned
         double aux[4] = {0.0, 0.0, 0.0, 0.0};
         s = AC{};
         spawn<KIND>(p, e, j, episode, s, aux, false);
-        memo_invalidate(memo, a, EN);
-#pragma unroll
-        for (int f = 0; f < MC_FIELDS; ++f) mc[f] = key_as_double(kNoKey);
+        memo_spawned<KIND>(p, memo, a, EN, mc);
         tag_out = la_tag(episode + 1u, 0, p.la_gen);
       } else if (p.mode == MODE_PRIME) {
         // from the state the previous launch finished writing: the next launch's post-step
@@ -2448,7 +2482,7 @@ __global__ __launch_bounds__(64 * CDW) BSG_WPE void step_kernel(KParams p) {
         }
       }
       if (active) store_ac_changed<WIND>(b, a, s, s_in);
-      if (resetting && mcache) memo_invalidate(mcache, a, (size_t)p.E * N);
+      if (resetting && mcache) memo_spawned<KIND>(p, mcache, a, (size_t)p.E * N, nullptr);
     }
     if (resetting && j == 0) {
       reset_scalars<KIND>(ev, aux);
@@ -2791,8 +2825,12 @@ static hipError_t launch_kind_w(const KParams& p0, hipStream_t st) {
     // at once (2 waves per SIMD x 1,024 SIMDs), or the lookahead blocks would queue behind
     // the main ones (1,024 envs at 4 waves: 98.6 us against 45.8 without the lookahead)
     const int slots = p.la ? 1024 : 2048;     // waves per copy of the grid
-    const int cdw = (!p.cfg.compute_cd || gs < 32) ? 1
-                    : (grid0 * 4 <= slots ? 4 : (grid0 * 2 <= slots ? 2 : 1));
+    int cdw = (!p.cfg.compute_cd || gs < 32) ? 1
+              : (grid0 * 4 <= slots ? 4 : (grid0 * 2 <= slots ? 2 : 1));
+#if defined(BSG_CDW_EXPERIMENT)
+    static const int cdw_cap = [] { const char* v = std::getenv("BSG_CDW_MAX"); return v ? std::atoi(v) : 4; }();
+    if (cdw > cdw_cap) cdw = cdw_cap >= 2 ? 2 : 1;
+#endif
 #define BSG_CASE_CD(G, W) \
   case G: hipLaunchKernelGGL((step_kernel<KIND, G, WIND, W>), dim3(grid), dim3(64 * W), p.lds_pad, st, p); break;
     if (cdw == 4) {
@@ -2824,6 +2862,35 @@ template <int KIND>
 static hipError_t launch_kind(const KParams& p, hipStream_t st) {
   return p.wind.np > 0 ? launch_kind_w<KIND, true>(p, st) : launch_kind_w<KIND, false>(p, st);
 }
+
+#if !defined(BSG_KIND_TU) || BSG_KIND_TU == 0
+// KParams::spawn_k for Merge: Traffic.cre's tas / cas at the creation speed and altitude, and
+// the speed memo the first substep of such an aircraft leaves (substep's spd_miss path and
+// general limits at vatmos(alt)); the 'level' form when the stored cas is the one
+// memo_final_cas would recompute.  out[4] = 1.0 when the creation state is the general-limits
+// case these values describe (selected altitude = altitude below HMAX).
+__global__ void spawn_consts_kernel(double spd, double alt, double* out) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  AC s{};
+  cre(s, 0.0, 0.0, 0.0, alt, spd);
+  const Atmos at = vatmos(alt);
+  const double ap_tas = casormach2tas_at(s.selspd, at);
+  const double allow_h = allow_h_of(s.selalt);
+  const double allow_tas = limits_general(ap_tas, at, ground_phase(s.alt));
+  const bool level = bits(tas2cas_at(s.tas, at)) == bits(s.cas);
+  const bool ok = bits(allow_h) == bits(s.alt) && allow_tas > 0.0 && ap_tas == ap_tas;
+  out[0] = s.tas;
+  out[1] = s.cas;
+  out[2] = ap_tas;
+  out[3] = level ? allow_tas : -allow_tas;
+  out[4] = ok ? 1.0 : 0.0;
+}
+
+hipError_t spawn_consts_merge(double spd, double alt, double* out, hipStream_t st) {
+  hipLaunchKernelGGL(spawn_consts_kernel, dim3(1), dim3(64), 0, st, spd, alt, out);
+  return hipGetLastError();
+}
+#endif
 
 // One translation unit per env kind (the Makefile compiles this file once per kind with
 // -DBSG_KIND_TU=<kind>, so the seven kinds build in parallel); launch_step dispatches

@@ -48,6 +48,9 @@ for spec in [
     ("merge32_full_16384", config.merge_config(num_ac=32), 16384, True),
     # the Merge lookahead forced off / on (DeviceBatch's default: on up to 2048 envs)
     ("merge32_full_512_nola", config.merge_config(num_ac=32), 512, True, False),
+    # C4 shards without episode ends in the timed window (no spawns: what resets cost)
+    ("merge32_full_512_noreset", config.merge_config(num_ac=32, max_episode_steps=1000000), 512, True),
+    ("merge32_full_2048_noreset", config.merge_config(num_ac=32, max_episode_steps=1000000), 2048, True),
     ("merge32_full_1024_nola", config.merge_config(num_ac=32), 1024, True, False),
     ("merge32_full_2048_nola", config.merge_config(num_ac=32), 2048, True, False),
     ("merge32_full_la", config.merge_config(num_ac=32), 4096, True, True),
