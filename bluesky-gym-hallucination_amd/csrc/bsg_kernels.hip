@@ -891,6 +891,26 @@ __device__ __forceinline__ void cd_pair2(const LT& L, int i, int k, CdOut* rik, 
                   cd_v(L, i) - cd_v(L, k), dv2, vrel, horizon, alti - altk + 0.0, vsi - vsk);
 }
 
+// row i / column k of the pair {i, k} alone: cd_pair2's first order for (i, k), its second
+// for (k, i) -- lati + latk and du^2 + dv^2 are the same bits in either order (IEEE addition
+// commutes; the two orders' du, dv are exact negatives)
+template <class LT>
+__device__ __forceinline__ CdOut cd_pair1(const LT& L, int i, int k) {
+  const double lati = L.lat[i], loni = L.lon[i];
+  const double latk = L.lat[k], lonk = L.lon[k];
+  const double dlat = (latk - lati) * kD2R;
+  const double dlon = (pymod360((lonk - loni) + 180.0) - 180.0) * kD2R;
+  const double cavelat = cos_t(((lati + latk) * kD2R) * 0.5);
+  const double du = cd_u(L, k) - cd_u(L, i);
+  const double dv = cd_v(L, k) - cd_v(L, i);
+  double dv2 = du * du + dv * dv;
+  dv2 = fabs(dv2) < 1e-6 ? 1e-6 : dv2;
+  const double vrel = sqrt(dv2);
+  const double horizon = (RPZ + DTLOOKAHEAD * vrel) * (1.0 + 1e-9) + 1.0;
+  return cd_order(dlat, dlon, cavelat, du, dv, dv2, vrel, horizon,
+                  L.alt[k] - L.alt[i] + 0.0, L.vs[k] - L.vs[i]);
+}
+
 // The StateBased pairs of one env group that a cd_pairs call covers:
 //   CD_ALL  every unordered pair of its nac aircraft;
 //   CD_OWN  the pairs with aircraft 0 only (the intruder pairs' rows came with the
@@ -973,22 +993,37 @@ __device__ __forceinline__ void cd_pairs(LT& L, unsigned short* cd_list, int lan
     *st4 = __builtin_amdgcn_s_memtime() | ((unsigned long long)total << 48);
     __builtin_amdgcn_sched_barrier(0);
   }
-  // phase 2: dense exact StateBased over the surviving pairs, both orders per lane
-  for (int t = lane; t < total; t += 64) {
-    const int pr = cd_list[t];
-    const int li = pr >> 6, lk = pr & 63;
-    CdOut r[2];
-    cd_pair2(L, li, lk, &r[0], &r[1]);
-    const int gb = (li / GS) * GS;
-#pragma unroll
-    for (int o = 0; o < 2; ++o) {
-      const int row = o ? lk : li, col = (o ? li : lk) - gb;
-      if (r[o].inside) {
-        atomicMin(&L.gmin[li / GS], bits(r[o].dist));
-        if (r[o].confl) atomicOr(&L.cm[row], 1ull << col);
-        if (r[o].lossep) atomicOr(&L.lm[row], 1ull << col);
-        if (r[o].confl && r[o].tcpa > 0.0) atomicMax(&L.tmax[row], bits(r[o].tcpa));
-      }
+  // phase 2: dense exact StateBased over the surviving pairs.  Up to 32 pairs (the common
+  // case: the list rarely fills half a wave) one order per lane -- lanes 2t and 2t+1 take
+  // pair t's (i, k) and (k, i) rows, so a wave's chain is one order, not two; beyond that both
+  // orders per lane (the shared terms once).  cd_pair1 of (k, i) is cd_pair2's second order
+  // bit for bit (its shared terms are symmetric in the pair), so the split changes no result.
+  auto put = [&](int row, int col, int gi, const CdOut& r) {
+    if (r.inside) {
+      atomicMin(&L.gmin[gi], bits(r.dist));
+      if (r.confl) atomicOr(&L.cm[row], 1ull << col);
+      if (r.lossep) atomicOr(&L.lm[row], 1ull << col);
+      if (r.confl && r.tcpa > 0.0) atomicMax(&L.tmax[row], bits(r.tcpa));
+    }
+  };
+  if (total <= 32) {
+    if (lane < 2 * total) {
+      const int pr = cd_list[lane >> 1];
+      const int li = pr >> 6, lk = pr & 63;
+      const int o = lane & 1;
+      const int row = o ? lk : li, other = o ? li : lk;
+      const int gb = (li / GS) * GS;
+      put(row, other - gb, li / GS, cd_pair1(L, row, other));
+    }
+  } else {
+    for (int t = lane; t < total; t += 64) {
+      const int pr = cd_list[t];
+      const int li = pr >> 6, lk = pr & 63;
+      CdOut r[2];
+      cd_pair2(L, li, lk, &r[0], &r[1]);
+      const int gb = (li / GS) * GS;
+      put(li, lk - gb, li / GS, r[0]);
+      put(lk, li - gb, li / GS, r[1]);
     }
   }
   __syncthreads();
