@@ -43,6 +43,9 @@ struct WindDev {
 // pairs' minimum separation (bits of a double), then the env-scalar snapshot the lookahead
 // waves read instead of the live env scalars: [2 launch parities][E][2] u64 (bsg_kernels.hip
 // la_snap).  Debug builds with -DBSG_LA_WAIT=1 append [E] u64 phase-A flags (tests only).
+// Last, Merge's spawn cache (bsg_kernels.hip spawn_cache_*): [3][EN] the next episode's
+// creation lat / lon / heading per aircraft, then [E] u64 the episode each env's entries
+// were drawn for.
 constexpr int LA_STATE = 10;
 constexpr int LA_F = LA_STATE + 3;
 constexpr int LA_MC = 2;           // = MC_FIELDS (bsg_kernels.hip)
@@ -52,6 +55,9 @@ constexpr size_t LA_WAIT_E = 1;
 constexpr size_t LA_WAIT_E = 0;
 #endif
 __host__ __device__ constexpr size_t la_doubles(size_t E, size_t N) {
+  return (2 * LA_F + LA_MC) * E * N + (8 + LA_WAIT_E) * E + 3 * E * N + E;
+}
+__host__ __device__ constexpr size_t la_sc_offset(size_t E, size_t N) {
   return (2 * LA_F + LA_MC) * E * N + (8 + LA_WAIT_E) * E;
 }
 

@@ -1045,8 +1045,9 @@ __device__ __forceinline__ double group_min(double v) {
 // ---------------------------------------------------------------------------------------
 // Spawn (device-side reset, K4): host parameters (parity mode) or Philox (throughput mode)
 // ---------------------------------------------------------------------------------------
-__device__ __forceinline__ void spawn_merge(const KParams& p, int e, int j, uint32_t episode,
-                                            AC& s) {
+// the drawn part of a Merge creation: position and heading (also the spawn cache's entries)
+__device__ __forceinline__ void spawn_merge_pos(const KParams& p, int e, int j, uint32_t episode,
+                                                double* lat, double* lon, double* hdg) {
   double brg, dist;
   if (p.spawn) {
     const int W = 2 * p.N;
@@ -1060,12 +1061,23 @@ __device__ __forceinline__ void spawn_merge(const KParams& p, int e, int j, uint
     const double dmin = j == 0 ? 50.0 : 20.0, dmax = j == 0 ? 200.0 : 500.0;   // :21-25
     dist = dmin + (dmax - dmin) * ub;
   }
-  double lat, lon;
-  get_point_at_distance(p.cfg.wpt_lat[0], p.cfg.wpt_lon[0], dist, brg, &lat, &lon);
+  get_point_at_distance(p.cfg.wpt_lat[0], p.cfg.wpt_lon[0], dist, brg, lat, lon);
+  *hdg = brg - 180;
+}
+
+__device__ __forceinline__ void spawn_merge_fin(const KParams& p, int j, AC& s, double lat,
+                                                double lon, double hdg) {
   // merge_env.py:119,154 (AC_SPD = 100, :30; kind_option > 0: another creation CAS, bsg.h)
-  if (p.spawn_k_ok) cre_k(s, lat, lon, brg - 180, 10000.0, p.spawn_k[0], p.spawn_k[1]);
-  else cre(s, lat, lon, brg - 180, 10000.0, p.cfg.kind_option > 0 ? (double)p.cfg.kind_option : 100.0);
+  if (p.spawn_k_ok) cre_k(s, lat, lon, hdg, 10000.0, p.spawn_k[0], p.spawn_k[1]);
+  else cre(s, lat, lon, hdg, 10000.0, p.cfg.kind_option > 0 ? (double)p.cfg.kind_option : 100.0);
   if (j > 0) s.nav = 1;                                      // ADDWPT FIX; DEST RWY -> LNAV on
+}
+
+__device__ __forceinline__ void spawn_merge(const KParams& p, int e, int j, uint32_t episode,
+                                            AC& s) {
+  double lat, lon, hdg;
+  spawn_merge_pos(p, e, j, episode, &lat, &lon, &hdg);
+  spawn_merge_fin(p, j, s, lat, lon, hdg);
 }
 
 // vertical_cr_env.py:267-268 / descent_env.py:170-171 (alt_init, target_alt)
@@ -2184,6 +2196,22 @@ __device__ __forceinline__ uint64_t* la_snap(const KParams& p, size_t EN, int pa
          (size_t)par * 2 * p.E;
 }
 
+// Merge's spawn cache (C4 shards: workgroups of CDW > 1 waves).  A main workgroup's CD
+// helper wave 1, idle while wave 0 runs phase A, draws its envs' next-episode creation
+// positions once per episode (spawn_merge_pos: Philox + get_point_at_distance, ~8 k cycles);
+// the launch that resets an env -- its main wave and its lookahead wave, both on the
+// launch's critical path -- takes them from here instead of drawing them again.  The
+// entries depend only on (env, episode, aircraft) and the ctx's seed, so a tag equal to the
+// episode is the whole validity check (the scratch's 0xFF fill matches no episode).  The
+// helper writes an env's entries only in a step launch that does not reset it, and a reader
+// uses them only in the launch that does: never both for one env in one launch.
+__device__ __forceinline__ double* sc_base(const KParams& p) {
+  return p.la + la_sc_offset((size_t)p.E, (size_t)p.N);
+}
+__device__ __forceinline__ uint64_t* sc_tags(const KParams& p) {
+  return reinterpret_cast<uint64_t*>(sc_base(p) + 3 * (size_t)p.E * p.N);
+}
+
 __device__ __forceinline__ void la_snap_store(const KParams& p, size_t EN, int par, int e,
                                               const EnvScalars& ev) {
   uint64_t* sn = la_snap(p, EN, par) + 2 * (size_t)e;
@@ -2287,6 +2315,16 @@ __device__ __forceinline__ void lookahead_role(const KParams& p, LT& L, unsigned
     if (p.mode == MODE_STEP) la_load(rslot, a, EN, s_slot);
     double mc[MC_FIELDS];
     memo_fetch(mc, memo, a, EN);
+    // (Merge, CDW > 1: this aircraft's spawn cache entry, used if the env resets)
+    double scv[3] = {0.0, 0.0, 0.0};
+    uint64_t sct = ~0ull;
+    if constexpr (KIND == BSG_ENV_MERGE && CDW > 1) {
+      if (p.mode != MODE_PRIME && !p.spawn) {
+        const double* sc = sc_base(p);
+        scv[0] = sc[a]; scv[1] = sc[EN + a]; scv[2] = sc[2 * EN + a];
+        sct = sc_tags(p)[e];
+      }
+    }
     bool resetting;
     if (p.mode == MODE_RESET) resetting = p.env_mask ? (p.env_mask[e] != 0) : true;
     else if (p.mode == MODE_PRIME) resetting = false;
@@ -2316,7 +2354,12 @@ __device__ __forceinline__ void lookahead_role(const KParams& p, LT& L, unsigned
       if (resetting) {
         double aux[4] = {0.0, 0.0, 0.0, 0.0};
         s = AC{};
-        spawn<KIND>(p, e, j, episode, s, aux, false);
+        if constexpr (KIND == BSG_ENV_MERGE && CDW > 1) {
+          if (sct == (uint64_t)episode) spawn_merge_fin(p, j, s, scv[0], scv[1], scv[2]);
+          else spawn<KIND>(p, e, j, episode, s, aux, false);
+        } else {
+          spawn<KIND>(p, e, j, episode, s, aux, false);
+        }
         memo_spawned<KIND>(p, memo, a, EN, mc);
         tag_out = la_tag(episode + 1u, 0, p.la_gen);
       } else if (p.mode == MODE_PRIME) {
@@ -2337,7 +2380,18 @@ __device__ __forceinline__ void lookahead_role(const KParams& p, LT& L, unsigned
         s = s_slot;
         tag_out = la_tag(episode, step + 1, p.la_gen);
       }
+#if defined(BSG_STAMPS) && BSG_STAMPS
+      // (lane 1 -- j = 1 of the wave's first env -- writes the lookahead wave's stamps)
+      const unsigned long long nrst = (unsigned long long)__popcll(__ballot(resetting));
+      if (p.stamps && threadIdx.x == 1) {
+        p.stamps[(size_t)blockIdx.x * 8 + 2] = stamp_clock();
+        p.stamps[(size_t)blockIdx.x * 8 + 4] = nrst;
+      }
+#endif
       propagate<KIND, WIND, true>(p, e, j, a, s, ev, sub_reward, sub_done, act, mc, oat, memo);
+#if defined(BSG_STAMPS) && BSG_STAMPS
+      if (p.stamps && threadIdx.x == 1) p.stamps[(size_t)blockIdx.x * 8 + 3] = stamp_clock();
+#endif
       la_store(p.la + (size_t)wslot * LA_F * EN, a, EN, s);
       if (j == 1) tags[(size_t)wslot * p.E + e] = tag_out;
     } else if (touch && j == 1) {
@@ -2456,6 +2510,18 @@ __global__ __launch_bounds__(64 * CDW) BSG_WPE void step_kernel(KParams p) {
     la_cd_in[3] = (unsigned long long)__double_as_longlong(
         p.la[(2 * LA_F + MC_FIELDS) * EN + 2 * (size_t)p.E + (size_t)p.la_par * p.E + e]);
   }
+  // (Merge C4 shards: this aircraft's spawn cache entry, used if the env resets)
+  constexpr bool kSC = kLA && KIND == BSG_ENV_MERGE && CDW > 1;
+  double scv[3] = {0.0, 0.0, 0.0};
+  uint64_t sct = ~0ull;
+  if constexpr (kSC) {
+    if (ok && p.la && !p.spawn) {
+      const size_t EN = (size_t)p.E * N;
+      const double* sc = sc_base(p);
+      scv[0] = sc[a]; scv[1] = sc[EN + a]; scv[2] = sc[2 * EN + a];
+      sct = sc_tags(p)[e];
+    }
+  }
   double mc[MC_FIELDS];
 #pragma unroll
   for (int f = 0; f < MC_FIELDS; ++f) mc[f] = key_as_double(kNoKey);
@@ -2502,8 +2568,35 @@ __global__ __launch_bounds__(64 * CDW) BSG_WPE void step_kernel(KParams p) {
     const bool on = ok && j < ev.nac;   // SectorCR: aircraft slot in use this episode
     const bool keep = kKeepsAircraft<KIND> && (ev.flags & BSG_FLAG_AC_PRESENT);
     AC s = (!resetting || keep) ? s_in : AC{};
+    if constexpr (kSC) {
+      // the spawn cache's producer: helper wave 1 draws its envs' next creation positions
+      // once per episode, in a step launch that does not reset the env
+      if (wv == 1 && p.la && p.mode == MODE_STEP && !p.spawn) {
+        const int eh = (int)blockIdx.x * (64 / GS) + g;
+        if (eh < p.E && j < N) {
+          const uint32_t epi = b.episode[eh];
+          const bool rst = p.cfg.autoreset_mode == BSG_AUTORESET_NEXT_STEP && (b.flags[eh] & 1);
+          uint64_t* tg = sc_tags(p);
+          if (!rst && tg[eh] != (uint64_t)epi) {
+            double lat_n, lon_n, hdg_n;
+            spawn_merge_pos(p, eh, j, epi, &lat_n, &lon_n, &hdg_n);
+            const size_t EN = (size_t)p.E * N, ah = (size_t)eh * N + j;
+            double* sc = sc_base(p);
+            sc[ah] = lat_n; sc[EN + ah] = lon_n; sc[2 * EN + ah] = hdg_n;
+            if (j == 0) tg[eh] = epi;
+          }
+        }
+      }
+    }
     if (ok) {
-      if (resetting) spawn<KIND>(p, e, j, ev.episode, s, aux, keep);
+      if (resetting) {
+        if constexpr (kSC) {
+          if (sct == (uint64_t)ev.episode) spawn_merge_fin(p, j, s, scv[0], scv[1], scv[2]);
+          else spawn<KIND>(p, e, j, ev.episode, s, aux, keep);
+        } else {
+          spawn<KIND>(p, e, j, ev.episode, s, aux, keep);
+        }
+      }
       if (stepping && on) {
         if (la_intr && la_tag_in == la_tag(ev.episode, ev.step_count, p.la_gen)) {
           s.lat = s_la.lat; s.lon = s_la.lon; s.alt = s_la.alt; s.hdg = s_la.hdg;

@@ -73,6 +73,27 @@ def test_lookahead_bit_identical_to_inline(kind, E, N):
     assert dones >= E * 3                               # autoresets in the window
 
 
+def test_spawn_cache_serves_the_resets():
+    """Merge's spawn cache (csrc/bsg_kernels.hip sc_base): at 512 envs (workgroups of four
+    waves) the CD helper waves draw each env's next creation positions once per episode,
+    and the resetting launches take them from there -- bit-identical to the inline path
+    (test_lookahead_bit_identical_to_inline[merge-512-32]); here: the cache is filled, i.e.
+    the resets it must serve find it."""
+    E, N = 512, 32
+    b = _batch(E, N, True, maxep=20)
+    g = torch.Generator(device="cuda").manual_seed(3)
+    b.reset()
+    for _ in range(45):
+        b.step(torch.rand((E, b.act_dim), dtype=torch.float64, device="cuda", generator=g) * 2 - 1)
+    torch.cuda.synchronize()
+    EN = E * N
+    off = (2 * 13 + 2) * EN + 8 * E + 3 * EN       # bsg_internal.h la_sc_offset + [3][EN]
+    tags = b._la_buf[off:off + E].view(torch.int64)
+    ep = b.envs["episode"].to(torch.int64) & 0xFFFFFFFF
+    hit = (tags == ep).float().mean().item()
+    assert hit > 0.9, hit
+
+
 @pytest.mark.parametrize("kind", ["merge", "vertical"])
 def test_lookahead_with_host_spawn_rows_and_toggle(kind):
     """Parity mode (host spawn rows for the NEXT_STEP resets) and switching the lookahead

@@ -180,10 +180,14 @@ if ran.any():
     lr0 = la[ran, 0].astype(np.int64); lr1 = la[ran, 6].astype(np.int64)
     print("lookahead waves: n per launch", int(ran.sum()) // 5, " life (us)", pct((lr1 - lr0) * 10 / 1000 * 1000))
     lc1 = la[ran, 1].astype(np.int64); lc2 = la[ran, 2].astype(np.int64); lc3 = la[ran, 3].astype(np.int64)
-    if (lc2 != 0).any():
-        print("lookahead propagate cyc", pct(lc2[lc2 != 0] - lc1[lc2 != 0]))
-    if (lc3 != 0).any():
-        print("lookahead intruder CD cyc", pct(lc3[lc3 != 0] - lc2[lc3 != 0]))
+    nr = la[ran, 4].astype(np.int64)
+    lr = (lr1 - lr0) * 10 / 1000
+    ok = (lc2 != 0) & (lc3 != 0)
+    for nm, sel in (("no resetting lane", ok & (nr == 0)), ("resetting lanes", ok & (nr > 0))):
+        if sel.any():
+            print(f"lookahead waves, {nm}: n={int(sel.sum())}  life us {pct(lr[sel] * 1000)}")
+            print(f"   entry -> propagate (loads, spawn) cyc {pct(lc2[sel] - lc1[sel])}")
+            print(f"   propagate cyc                         {pct(lc3[sel] - lc2[sel])}")
     for run in range(1, 5):
         s_ = slice(run * grid, (run + 1) * grid)
         t0k = rt0[s_].min()
