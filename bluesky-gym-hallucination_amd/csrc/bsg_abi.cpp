@@ -52,7 +52,7 @@ struct bsg_ctx {
   // Merge's creation-state constants (KParams::spawn_k), computed once by the first launch
   // outside a stream capture: 0 = not yet, 1 = valid, -1 = unavailable
   int spawn_k_state = 0;
-  double spawn_k[4] = {};
+  double spawn_k[8] = {};
   double* spawn_k_dev = nullptr;
 };
 
@@ -125,7 +125,7 @@ bsg::KParams make_params(const bsg_ctx* c, int mode) {
   p.la_seq = c->la_seq;
   p.no_fastpath = c->no_fastpath;
   p.spawn_k_ok = c->spawn_k_state == 1 ? 1 : 0;
-  for (int k = 0; k < 4; ++k) p.spawn_k[k] = c->spawn_k[k];
+  for (int k = 0; k < 8; ++k) p.spawn_k[k] = c->spawn_k[k];
   return p;
 }
 
@@ -140,9 +140,9 @@ int spawn_k_prepare(bsg_ctx* c, hipStream_t st) {
   if (e != hipSuccess) return hip_fail(e, "hipStreamIsCapturing");
   if (cs != hipStreamCaptureStatusNone) return BSG_OK;          // (a later launch does it)
   c->spawn_k_state = -1;
-  if (!c->spawn_k_dev && (e = hipMalloc(reinterpret_cast<void**>(&c->spawn_k_dev), 64)) != hipSuccess)
+  if (!c->spawn_k_dev && (e = hipMalloc(reinterpret_cast<void**>(&c->spawn_k_dev), 8 * sizeof(double))) != hipSuccess)
     return hip_fail(e, "hipMalloc(spawn_k)");
-  double h[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+  double h[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
   const double spd = c->cfg.kind_option > 0 ? (double)c->cfg.kind_option : 100.0;   // spawn_merge
   if ((e = bsg::spawn_consts_merge(spd, 10000.0, c->spawn_k_dev, st)) != hipSuccess)
     return hip_fail(e, "spawn constants launch");
@@ -150,7 +150,7 @@ int spawn_k_prepare(bsg_ctx* c, hipStream_t st) {
     return hip_fail(e, "hipMemcpyAsync(spawn_k)");
   if ((e = hipStreamSynchronize(st)) != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
   if (h[4] == 1.0) {
-    for (int k = 0; k < 4; ++k) c->spawn_k[k] = h[k];
+    for (int k = 0; k < 8; ++k) c->spawn_k[k] = h[k];
     c->spawn_k_state = 1;
   }
   return BSG_OK;

@@ -96,14 +96,14 @@ struct KParams {
   // spawn_consts_merge): [0] tas, [1] cas of Traffic.cre, [2] the speed memo's ap_tas,
   // [3] its allow_tas entry (> 0: the 'level' form, bsg_kernels.hip Memo).  spawn_k_ok = 0:
   // not available (cre and the memo as before).
-  double spawn_k[4];
+  double spawn_k[8];
   int spawn_k_ok;
 };
 
 hipError_t launch_step(const KParams& p, hipStream_t stream);
 
-// Merge's creation-state constants (KParams::spawn_k) into out[0..4] (device; out[4] = 1.0
-// when valid), one thread, on `stream` (bsg_kernels.hip, the Merge translation unit)
+// Merge's creation-state constants (KParams::spawn_k) into out[0..7] (device; out[4] = 1.0
+// when valid; out[5..7] the creation altitude's atmosphere), one thread, on `stream` (bsg_kernels.hip, the Merge translation unit)
 hipError_t spawn_consts_merge(double spd, double alt, double* out, hipStream_t stream);
 
 // per-kind launchers, one translation unit each (bsg_kernels.hip -DBSG_KIND_TU=<kind>;

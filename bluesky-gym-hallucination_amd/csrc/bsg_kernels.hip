@@ -1958,11 +1958,13 @@ constexpr int kActDim = (KIND == BSG_ENV_MERGE || KIND == BSG_ENV_STATIC_OBSTACL
 // act: the env's action row, mc: its memo-cache entries (both fetched at kernel entry)
 // mcache: the memo-cache buffer this aircraft's entries live in (b.memo_cache; the
 // lookahead blocks' own region; nullptr = no memo -- the same bits, computed in full)
-template <int KIND, bool WIND, bool LA_ROLE = false>
+// LAK = false: a launch without the lookahead (its main waves' ownship loops compiled out)
+template <int KIND, bool WIND, bool LA_ROLE = false, bool LAK = true>
 __device__ __forceinline__ void propagate(const KParams& p, int e, int j, size_t a, AC& s,
                                           EnvScalars& ev, double& sub_reward, bool& sub_done,
                                           const double act[2], const double mc[MC_FIELDS],
-                                          const double oat[4], double* mcache) {
+                                          const double oat[4], double* mcache,
+                                          bool spawned = false) {
   const Buffers& b = p.b;
   const int N = p.N;
   const AC s0 = s;                  // as loaded: the cross-step memo's keys (memo_load)
@@ -1989,7 +1991,7 @@ __device__ __forceinline__ void propagate(const KParams& p, int e, int j, size_t
   // Vertical: only with the lookahead, whose main waves propagate the ownships alone (inline,
   // the intruders would run substep() after the ownship's loop in the same wave: the union
   // measured slower than substep() alone, 121.7 against 90.6 us at 2,048 envs)
-  if constexpr ((KIND == BSG_ENV_DESCENT || KIND == BSG_ENV_VERTICAL_CR) && !WIND) {
+  if constexpr ((KIND == BSG_ENV_DESCENT || (KIND == BSG_ENV_VERTICAL_CR && LAK)) && !WIND) {
     bool fast_ok = false;
     if (j == 0 && S > 0 && !p.no_fastpath && (KIND == BSG_ENV_DESCENT || p.la)) {
       const AC saved = s;
@@ -2019,7 +2021,7 @@ __device__ __forceinline__ void propagate(const KParams& p, int e, int j, size_t
     if (__ballot(!fast_ok) == 0) return;
     if (fast_ok) return;
   }
-  if constexpr (KIND == BSG_ENV_MERGE && !WIND) {
+  if constexpr (KIND == BSG_ENV_MERGE && !WIND && LAK) {
     // the lookahead's main waves propagate only the ownships: merge_own_fast
     bool fast_ok = false;
     if (j == 0 && p.la && !p.no_fastpath) {
@@ -2050,6 +2052,18 @@ __device__ __forceinline__ void propagate(const KParams& p, int e, int j, size_t
     Memo m;
     memo_init(m, s);
     if (mcache) memo_load(m, mc, s0);
+    if constexpr (KIND == BSG_ENV_MERGE && LA_ROLE) {
+      // an aircraft created this launch (its memo from memo_spawned): whatever the level flag
+      // says about its stored cas, ap_tas is casormach2tas(selspd, alt) of exactly this state,
+      // and the atmosphere of the creation altitude is known -- the first substep needs no
+      // vatmos and no speed conversion but the ones its state change asks for
+      if (spawned && mcache && p.spawn_k_ok) {
+        m.spd_bits = bits(s0.selspd);
+        m.spdalt_bits = bits(s0.alt);
+        m.alt_bits = bits(s0.alt);
+        m.at = Atmos{p.spawn_k[5], p.spawn_k[6], p.spawn_k[7]};
+      }
+    }
     if (j == 0 && mcache) { m.alt_bits = bits(oat[0]); m.at = Atmos{oat[1], oat[2], oat[3]}; }
     RouteRegs rt;
     rt.load(p.route, p.route_t);
@@ -2066,17 +2080,24 @@ __device__ __forceinline__ void propagate(const KParams& p, int e, int j, size_t
     // is level with vs = 0, at tas == the memoised allow_tas with the speed memo valid for
     // this state, the whole step stays so and the cruise substep (no speed schedule,
     // limits, update_airspeed or vertical update: identities there) gives the same bits.
-    // Waves with an ownship lane (the inline path) never qualify.
-    bool cruise = false;
-    if constexpr (LA_ROLE && KIND == BSG_ENV_MERGE && !WIND) {
-      const double allow_h = s.selalt > HMAX ? HMAX : s.selalt;
-      const bool ok_l = j > 0 && !p.no_fastpath && mcache != nullptr &&
-                        bits(s.alt) == bits(allow_h) && s.vs == 0.0 &&
-                        m.spd_bits == bits(s.selspd) && m.spdalt_bits == bits(s.alt) &&
-                        m.lim_tas_bits == bits(m.ap_tas) && m.lim_h_bits == bits(allow_h) &&
-                        m.lim_gd == ground_phase(s.alt) && bits(s.tas) == bits(m.allow_tas);
-      cruise = __ballot(!ok_l) == 0;
-    }
+    // Waves with an ownship lane (the inline path) never qualify.  The same holds from any
+    // substep on: a wave that starts the step off cruise (an env's first step after its
+    // creation, whose tas snaps to allow_tas in the first substep) is checked again after
+    // each general substep and switches to the cruise substep once every lane qualifies.
+    auto cruise_now = [&]() -> bool {
+      if constexpr (LA_ROLE && KIND == BSG_ENV_MERGE && !WIND) {
+        const double allow_h = s.selalt > HMAX ? HMAX : s.selalt;
+        const bool ok_l = j > 0 && !p.no_fastpath && mcache != nullptr &&
+                          bits(s.alt) == bits(allow_h) && s.vs == 0.0 &&
+                          m.spd_bits == bits(s.selspd) && m.spdalt_bits == bits(s.alt) &&
+                          m.lim_tas_bits == bits(m.ap_tas) && m.lim_h_bits == bits(allow_h) &&
+                          m.lim_gd == ground_phase(s.alt) && bits(s.tas) == bits(m.allow_tas);
+        return __ballot(!ok_l) == 0;
+      } else {
+        return false;
+      }
+    };
+    const bool cruise = cruise_now();
     if constexpr (KIND == BSG_ENV_STATIC_OBSTACLE) {
       // static_obstacle_env.py:132-150: _get_reward after every substep, with the
       // waypoint distance and drift of the previous observation; stop when done
@@ -2114,20 +2135,38 @@ __device__ __forceinline__ void propagate(const KParams& p, int e, int j, size_t
       // top priority over the main and CD helper waves they share SIMDs with (512 / 1,024 /
       // 2,048 envs: -2 / -1 / -3 %, profiles/r03/ab29.txt).
       const int sw = (p.prio_sw_num * S + p.prio_sw_den - 1) / p.prio_sw_den;
-      auto loop = [&](auto cruise_tag) {
+      // substeps it0.. (the cruise form or the general one); with `recheck` the general loop
+      // stops after a substep that leaves the wave in cruise and returns the next index
+      auto loop = [&](auto cruise_tag, int it0, bool recheck) -> int {
         constexpr bool CR = decltype(cruise_tag)::value && LA_ROLE && KIND == BSG_ENV_MERGE && !WIND;
-        for (int it = 0; it < S; ++it) {
+        int it = it0;
+        for (; it < S; ++it) {
           if (p.la) __builtin_amdgcn_s_setprio(3);
           else if ((slot & 1) ? (it < sw) : (it >= sw)) __builtin_amdgcn_s_setprio(1);
           else __builtin_amdgcn_s_setprio(0);
           substep<WIND, KIND != BSG_ENV_MERGE, CR>(s, m, dt, rt, p.wind, it == 0 ? fh0 : trk_ok);
+#if defined(BSG_STAMPS) && BSG_STAMPS
+          // (lookahead waves: the first substep's end and whether the wave ran the cruise loop)
+          if (LA_ROLE && it == 0 && p.stamps && threadIdx.x == 1) {
+            p.stamps[(size_t)blockIdx.x * 8 + 5] = stamp_clock();
+            p.stamps[(size_t)blockIdx.x * 8 + 7] = CR ? 1ull : 0ull;
+          }
+#endif
+          if constexpr (!CR && LA_ROLE && KIND == BSG_ENV_MERGE && !WIND) {
+            if (recheck && it + 1 < S && cruise_now()) { ++it; break; }
+          }
         }
+        return it;
       };
       if constexpr (LA_ROLE && KIND == BSG_ENV_MERGE && !WIND) {
-        if (cruise) loop(std::true_type{});
-        else loop(std::false_type{});
+        if (cruise) {
+          loop(std::true_type{}, 0, false);
+        } else {
+          const int it = loop(std::false_type{}, 0, true);
+          if (it < S) loop(std::true_type{}, it, false);
+        }
       } else {
-        loop(std::false_type{});
+        loop(std::false_type{}, 0, false);
       }
       __builtin_amdgcn_s_setprio(0);
 #endif
@@ -2388,7 +2427,8 @@ __device__ __forceinline__ void lookahead_role(const KParams& p, LT& L, unsigned
         p.stamps[(size_t)blockIdx.x * 8 + 4] = nrst;
       }
 #endif
-      propagate<KIND, WIND, true>(p, e, j, a, s, ev, sub_reward, sub_done, act, mc, oat, memo);
+      propagate<KIND, WIND, true>(p, e, j, a, s, ev, sub_reward, sub_done, act, mc, oat, memo,
+                                  resetting);
 #if defined(BSG_STAMPS) && BSG_STAMPS
       if (p.stamps && threadIdx.x == 1) p.stamps[(size_t)blockIdx.x * 8 + 3] = stamp_clock();
 #endif
@@ -2435,16 +2475,18 @@ __device__ __forceinline__ void lookahead_role(const KParams& p, LT& L, unsigned
 #else
 #define BSG_WPE
 #endif
-template <int KIND, int GS, bool WIND, int CDW = 1>
+// LAK: the lookahead's code compiled in (launches without a lookahead scratch take the
+// instance without it: the 4,096-env headline launch keeps its own registers and code).
+template <int KIND, int GS, bool WIND, int CDW = 1, bool LAK = true>
 __global__ __launch_bounds__(64 * CDW) BSG_WPE void step_kernel(KParams p) {
 #if defined(BSG_STAMPS) && BSG_STAMPS
   BSG_STAMP(0, __builtin_amdgcn_s_memrealtime());
   BSG_STAMP(1, stamp_clock());
 #endif
-  constexpr bool kLA = (KIND == BSG_ENV_MERGE || KIND == BSG_ENV_VERTICAL_CR) && !WIND;
+  constexpr bool kLA = (KIND == BSG_ENV_MERGE || KIND == BSG_ENV_VERTICAL_CR) && !WIND && LAK;
   // (la_cd is Vertical's only: compiled out of the other kinds, whose registers it would
   // otherwise hold across the substep loop)
-  constexpr bool kLaCd = KIND == BSG_ENV_VERTICAL_CR && !WIND;
+  constexpr bool kLaCd = KIND == BSG_ENV_VERTICAL_CR && !WIND && LAK;
   __shared__ Lds<WIND> L;
   constexpr int kList = 64 * (GS > 1 ? GS - 1 : 1);
   __shared__ unsigned short cd_lists[CDW * kList];   // per-wave CD work lists (cd_pairs)
@@ -2606,7 +2648,7 @@ __global__ __launch_bounds__(64 * CDW) BSG_WPE void step_kernel(KParams p) {
 #if defined(BSG_EXP_NOOWN) && BSG_EXP_NOOWN
           if (j > 0)   // timing experiment only: the ownship does not move (wrong results)
 #endif
-          propagate<KIND, WIND>(p, e, j, a, s, ev, sub_reward, sub_done, act, mc, oat, mcache);
+          propagate<KIND, WIND, false, LAK>(p, e, j, a, s, ev, sub_reward, sub_done, act, mc, oat, mcache);
         }
       }
       if (active) store_ac_changed<WIND>(b, a, s, s_in);
@@ -2977,6 +3019,18 @@ static hipError_t launch_kind_w(const KParams& p0, hipStream_t st) {
   } else if constexpr (KIND == BSG_ENV_SECTOR_CR) {
     switch (gs) { BSG_CASE(8) BSG_CASE(16) BSG_CASE(32) BSG_CASE(64) default: return hipErrorInvalidValue; }
   } else {
+    if constexpr ((KIND == BSG_ENV_MERGE || KIND == BSG_ENV_VERTICAL_CR) && !WIND) {
+      if (!p.la) {
+#define BSG_CASE_NL(G) \
+  case G: hipLaunchKernelGGL((step_kernel<KIND, G, WIND, 1, false>), dim3(grid), dim3(64), p.lds_pad, st, p); break;
+        switch (gs) {
+          BSG_CASE_NL(2) BSG_CASE_NL(4) BSG_CASE_NL(8) BSG_CASE_NL(16) BSG_CASE_NL(32) BSG_CASE_NL(64)
+          default: return hipErrorInvalidValue;
+        }
+#undef BSG_CASE_NL
+        return hipGetLastError();
+      }
+    }
     switch (gs) {
       BSG_CASE(2) BSG_CASE(4) BSG_CASE(8) BSG_CASE(16) BSG_CASE(32) BSG_CASE(64)
       default: return hipErrorInvalidValue;
@@ -3012,6 +3066,9 @@ __global__ void spawn_consts_kernel(double spd, double alt, double* out) {
   out[2] = ap_tas;
   out[3] = level ? allow_tas : -allow_tas;
   out[4] = ok ? 1.0 : 0.0;
+  out[5] = at.p;                    // the creation altitude's atmosphere (a created aircraft's
+  out[6] = at.rho;                  //   first substep: propagate's `spawned`)
+  out[7] = at.T;
 }
 
 hipError_t spawn_consts_merge(double spd, double alt, double* out, hipStream_t st) {

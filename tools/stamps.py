@@ -188,6 +188,12 @@ if ran.any():
             print(f"lookahead waves, {nm}: n={int(sel.sum())}  life us {pct(lr[sel] * 1000)}")
             print(f"   entry -> propagate (loads, spawn) cyc {pct(lc2[sel] - lc1[sel])}")
             print(f"   propagate cyc                         {pct(lc3[sel] - lc2[sel])}")
+            lc5 = la[ran, 5].astype(np.int64); cr = la[ran, 7].astype(np.int64)
+            s5 = sel & (lc5 != 0)
+            if s5.any():
+                print(f"   first substep cyc                     {pct(lc5[s5] - lc2[s5])}")
+                print(f"   substeps 2.. cyc                      {pct(lc3[s5] - lc5[s5])}")
+                print(f"   cruise loop: {int((cr[s5] == 1).sum())} of {int(s5.sum())} waves")
     for run in range(1, 5):
         s_ = slice(run * grid, (run + 1) * grid)
         t0k = rt0[s_].min()
