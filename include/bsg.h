@@ -229,8 +229,10 @@ int32_t bsg_set_learner(bsg_ctx* ctx, float* learner_rows);
  * vertical_cr_env.py:183-200; RESO OFF), so with a caller-owned scratch of
  * bsg_lookahead_bytes() bytes bound, every launch also propagates the intruders one RL
  * step ahead in extra workgroups, and the next step consumes that state instead of
- * integrating the intruders on its critical path.  Results are bit-identical to the
- * inline path.  bsg_lookahead_bytes returns 0 when the ctx cannot use it;
+ * integrating the intruders on its critical path (Merge, small batches: the scratch also
+ * holds a cache of each env's next-episode creation positions, drawn ahead by idle waves).
+ * Results are bit-identical to the inline path.  bsg_lookahead_bytes returns 0 when the
+ * ctx cannot use it;
  * bsg_set_lookahead(ctx, NULL, 0) turns it off.  Binding, a wind change or calling
  * bsg_set_lookahead again restarts it from the state buffers (call it again after
  * writing aircraft state directly, as for memo_cache).  Replaces nothing in the reference
