@@ -42,12 +42,12 @@ constexpr double EPS_SPD = 0.01;
 constexpr double AXMAX = 0.5;
 constexpr double VMIN_CAS = 140.0 * KTS;
 constexpr double VMAX_CAS = 163.0;
-constexpr double MMO = 0.82;
+constexpr double MMO = 0.80;   // pinned by the reference's saved Merge states (M0.80 at 10,000 m)
 constexpr double HMAX = 39800.0 * FT;
 constexpr double VSMAX = 4000.0 * FPM;
 constexpr double VSMIN = -4000.0 * FPM;  // unreachable: the limits see |ap.vs|
 constexpr double GD_ALT_FT = 75.0;       // OpenAP phase GD: alt / ft <= 75
-constexpr double VMAX_GD = 88.5;         // phase GD: CAS in [0, VMAX_GD], axmax AXMAX_GD
+constexpr double VMAX_GD = 89.0;         // phase GD: CAS in [0, VMAX_GD], axmax AXMAX_GD (saved Horizontal states)
 constexpr double AXMAX_GD = 2.0;
 constexpr double RPZ = 5.0 * NM;
 constexpr double HPZ = 1000.0 * FT;
@@ -157,8 +157,8 @@ constexpr AtmosK kAtmosSL_K = {kAtmosSL, 0x1.5a535faa0890cp+19, 0x1.7a76ee408d54
 // the (1 + x)^3.5 - 1 and y^(2/7) - 1 steps).  Saves four powers, two square roots and
 // two divisions on the climbing / descending aircraft's substep chain.
 struct LimK { double tvmin, tvmax, tvmax_gd; };
-constexpr LimK kLimHMAX = {0x1.1a6f5cb8f15bcp+7, 0x1.2959d9f9eb8a9p+8, 0x1.5760fe910b786p+7};
-constexpr LimK kLimSL = {0x1.2016b11c07f8ap+6, 0x1.45fffffdd454fp+7, 0x1.61ffffff45996p+6};
+constexpr LimK kLimHMAX = {0x1.1a6f5cb8f15bcp+7, 0x1.2959d9f9eb8a9p+8, 0x1.5933010daea59p+7};
+constexpr LimK kLimSL = {0x1.2016b11c07f8ap+6, 0x1.45fffffdd454fp+7, 0x1.63ffffff427a1p+6};
 
 // vtas2cas / vcas2tas: both powers by polynomial with one range test for the pair (a
 // branch is ~80 cycles of latency even when not taken); outside, both by the libm.

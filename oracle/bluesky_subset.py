@@ -58,7 +58,8 @@ Tstrat = 216.65         # K
 # logs (scripts/common/results/logs_backup/*_SAC.csv) by rolling out its saved actors
 # (tests/golden/sac_actors.npz; tests/test_ref_logs.py):
 #   VMAX_CAS: Descent + Vertical episode-length distributions (162.5..163.5 bracket)
-#   VMAX_GD:  Horizontal + PlanWaypoint episode lengths (aircraft created at alt 0)
+#   VMAX_GD:  was fitted to Horizontal + PlanWaypoint episode lengths (88.5); round 5 pins it
+#             at 89.0 from the saved models' observations (tests/test_last_obs.py)
 # VSMAX is NOT fitted (round 4): the round-2 fit (12.1 m/s, from Descent SAC's final
 # altitude) bound below the envs' 12.5 m/s command and the held-out DDPG / PPO actors
 # rejected it; it is 4000 fpm, non-binding for every command the envs issue.
@@ -69,12 +70,15 @@ EPS_SPD = 0.01                        # traf.eps
 AXMAX = 0.5                           # perf.axmax  (m/s2), airborne
 VMIN_CAS = 140.0 * kts                # perf.vmin   (m/s CAS)
 VMAX_CAS = 163.0                      # perf.vmax   (m/s CAS), fitted
-MMO = 0.82                            # perf.mmo
+MMO = 0.80                            # perf.mmo: the reference's saved Merge states hold the
+                                      # ownship at M0.80 (tests/golden/extract_last_obs.py)
 HMAX = 39800.0 * ft                   # perf.hmax   (m)
 VSMAX = 4000.0 * fpm                  # perf.vsmax  (m/s), non-binding (the fit is withdrawn)
 VSMIN = -4000.0 * fpm                 # perf.vsmin  (m/s); unreachable: the intent is |ap.vs|
 GD_ALT_FT = 75.0                      # OpenAP phase GD: alt <= 75 ft
-VMAX_GD = 88.5                        # perf.vmax in phase GD (m/s CAS), fitted; vmin 0
+VMAX_GD = 89.0                        # perf.vmax in phase GD (m/s CAS); vmin 0.  Pinned by the
+                                      # reference's saved HorizontalCR states: every aircraft at
+                                      # TAS 89.000 at alt 0 (was fitted: 88.5)
 AXMAX_GD = 2.0                        # perf.axmax in phase GD (m/s2)
 
 # asas defaults (bluesky settings: asas_pzr, asas_pzh, asas_dtlookahead)
