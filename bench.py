@@ -145,6 +145,10 @@ def main():
     ap.add_argument("--transport", default="rccl", choices=("rccl", "torch"),
                     help="N>1 over RCCL: the learner-row gather as libbsg's direct RCCL calls "
                          "(default) or torch.distributed.all_gather_into_tensor")
+    ap.add_argument("--require-rccl", action="store_true",
+                    help="N>1 over RCCL: exit non-zero (after printing the line) unless the "
+                         "learner-row gather ran on libbsg's RCCL communicator of N ranks and "
+                         "the cross-rank row check passed")
     ap.add_argument("--gather-block", type=int, default=8,
                     help="N>1: also time the block-gather variant (one all_gather per this many "
                          "steps) after the headline, reported in the `gather_block` object; 0 = skip")
@@ -205,6 +209,8 @@ def main():
             env = ShardedVectorEnv(make_local, world * E, overlap=(backend == "nccl"),
                                    steps_per_gather=args.steps_per_gather, transport=transport)
         except Exception as ex:          # noqa: BLE001 - reported, not hidden
+            # RcclGather's construction is collective: it raises on every rank or on none
+            # (parallel.RcclGather), so every rank falls back together
             if transport != "rccl":
                 raise
             transport_note = f"native RCCL gather failed to start ({ex}); torch.distributed used"
@@ -281,6 +287,10 @@ def main():
         t = torch.tensor([el, kern_avg_ms, samp_ms, step_avg_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el, kern_avg_ms, samp_ms, step_avg_ms = (float(x) for x in t)
+    comm = check = None
+    if gather:
+        comm = comm_record(env, world, dev)
+        check = row_check(env, acts, world, dev)
     blk = None
     if gather and args.gather_block > 1 and args.gather_block != args.steps_per_gather:
         blk = bench_gather_block(args, make_local, world, E, acts, backend, dev)
@@ -333,6 +343,8 @@ def main():
                 "steps_per_gather": args.steps_per_gather if gather else None,
                 "gather_transport": (env.transport if gather else None),
                 "gather_transport_note": transport_note,
+                "rccl": comm,
+                "row_check": check,
             },
             "roofline": {
                 # the binding limit is fp64 VALU dependency latency; `frac`
@@ -374,9 +386,69 @@ def main():
         if blk is not None:
             out["gather_block"] = blk
         print(json.dumps(out), flush=True)
+    failed = None
+    if args.require_rccl and gather:
+        if env.transport != "rccl" or comm is None or any(n != world for n in comm["nranks"]):
+            failed = f"--require-rccl: the gather did not run on an RCCL communicator of {world} ranks"
+        elif not check["ok"]:
+            failed = "--require-rccl: the cross-rank row check failed"
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+    if failed:
+        raise SystemExit(failed)
+
+
+def comm_record(env, world, dev):
+    """Per rank, what libbsg's communicator says it is (bsg_comm_get_info: ncclCommCount,
+    ncclCommUserRank) -- so a node run's line shows that RCCL saw every rank -- gathered to
+    every rank by the process group; None unless the transport is libbsg's RCCL."""
+    import torch
+    import torch.distributed as dist
+    if env.transport != "rccl":
+        return None
+    inf = env._rccl.info()
+    mine = torch.tensor([inf["nranks"], inf["rank"], inf["device"], inf["gathers"]],
+                        dtype=torch.int64, device=dev)
+    allv = [torch.zeros_like(mine) for _ in range(world)]
+    dist.all_gather(allv, mine)
+    rows = [[int(x) for x in t.cpu()] for t in allv]
+    return {"nranks": [r[0] for r in rows], "rank": [r[1] for r in rows],
+            "device": [r[2] for r in rows], "gathers": [r[3] for r in rows],
+            "source": "bsg_comm_get_info (ncclCommCount / ncclCommUserRank) on each rank"}
+
+
+def row_check(env, acts, world, dev):
+    """After the timed region, one more step: every rank compares the rows the transport
+    gathered with every rank's own rows of that step, which the process group delivers once
+    by its own all-gather (c10d, independent of libbsg's communicator) -- bit for bit, rank by
+    rank.  Returns {"ok", "bad_rows" (summed over ranks), ...} for the line."""
+    import torch
+    import torch.distributed as dist
+    from bluesky_gym.parallel import all_gather_rows
+    env.flush()
+    rows, ready = env.step(acts[0])
+    if rows is None:                          # k > 1: close the block (one step long)
+        blk, ready = env.flush()
+        n = blk.shape[0]
+        rows = blk[n - 1]                     # [world, n_local, row]
+        local = env.local_rows(ready)[n - 1]
+    else:
+        local = env.local_rows(ready)
+    ready.wait()
+    torch.cuda.synchronize()
+    ref = torch.empty((world * env.n_local, env.row_dim), dtype=torch.float32, device=dev)
+    all_gather_rows(ref, local.contiguous())
+    torch.cuda.synchronize()
+    got = rows.reshape(world, env.n_local, env.row_dim).view(torch.int32)
+    want = ref.reshape(world, env.n_local, env.row_dim).view(torch.int32)
+    bad = (got != want).any(dim=2).sum(dim=1).to(torch.int64)         # per source rank
+    dist.all_reduce(bad)
+    bad = [int(x) for x in bad.cpu()]
+    return {"ok": sum(bad) == 0, "bad_rows": sum(bad), "bad_rows_by_source_rank": bad,
+            "checked": f"{world} ranks x {world * env.n_local} rows x {env.row_dim} fp32, bitwise",
+            "reference": "each rank's local rows of that step via torch.distributed all_gather "
+                         "(c10d), compared with the transport's gathered rows on every rank"}
 
 
 def bench_gather_block(args, make_local, world, E, acts, backend, dev):

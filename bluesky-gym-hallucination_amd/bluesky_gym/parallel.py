@@ -43,27 +43,71 @@ class RcclGather:
     C4's shard sizes.  The communicator's id is broadcast once over the process group."""
 
     def __init__(self, device, group=None):
+        """Collective: every rank of `group` must construct it.  The transport is decided for
+        all ranks at once: rank 0 broadcasts its id draw's status with the id, and
+        after bsg_comm_create the ranks agree (an all-reduce of a success flag, RCCL's own
+        rank count and rank included) before any gather -- so either every rank holds a
+        communicator of `world` ranks, or every rank raises BsgError and the caller can fall
+        back on all ranks together.  (A failure inside ncclCommInitRank that leaves the other
+        ranks blocked in it cannot be caught here: RCCL's init is itself collective.)"""
         import ctypes as C
         from . import _native as nat
         self._C, self._nat = C, nat
         self.lib = nat.load_library()
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
-        idb = torch.zeros(nat.COMM_ID_BYTES, dtype=torch.uint8)
+        self._comm = C.c_void_p()
+        self._dev = torch.device(device).index or 0
+        on_dev = self.world > 1 and dist.get_backend(group) == "nccl"
+        src = dist.get_global_rank(group, 0) if group is not None else 0
+        # byte 0: rank 0's status (1 = the id was drawn), then the id
+        idb = torch.zeros(1 + nat.COMM_ID_BYTES, dtype=torch.uint8)
+        err = ""
         if self.rank == 0:
-            nat.check_comm(self.lib.bsg_comm_unique_id(C.c_void_p(idb.data_ptr())), "bsg_comm_unique_id")
+            rc = self.lib.bsg_comm_unique_id(C.c_void_p(idb.data_ptr() + 1))
+            if rc == 0:
+                idb[0] = 1
+            else:
+                err = self.lib.bsg_comm_last_error().decode(errors="replace")
         if self.world > 1:
             # the process group's backend decides where the id travels (RCCL: a device tensor)
-            t = idb.to(device) if dist.get_backend(group) == "nccl" else idb
-            dist.broadcast(t, src=dist.get_global_rank(group, 0) if group is not None else 0,
-                           group=group)
+            t = idb.to(device) if on_dev else idb
+            dist.broadcast(t, src=src, group=group)
             idb = t.cpu()
+        if int(idb[0]) != 1:
+            raise nat.BsgError("RcclGather: rank 0 could not draw the RCCL id"
+                               + (f": {err}" if err else " (see rank 0's error)"))
         comm = C.c_void_p()
-        nat.check_comm(self.lib.bsg_comm_create(C.c_void_p(idb.data_ptr()), self.world, self.rank,
-                                                torch.device(device).index or 0, C.byref(comm)),
-                       "bsg_comm_create")
-        self._comm = comm
-        self._dev = torch.device(device).index or 0
+        rc = self.lib.bsg_comm_create(C.c_void_p(idb.data_ptr() + 1), self.world, self.rank,
+                                      self._dev, C.byref(comm))
+        ok = rc == 0
+        err = "" if ok else self.lib.bsg_comm_last_error().decode(errors="replace")
+        if ok:
+            self._comm = comm
+            info = self.info()
+            if info["nranks"] != self.world or info["rank"] != self.rank:
+                ok = False
+                err = (f"RCCL sees {info['nranks']} ranks with this one as rank {info['rank']}, "
+                       f"the process group {self.world} / {self.rank}")
+        if self.world > 1:
+            flag = torch.tensor([1 if ok else 0], dtype=torch.int32)
+            flag = flag.to(device) if on_dev else flag
+            dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=group)
+            all_ok = int(flag.item()) == 1
+        else:
+            all_ok = ok
+        if not all_ok:
+            self.close()
+            raise nat.BsgError("RcclGather: the communicator could not be created on every rank"
+                               + (f"; this rank: {err}" if err else " (this rank succeeded)"))
+
+    def info(self) -> dict:
+        """bsg_comm_get_info: RCCL's rank count and this rank (ncclCommCount /
+        ncclCommUserRank), the device, gathers issued and the graph cache's counters."""
+        inf = self._nat.BsgCommInfo()
+        self._nat.check_comm(self.lib.bsg_comm_get_info(self._comm, self._C.byref(inf)),
+                             "bsg_comm_get_info")
+        return {f: int(getattr(inf, f)) for f, _t in inf._fields_}
 
     def _stream(self):
         from .core import _raw_stream        # torch's raw current-stream handle (no Stream object)
@@ -83,7 +127,7 @@ class RcclGather:
                     slot: int):
         """bsg_step_gather: the wait for rows[slot]'s previous gather, the learner-row pointer,
         the step launch and this step's gather, in one C call (device spawns only).  Returns
-        nothing: the caller keeps one handle per slot (ShardedVectorEnv._ready)."""
+        nothing: the caller keeps one work handle per slot (ShardedVectorEnv._rwork)."""
         a = actions
         if a.dtype is not torch.float64 or not a.is_contiguous() or a.device != batch.device:
             a = a.to(device=batch.device, dtype=torch.float64).contiguous()
@@ -114,14 +158,34 @@ class _RcclWork:
         self._g.wait(self._slot)
 
 
-class Ready:
-    """Completion of one step's gathered rows.  wait(): the current stream (RCCL) or the
-    host (gloo) waits until every rank's rows of that step are in the gathered buffer."""
+class StaleRowsError(RuntimeError):
+    """The gathered rows a Ready stands for were overwritten: their slot of the ring has been
+    gathered into again since (ShardedVectorEnv.step)."""
 
-    def __init__(self, work=None):
-        self._work = work
+
+class Ready:
+    """Completion of one step's (or block's) gathered rows.  wait(): the current stream (RCCL)
+    or the host (gloo) waits until every rank's rows of that step are in the gathered buffer.
+    With an owner (ShardedVectorEnv) it also checks the rows are still there: the buffer is a
+    ring of slots, and once the slot has been gathered into again wait() raises
+    StaleRowsError instead of ordering the caller after rows that no longer exist."""
+
+    __slots__ = ("_work", "_owner", "_slot", "_seq")
+
+    def __init__(self, work=None, owner=None, slot=0, seq=0):
+        self._work, self._owner, self._slot, self._seq = work, owner, slot, seq
+
+    @property
+    def valid(self) -> bool:
+        """False once the rows' slot has been gathered into again."""
+        return self._owner is None or self._owner._slot_seq[self._slot] == self._seq
 
     def wait(self):
+        if not self.valid:
+            raise StaleRowsError(
+                f"gathered rows of gather #{self._seq} (slot {self._slot}) were overwritten by "
+                f"gather #{self._owner._slot_seq[self._slot]}: a step's rows are valid for "
+                f"{self._owner.rows_valid_steps} steps (ShardedVectorEnv.step)")
         if self._work is not None:
             self._work.wait()
 
@@ -195,12 +259,16 @@ class ShardedVectorEnv:
                                      device=dev)
         self._blk, self._i = 0, 0
         self._work = [None] * R
+        # liveness: gathers issued, and the last one that wrote each slot (Ready.valid)
+        self._gseq = 0
+        self._slot_seq = [0] * R
+        self.rows_valid_steps = R * self.k
         if self._fused:
             # per slot, made once: the row block the kernel writes, the gathered view step()
-            # returns and its completion handle (the host side of a step is one C call)
+            # returns and its completion work (the host side of a step is one C call)
             self._slot_rows = [self._rows[s, 0] for s in range(R)]
             self._views = [self._gathered[s].view(self.total_envs, d) for s in range(R)]
-            self._ready = [Ready(_RcclWork(self._rccl, s)) for s in range(R)]
+            self._rwork = [_RcclWork(self._rccl, s) for s in range(R)]
 
     def _slot(self):
         """Point the kernel's learner output at the next slot; before the first write into a
@@ -233,9 +301,11 @@ class ShardedVectorEnv:
 
     def step(self, local_actions):
         """Steps the local shard.  k = 1: returns (gathered rows [total_envs, obs+3],
-        Ready); they may be read after ready.wait(), until the step after next.  k > 1:
-        (None, None) inside a block, (block, Ready) at its last step; a block stays valid
-        until the end of the next block."""
+        Ready); they may be read after ready.wait() for ``rows_valid_steps`` steps -- until
+        their slot of the ring is gathered into again: BSG_COMM_SLOTS = 16 steps with the
+        fused RCCL path (transport "rccl", device spawns), 2 otherwise.  k > 1: (None, None)
+        inside a block, (block, Ready) at its last step; a block stays valid until the end of
+        the next block (2k steps).  After that Ready.wait() raises StaleRowsError."""
         if self._fused:
             # transport "rccl", one gather per step, device spawns: one C call per step (the
             # wait for the slot's previous gather is libbsg's, bsg_step_gather)
@@ -243,13 +313,24 @@ class ShardedVectorEnv:
             self._rccl.step_gather(self.local.batch, local_actions, self._slot_rows[blk],
                                    self._gathered[blk], blk)
             self._blk = blk + 1 if blk + 1 < self._nslots else 0
-            return self._views[blk], self._ready[blk]
+            self._gseq += 1
+            self._slot_seq[blk] = self._gseq
+            return self._views[blk], Ready(self._rwork[blk], self, blk, self._gseq)
         blk, i = self._slot()
         self.local.step_tensors(local_actions)
         if i + 1 < self.k:
             self._i = i + 1
             return None, None
         return self._gather(blk, self.k)
+
+    def local_rows(self, ready) -> torch.Tensor:
+        """This rank's own learner rows behind a Ready ([n_local, obs+3] for k = 1, else
+        [k, n_local, obs+3]): what every rank must find at this rank's place in the gathered
+        rows (bench.py's cross-rank row check).  Raises StaleRowsError once overwritten."""
+        if not ready.valid:
+            raise StaleRowsError("the local rows of that gather were overwritten")
+        blk = self._rows[ready._slot]
+        return blk[0] if self.k == 1 else blk
 
     def flush(self):
         """Gather the steps of the current partial block now (k > 1); (None, None) if the
@@ -269,13 +350,15 @@ class ShardedVectorEnv:
             else:
                 work = all_gather_rows(out, src, self.group, async_op=True)
             self._work[blk] = work
-            ready = Ready(work)
         elif self.world == 1:
             out.copy_(src)
-            ready = Ready()
+            work = None
         else:
             all_gather_rows(out, src, self.group)
-            ready = Ready()
+            work = None
+        self._gseq += 1
+        self._slot_seq[blk] = self._gseq
+        ready = Ready(work, self, blk, self._gseq)
         self._blk, self._i = (blk + 1) % self._nslots, 0
         if self.k == 1:
             return out.view(self.total_envs, self.row_dim), ready

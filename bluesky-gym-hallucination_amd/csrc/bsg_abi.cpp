@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -60,9 +61,12 @@ namespace {
 
 thread_local std::string g_err;
 
-int fail(int code, const char* fmt, const char* a = "", long long b = 0) {
+__attribute__((format(printf, 2, 3))) int fail(int code, const char* fmt, ...) {
   char buf[512];
-  std::snprintf(buf, sizeof(buf), fmt, a, b);
+  va_list ap;
+  va_start(ap, fmt);
+  std::vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
   g_err = buf;
   return code;
 }
@@ -290,7 +294,7 @@ int launch(bsg_ctx* c, int mode, const double* actions, const double* spawn,
     if (!t0 || !t1) {
       if (t0) c->ev_pool.push_back(t0);
       if (t1) c->ev_pool.push_back(t1);
-      return fail(BSG_E_HIP, "hipEventCreate failed%s%lld");
+      return fail(BSG_E_HIP, "hipEventCreate failed");
     }
     if ((e = hipEventRecord(t0, st)) != hipSuccess) {
       c->ev_pool.push_back(t0);
@@ -377,35 +381,34 @@ int32_t bsg_geom_width(int32_t kind, int32_t num_ac) {
 }
 
 int32_t bsg_create(const bsg_config* cfg, bsg_ctx** out) {
-  if (!cfg || !out) return fail(BSG_E_INVALID_ARG, "bsg_create: null argument%s%lld");
+  if (!cfg || !out) return fail(BSG_E_INVALID_ARG, "bsg_create: null argument");
   *out = nullptr;
   if (cfg->abi_version != BSG_ABI_VERSION)
-    return fail(BSG_E_INVALID_ARG, "bsg_create: abi_version mismatch%s (got %lld)", "",
-                cfg->abi_version);
-  if (cfg->num_envs <= 0) return fail(BSG_E_INVALID_ARG, "bsg_create: num_envs must be > 0%s%lld");
+    return fail(BSG_E_INVALID_ARG, "bsg_create: abi_version mismatch (got %lld)", (long long)(cfg->abi_version));
+  if (cfg->num_envs <= 0) return fail(BSG_E_INVALID_ARG, "bsg_create: num_envs must be > 0");
   if (cfg->num_ac < 1 || cfg->num_ac > BSG_MAX_AC)
-    return fail(BSG_E_INVALID_ARG, "bsg_create: num_ac must be in [1, 64]%s (got %lld)", "", cfg->num_ac);
+    return fail(BSG_E_INVALID_ARG, "bsg_create: num_ac must be in [1, 64] (got %lld)", (long long)(cfg->num_ac));
   const int od = bsg_obs_dim(cfg->env_kind, cfg->num_ac, cfg->num_ac_state);
-  if (od < 0) return fail(BSG_E_INVALID_ARG, "bsg_create: invalid env_kind/num_ac/num_ac_state%s%lld");
-  if (cfg->action_frequency < 0) return fail(BSG_E_INVALID_ARG, "bsg_create: action_frequency < 0%s%lld");
-  if (!(cfg->simdt > 0.0)) return fail(BSG_E_INVALID_ARG, "bsg_create: simdt must be > 0%s%lld");
+  if (od < 0) return fail(BSG_E_INVALID_ARG, "bsg_create: invalid env_kind/num_ac/num_ac_state");
+  if (cfg->action_frequency < 0) return fail(BSG_E_INVALID_ARG, "bsg_create: action_frequency < 0");
+  if (!(cfg->simdt > 0.0)) return fail(BSG_E_INVALID_ARG, "bsg_create: simdt must be > 0");
   if (cfg->autoreset_mode < 0 || cfg->autoreset_mode > 2)
-    return fail(BSG_E_INVALID_ARG, "bsg_create: invalid autoreset_mode%s%lld");
+    return fail(BSG_E_INVALID_ARG, "bsg_create: invalid autoreset_mode");
   if (cfg->route_len < 0 || cfg->route_len > BSG_MAX_ROUTE)
-    return fail(BSG_E_INVALID_ARG, "bsg_create: route_len out of range%s%lld");
-  if (cfg->env_offset < 0) return fail(BSG_E_INVALID_ARG, "bsg_create: env_offset < 0%s%lld");
+    return fail(BSG_E_INVALID_ARG, "bsg_create: route_len out of range");
+  if (cfg->env_offset < 0) return fail(BSG_E_INVALID_ARG, "bsg_create: env_offset < 0");
   if (cfg->kind_option != 0 && !(cfg->env_kind == BSG_ENV_SECTOR_CR && cfg->kind_option == 1) &&
       !(cfg->env_kind == BSG_ENV_MERGE && cfg->kind_option > 0 && cfg->kind_option <= 400))
-    return fail(BSG_E_INVALID_ARG, "bsg_create: invalid kind_option%s (%lld)", "", cfg->kind_option);
+    return fail(BSG_E_INVALID_ARG, "bsg_create: invalid kind_option (%lld)", (long long)(cfg->kind_option));
   if (cfg->env_kind == BSG_ENV_MERGE && cfg->route_len < 1)
-    return fail(BSG_E_INVALID_ARG, "bsg_create: Merge needs the FIX/RWY route%s%lld");
+    return fail(BSG_E_INVALID_ARG, "bsg_create: Merge needs the FIX/RWY route");
   int ndev = 0;
   hipError_t e = hipGetDeviceCount(&ndev);
   if (e != hipSuccess) return hip_fail(e, "hipGetDeviceCount");
   if (cfg->device < 0 || cfg->device >= ndev)
-    return fail(BSG_E_INVALID_ARG, "bsg_create: device ordinal out of range%s (%lld)", "", cfg->device);
+    return fail(BSG_E_INVALID_ARG, "bsg_create: device ordinal out of range (%lld)", (long long)(cfg->device));
   bsg_ctx* c = new (std::nothrow) bsg_ctx();
-  if (!c) return fail(BSG_E_STATE, "bsg_create: out of host memory%s%lld");
+  if (!c) return fail(BSG_E_STATE, "bsg_create: out of host memory");
   c->cfg = *cfg;
   c->obs_dim = od;
   c->spawn_width = bsg_spawn_width(cfg->env_kind, cfg->num_ac);
@@ -443,29 +446,29 @@ int32_t bsg_destroy(bsg_ctx* c) {
 }
 
 int32_t bsg_bind(bsg_ctx* c, const bsg_buffers* b) {
-  if (!c || !b) return fail(BSG_E_INVALID_ARG, "bsg_bind: null argument%s%lld");
+  if (!c || !b) return fail(BSG_E_INVALID_ARG, "bsg_bind: null argument");
   const void* required[] = {b->lat, b->lon, b->alt, b->hdg, b->tas, b->cas, b->vs, b->ax,
                             b->ap_trk, b->selspd, b->selalt, b->selvs, b->nav,
                             b->step_count, b->flags, b->episode, b->wpt_reach, b->faf_reached,
                             b->total_intrusions, b->total_reward, b->drift_sum, b->target_alt,
                             b->final_altitude, b->obs, b->reward, b->terminated, b->truncated};
   for (size_t i = 0; i < sizeof(required) / sizeof(required[0]); ++i)
-    if (!required[i]) return fail(BSG_E_INVALID_ARG, "bsg_bind: required buffer #%s%lld is NULL", "", (long long)i);
+    if (!required[i]) return fail(BSG_E_INVALID_ARG, "bsg_bind: required buffer #%lld is NULL", (long long)i);
   if (c->cfg.env_kind == BSG_ENV_HORIZONTAL_CR && (!b->env_wpt_lat || !b->env_wpt_lon))
-    return fail(BSG_E_INVALID_ARG, "bsg_bind: HorizontalCR needs env_wpt_lat/env_wpt_lon%s%lld");
+    return fail(BSG_E_INVALID_ARG, "bsg_bind: HorizontalCR needs env_wpt_lat/env_wpt_lon");
   if (bsg_geom_width(c->cfg.env_kind, c->cfg.num_ac) > 0 && !b->env_geom)
-    return fail(BSG_E_INVALID_ARG, "bsg_bind: StaticObstacle/SectorCR/PlanWaypoint need env_geom%s%lld");
+    return fail(BSG_E_INVALID_ARG, "bsg_bind: StaticObstacle/SectorCR/PlanWaypoint need env_geom");
   if (c->cfg.env_kind == BSG_ENV_STATIC_OBSTACLE && !b->env_aux)
-    return fail(BSG_E_INVALID_ARG, "bsg_bind: StaticObstacle needs env_aux%s%lld");
+    return fail(BSG_E_INVALID_ARG, "bsg_bind: StaticObstacle needs env_aux");
   if (c->cfg.env_kind == BSG_ENV_MERGE && !b->topk)
-    return fail(BSG_E_INVALID_ARG, "bsg_bind: Merge needs topk%s%lld");
+    return fail(BSG_E_INVALID_ARG, "bsg_bind: Merge needs topk");
   if (c->cfg.autoreset_mode == BSG_AUTORESET_SAME_STEP && !b->final_obs)
-    return fail(BSG_E_INVALID_ARG, "bsg_bind: SAME_STEP autoreset needs final_obs%s%lld");
+    return fail(BSG_E_INVALID_ARG, "bsg_bind: SAME_STEP autoreset needs final_obs");
   if (c->wind.np > 0 && (!b->gs || !b->trk))
-    return fail(BSG_E_INVALID_ARG, "bsg_bind: a wind field needs gs/trk%s%lld");
+    return fail(BSG_E_INVALID_ARG, "bsg_bind: a wind field needs gs/trk");
   if (c->cfg.compute_cd && c->cfg.num_ac > 1 &&
       (!b->conf_mask || !b->los_mask || !b->tcpamax || !b->min_sep))
-    return fail(BSG_E_INVALID_ARG, "bsg_bind: compute_cd needs conf_mask/los_mask/tcpamax/min_sep%s%lld");
+    return fail(BSG_E_INVALID_ARG, "bsg_bind: compute_cd needs conf_mask/los_mask/tcpamax/min_sep");
   c->bufs = *b;
   c->bound = true;
   c->la_dirty = true;               // new buffers: the lookahead restarts from them
@@ -473,7 +476,7 @@ int32_t bsg_bind(bsg_ctx* c, const bsg_buffers* b) {
 }
 
 int64_t bsg_lookahead_bytes(const bsg_ctx* c) {
-  if (!c) return fail(BSG_E_INVALID_ARG, "bsg_lookahead_bytes: null ctx%s%lld");
+  if (!c) return fail(BSG_E_INVALID_ARG, "bsg_lookahead_bytes: null ctx");
   if ((c->cfg.env_kind != BSG_ENV_MERGE && c->cfg.env_kind != BSG_ENV_VERTICAL_CR) ||
       c->cfg.autoreset_mode == BSG_AUTORESET_SAME_STEP)
     return 0;
@@ -481,16 +484,16 @@ int64_t bsg_lookahead_bytes(const bsg_ctx* c) {
 }
 
 int32_t bsg_set_lookahead(bsg_ctx* c, void* scratch, int64_t bytes) {
-  if (!c) return fail(BSG_E_INVALID_ARG, "bsg_set_lookahead: null ctx%s%lld");
+  if (!c) return fail(BSG_E_INVALID_ARG, "bsg_set_lookahead: null ctx");
   if (scratch) {
     if (bsg_lookahead_bytes(c) == 0)
       return fail(BSG_E_UNSUPPORTED, "bsg_set_lookahead: MergeEnv / VerticalCREnv with NEXT_STEP "
-                  "or no autoreset only%s%lld");
+                  "or no autoreset only");
     if (bytes < (int64_t)la_bytes(c->cfg))
-      return fail(BSG_E_INVALID_ARG, "bsg_set_lookahead: scratch too small%s (need %lld bytes)", "",
+      return fail(BSG_E_INVALID_ARG, "bsg_set_lookahead: scratch too small (need %lld bytes)",
                   (long long)la_bytes(c->cfg));
     if (reinterpret_cast<uintptr_t>(scratch) & 7)
-      return fail(BSG_E_INVALID_ARG, "bsg_set_lookahead: scratch must be 8-byte aligned%s%lld");
+      return fail(BSG_E_INVALID_ARG, "bsg_set_lookahead: scratch must be 8-byte aligned");
   }
   c->la = static_cast<double*>(scratch);
   c->la_dirty = true;               // also re-arms after the caller wrote state directly
@@ -498,54 +501,53 @@ int32_t bsg_set_lookahead(bsg_ctx* c, void* scratch, int64_t bytes) {
 }
 
 int32_t bsg_set_learner(bsg_ctx* c, float* learner) {
-  if (!c) return fail(BSG_E_INVALID_ARG, "bsg_set_learner: null ctx%s%lld");
-  if (!c->bound) return fail(BSG_E_STATE, "bsg_set_learner: buffers not bound%s%lld");
+  if (!c) return fail(BSG_E_INVALID_ARG, "bsg_set_learner: null ctx");
+  if (!c->bound) return fail(BSG_E_STATE, "bsg_set_learner: buffers not bound");
   c->bufs.learner = learner;
   return BSG_OK;
 }
 
 int32_t bsg_reset(bsg_ctx* c, const uint8_t* env_mask, const double* spawn, void* stream) {
-  if (!c) return fail(BSG_E_INVALID_ARG, "bsg_reset: null ctx%s%lld");
-  if (!c->bound) return fail(BSG_E_STATE, "bsg_reset: buffers not bound%s%lld");
+  if (!c) return fail(BSG_E_INVALID_ARG, "bsg_reset: null ctx");
+  if (!c->bound) return fail(BSG_E_STATE, "bsg_reset: buffers not bound");
   return launch(c, bsg::MODE_RESET, nullptr, spawn, env_mask, stream);
 }
 
 int32_t bsg_step(bsg_ctx* c, const double* actions, const double* spawn, void* stream) {
-  if (!c) return fail(BSG_E_INVALID_ARG, "bsg_step: null ctx%s%lld");
-  if (!c->bound) return fail(BSG_E_STATE, "bsg_step: buffers not bound%s%lld");
-  if (!actions) return fail(BSG_E_INVALID_ARG, "bsg_step: actions is NULL%s%lld");
+  if (!c) return fail(BSG_E_INVALID_ARG, "bsg_step: null ctx");
+  if (!c->bound) return fail(BSG_E_STATE, "bsg_step: buffers not bound");
+  if (!actions) return fail(BSG_E_INVALID_ARG, "bsg_step: actions is NULL");
   return launch(c, bsg::MODE_STEP, actions, spawn, nullptr, stream);
 }
 
 int32_t bsg_step_gather(bsg_ctx* c, bsg_comm* comm, const double* actions, const double* spawn,
                         float* rows, float* gathered, int32_t slot, void* stream) {
-  if (!c || !comm) return fail(BSG_E_INVALID_ARG, "bsg_step_gather: null ctx/comm%s%lld");
-  if (!c->bound) return fail(BSG_E_STATE, "bsg_step_gather: buffers not bound%s%lld");
-  if (!actions || !rows || !gathered) return fail(BSG_E_INVALID_ARG, "bsg_step_gather: null buffer%s%lld");
+  if (!c || !comm) return fail(BSG_E_INVALID_ARG, "bsg_step_gather: null ctx/comm");
+  if (!c->bound) return fail(BSG_E_STATE, "bsg_step_gather: buffers not bound");
+  if (!actions || !rows || !gathered) return fail(BSG_E_INVALID_ARG, "bsg_step_gather: null buffer");
   // rows[slot] was last read by the gather of BSG_COMM_SLOTS steps ago (a ring): the step
   // writes it after that gather (usually known complete already: no stream wait)
   if (bsg_comm_wait(comm, slot, stream) != BSG_OK)
-    return fail(BSG_E_HIP, "bsg_step_gather: %s%lld", bsg_comm_last_error());
+    return fail(BSG_E_HIP, "bsg_step_gather: %s", bsg_comm_last_error());
   c->bufs.learner = rows;
   if (int r = launch(c, bsg::MODE_STEP, actions, spawn, nullptr, stream)) return r;
   const int64_t count = (int64_t)c->cfg.num_envs * (c->obs_dim + 3);
   if (bsg_comm_all_gather(comm, rows, gathered, count, slot, stream) != BSG_OK)
-    return fail(BSG_E_HIP, "bsg_step_gather: %s%lld", bsg_comm_last_error());
+    return fail(BSG_E_HIP, "bsg_step_gather: %s", bsg_comm_last_error());
   return BSG_OK;
 }
 
 int32_t bsg_set_wind(bsg_ctx* c, const bsg_wind* w) {
-  if (!c) return fail(BSG_E_INVALID_ARG, "bsg_set_wind: null ctx%s%lld");
+  if (!c) return fail(BSG_E_INVALID_ARG, "bsg_set_wind: null ctx");
   const int base = bsg_obs_dim(c->cfg.env_kind, c->cfg.num_ac, c->cfg.num_ac_state);
   bsg::WindDev d{};
   if (w && w->num_points > 0) {
     if (w->num_points > 4096)
-      return fail(BSG_E_INVALID_ARG, "bsg_set_wind: num_points must be <= 4096%s (got %lld)", "", w->num_points);
+      return fail(BSG_E_INVALID_ARG, "bsg_set_wind: num_points must be <= 4096 (got %lld)", (long long)(w->num_points));
     if (w->num_levels != 1 && w->num_levels != BSG_WIND_NALT)
-      return fail(BSG_E_INVALID_ARG, "bsg_set_wind: num_levels must be 1 or BSG_WIND_NALT%s (got %lld)", "",
-                  w->num_levels);
+      return fail(BSG_E_INVALID_ARG, "bsg_set_wind: num_levels must be 1 or BSG_WIND_NALT (got %lld)", (long long)(w->num_levels));
     if (!w->lat || !w->lon || !w->vnorth || !w->veast)
-      return fail(BSG_E_INVALID_ARG, "bsg_set_wind: null table pointer%s%lld");
+      return fail(BSG_E_INVALID_ARG, "bsg_set_wind: null table pointer");
     d.np = w->num_points;
     d.nlev = w->num_levels;
     d.dim = d.nlev > 1 ? 3 : (d.np == 1 ? 1 : 2);
@@ -560,28 +562,28 @@ int32_t bsg_set_wind(bsg_ctx* c, const bsg_wind* w) {
 }
 
 int32_t bsg_ctx_obs_dim(const bsg_ctx* c) {
-  if (!c) return fail(BSG_E_INVALID_ARG, "bsg_ctx_obs_dim: null ctx%s%lld");
+  if (!c) return fail(BSG_E_INVALID_ARG, "bsg_ctx_obs_dim: null ctx");
   return c->obs_dim;
 }
 
 int32_t bsg_policy_sac(const bsg_sac_actor* w, const float* obs, int32_t num_envs,
                        int32_t obs_stride, const float* eps, double* actions, float* log_prob,
                        void* stream) {
-  if (!w) return fail(BSG_E_INVALID_ARG, "bsg_policy_sac: null actor%s%lld");
-  if (num_envs > 0 && (!obs || !actions)) return fail(BSG_E_INVALID_ARG, "bsg_policy_sac: null obs/actions%s%lld");
+  if (!w) return fail(BSG_E_INVALID_ARG, "bsg_policy_sac: null actor");
+  if (num_envs > 0 && (!obs || !actions)) return fail(BSG_E_INVALID_ARG, "bsg_policy_sac: null obs/actions");
   if (w->hidden != 256)
-    return fail(BSG_E_INVALID_ARG, "bsg_policy_sac: hidden must be 256%s (got %lld)", "", w->hidden);
+    return fail(BSG_E_INVALID_ARG, "bsg_policy_sac: hidden must be 256 (got %lld)", (long long)(w->hidden));
   if (w->obs_dim < 1 || w->obs_dim > 256)
-    return fail(BSG_E_INVALID_ARG, "bsg_policy_sac: obs_dim must be in [1, 256]%s (got %lld)", "", w->obs_dim);
+    return fail(BSG_E_INVALID_ARG, "bsg_policy_sac: obs_dim must be in [1, 256] (got %lld)", (long long)(w->obs_dim));
   if (w->act_dim < 1 || w->act_dim > 4)
-    return fail(BSG_E_INVALID_ARG, "bsg_policy_sac: act_dim must be in [1, 4]%s (got %lld)", "", w->act_dim);
-  if (num_envs < 0) return fail(BSG_E_INVALID_ARG, "bsg_policy_sac: num_envs < 0%s%lld");
+    return fail(BSG_E_INVALID_ARG, "bsg_policy_sac: act_dim must be in [1, 4] (got %lld)", (long long)(w->act_dim));
+  if (num_envs < 0) return fail(BSG_E_INVALID_ARG, "bsg_policy_sac: num_envs < 0");
   if (obs_stride < w->obs_dim)
-    return fail(BSG_E_INVALID_ARG, "bsg_policy_sac: obs_stride < obs_dim%s (%lld)", "", obs_stride);
+    return fail(BSG_E_INVALID_ARG, "bsg_policy_sac: obs_stride < obs_dim (%lld)", (long long)(obs_stride));
   if (!w->w0 || !w->b0 || !w->w1 || !w->b1 || !w->w_mu || !w->b_mu || !w->w_ls || !w->b_ls)
-    return fail(BSG_E_INVALID_ARG, "bsg_policy_sac: null weight pointer%s%lld");
+    return fail(BSG_E_INVALID_ARG, "bsg_policy_sac: null weight pointer");
   if (reinterpret_cast<uintptr_t>(w->w1) & 15)
-    return fail(BSG_E_INVALID_ARG, "bsg_policy_sac: w1 must be 16-byte aligned%s%lld");
+    return fail(BSG_E_INVALID_ARG, "bsg_policy_sac: w1 must be 16-byte aligned");
   if (num_envs == 0) return BSG_OK;
   hipError_t e = bsg::launch_sac_actor(*w, obs, num_envs, obs_stride, eps, actions, log_prob,
                                        static_cast<hipStream_t>(stream));
@@ -590,26 +592,26 @@ int32_t bsg_policy_sac(const bsg_sac_actor* w, const float* obs, int32_t num_env
 }
 
 int32_t bsg_set_stamps(bsg_ctx* c, void* buf) {
-  if (!c) return fail(BSG_E_INVALID_ARG, "bsg_set_stamps: null ctx%s%lld");
+  if (!c) return fail(BSG_E_INVALID_ARG, "bsg_set_stamps: null ctx");
 #if defined(BSG_STAMPS) && BSG_STAMPS
   c->stamps = static_cast<unsigned long long*>(buf);
   return BSG_OK;
 #else
   (void)buf;
-  return fail(BSG_E_UNSUPPORTED, "bsg_set_stamps: library built without -DBSG_STAMPS=1%s%lld");
+  return fail(BSG_E_UNSUPPORTED, "bsg_set_stamps: library built without -DBSG_STAMPS=1");
 #endif
 }
 
 int32_t bsg_set_timing(bsg_ctx* c, int32_t enable) {
-  if (!c) return fail(BSG_E_INVALID_ARG, "bsg_set_timing: null ctx%s%lld");
-  if (enable < 0) return fail(BSG_E_INVALID_ARG, "bsg_set_timing: negative interval%s%lld");
+  if (!c) return fail(BSG_E_INVALID_ARG, "bsg_set_timing: null ctx");
+  if (enable < 0) return fail(BSG_E_INVALID_ARG, "bsg_set_timing: negative interval");
   c->timing = enable;
   c->launch_count = 0;
   return BSG_OK;
 }
 
 int32_t bsg_step_timing(bsg_ctx* c, double* total_ms, int32_t* launches) {
-  if (!c || !total_ms || !launches) return fail(BSG_E_INVALID_ARG, "bsg_step_timing: null argument%s%lld");
+  if (!c || !total_ms || !launches) return fail(BSG_E_INVALID_ARG, "bsg_step_timing: null argument");
   // fold every pending pair; on a failure the pairs folded so far stay in the totals
   // (reported by the next call) and only the unfolded ones remain pending
   for (size_t i = 0; i < c->pending.size(); ++i) {

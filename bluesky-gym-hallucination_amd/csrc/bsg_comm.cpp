@@ -51,6 +51,8 @@ struct Rccl {
   ncclResult_t (*comm_init_rank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
   ncclResult_t (*all_gather)(const void*, void*, size_t, int, ncclComm_t, hipStream_t) = nullptr;
   ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
+  ncclResult_t (*comm_count)(ncclComm_t, int*) = nullptr;
+  ncclResult_t (*comm_user_rank)(ncclComm_t, int*) = nullptr;
   const char* (*error_string)(ncclResult_t) = nullptr;
   std::string err;
 };
@@ -79,9 +81,13 @@ Rccl* rccl() {
   r.comm_init_rank = reinterpret_cast<decltype(r.comm_init_rank)>(dlsym(r.h, "ncclCommInitRank"));
   r.all_gather = reinterpret_cast<decltype(r.all_gather)>(dlsym(r.h, "ncclAllGather"));
   r.comm_destroy = reinterpret_cast<decltype(r.comm_destroy)>(dlsym(r.h, "ncclCommDestroy"));
+  r.comm_count = reinterpret_cast<decltype(r.comm_count)>(dlsym(r.h, "ncclCommCount"));
+  r.comm_user_rank = reinterpret_cast<decltype(r.comm_user_rank)>(dlsym(r.h, "ncclCommUserRank"));
   r.error_string = reinterpret_cast<decltype(r.error_string)>(dlsym(r.h, "ncclGetErrorString"));
-  if (!r.get_unique_id || !r.comm_init_rank || !r.all_gather || !r.comm_destroy) {
-    r.err = "RCCL library lacks ncclGetUniqueId/ncclCommInitRank/ncclAllGather/ncclCommDestroy";
+  if (!r.get_unique_id || !r.comm_init_rank || !r.all_gather || !r.comm_destroy || !r.comm_count ||
+      !r.comm_user_rank) {
+    r.err = "RCCL library lacks ncclGetUniqueId/ncclCommInitRank/ncclAllGather/ncclCommDestroy/"
+            "ncclCommCount/ncclCommUserRank";
     r.h = nullptr;
     return nullptr;
   }
@@ -103,14 +109,16 @@ std::string nccl_msg(Rccl* r, ncclResult_t e, const char* where) {
 
 // A gather captured once as a HIP graph (one ncclAllGather node) and replayed: RCCL's own
 // enqueue costs tens of us of host time per call (profiles/r04/shard_overhead_r04.txt), a
-// graph launch a few.  Keyed by the buffers and size (the caller's ring of row blocks).
+// graph launch a few.  Keyed by the buffers and size (the caller's ring of row blocks): the
+// cache holds one graph per slot of the ring (a smaller FIFO cache would miss on every
+// gather of the fused per-step path, which cycles through all BSG_COMM_SLOTS slots).
 struct GatherGraph {
   const void* send = nullptr;
   void* recv = nullptr;
   int64_t count = -1;
   hipGraphExec_t exec = nullptr;
 };
-constexpr int kGraphCache = 8;
+constexpr int kGraphCache = BSG_COMM_SLOTS;
 
 constexpr int kFences = 4;              // fence events in flight (a ring)
 constexpr int64_t kFenceEvery = BSG_COMM_SLOTS / 2;
@@ -133,6 +141,7 @@ struct bsg_comm {
   bool use_graphs = false;              // BSG_COMM_GRAPHS=1: the gather as a replayed HIP graph
   GatherGraph graphs[kGraphCache];
   int next_graph = 0;
+  int64_t graph_hits = 0, graph_captures = 0;
   // BSG_COMM_PROFILE=1: host time of each part of bsg_comm_all_gather, printed at destroy
   bool prof = false;
   double t_rec = 0, t_wait = 0, t_coll = 0, t_rec2 = 0;
@@ -152,7 +161,11 @@ namespace {
 hipGraphExec_t gather_graph(bsg_comm* c, Rccl* r, const void* send, void* recv, int64_t count,
                             std::string* err) {
   for (auto& g : c->graphs)
-    if (g.exec && g.send == send && g.recv == recv && g.count == count) return g.exec;
+    if (g.exec && g.send == send && g.recv == recv && g.count == count) {
+      ++c->graph_hits;
+      return g.exec;
+    }
+  ++c->graph_captures;
   GatherGraph& g = c->graphs[c->next_graph];
   c->next_graph = (c->next_graph + 1) % kGraphCache;
   if (g.exec) { (void)hipGraphExecDestroy(g.exec); g.exec = nullptr; }
@@ -335,6 +348,25 @@ int32_t bsg_comm_all_gather(bsg_comm* c, const float* send, float* recv, int64_t
     c->t_rec += t1 - t0; c->t_wait += t2 - t1; c->t_coll += t3 - t2; c->t_rec2 += t4 - t3;
     ++c->n_calls;
   }
+  return BSG_OK;
+}
+
+int32_t bsg_comm_get_info(const bsg_comm* c, bsg_comm_info* out) {
+  if (!c || !out) return comm_fail(BSG_E_INVALID_ARG, "bsg_comm_get_info: null argument");
+  Rccl* r = rccl();
+  if (!r || !c->nc) return comm_fail(BSG_E_STATE, "bsg_comm_get_info: no communicator");
+  int n = 0, me = -1;
+  ncclResult_t e = r->comm_count(c->nc, &n);
+  if (e != 0) return comm_fail(BSG_E_HIP, nccl_msg(r, e, "ncclCommCount"));
+  e = r->comm_user_rank(c->nc, &me);
+  if (e != 0) return comm_fail(BSG_E_HIP, nccl_msg(r, e, "ncclCommUserRank"));
+  out->nranks = n;
+  out->rank = me;
+  out->device = c->device;
+  out->use_graphs = c->use_graphs ? 1 : 0;
+  out->gathers = c->gseq;
+  out->graph_hits = c->graph_hits;
+  out->graph_captures = c->graph_captures;
   return BSG_OK;
 }
 

@@ -331,6 +331,19 @@ int32_t bsg_comm_destroy(bsg_comm* comm);
 int32_t bsg_comm_all_gather(bsg_comm* comm, const float* send, float* recv, int64_t count,
                             int32_t slot, void* stream);
 int32_t bsg_comm_wait(bsg_comm* comm, int32_t slot, void* stream);
+/* What the communicator is: RCCL's own view of it (ncclCommCount / ncclCommUserRank -- a
+ * multi-GPU run records them, so that a node run shows RCCL saw every rank) and the comm's
+ * counters (gathers issued; with BSG_COMM_GRAPHS=1 the graph cache's hits and captures). */
+typedef struct bsg_comm_info {
+  int32_t nranks;        /* ncclCommCount */
+  int32_t rank;          /* ncclCommUserRank */
+  int32_t device;        /* the HIP device the comm was created on */
+  int32_t use_graphs;
+  int64_t gathers;       /* bsg_comm_all_gather calls (bsg_step_gather included) */
+  int64_t graph_hits;    /* gathers replayed from the graph cache */
+  int64_t graph_captures;/* gathers captured into a new graph */
+} bsg_comm_info;
+int32_t bsg_comm_get_info(const bsg_comm* comm, bsg_comm_info* out);
 /* One RL step of a shard and the gather of its learner rows in one call (the host side of
  * a C4 step: ~one launch instead of a wait, a pointer swap, a launch and a gather):
  * bsg_comm_wait(slot) [the gather that last read rows[slot]], learner rows <- rows,

@@ -190,3 +190,61 @@ def test_load_sb3_actor_from_zip(tmp_path):
         z.writestr("policy.pth", b2.getvalue())
     with pytest.raises(KeyError):
         load_sb3_actor(tmp_path / "bad.zip")
+
+
+def test_comm_info_struct_layout_matches_c(tmp_path):
+    prog = tmp_path / "comm_layout.c"
+    fields = [f[0] for f in nat.BsgCommInfo._fields_]
+    lines = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{HDR}"', "int main(void){",
+             'printf("%zu\\n", sizeof(bsg_comm_info));']
+    lines += [f'printf("%zu\\n", offsetof(bsg_comm_info, {f}));' for f in fields]
+    lines += ["return 0;}"]
+    prog.write_text("\n".join(lines))
+    exe = tmp_path / "comm_layout"
+    subprocess.run(["gcc", "-std=c99", "-o", str(exe), str(prog)], check=True)
+    vals = [int(v) for v in subprocess.run([str(exe)], capture_output=True, text=True,
+                                           check=True).stdout.split()]
+    assert vals[0] == C.sizeof(nat.BsgCommInfo)
+    assert vals[1:] == [getattr(nat.BsgCommInfo, f).offset for f in fields]
+
+
+def test_comm_argument_errors_before_any_device_call():
+    """bsg_comm_* validate their arguments before touching RCCL or the device (VERDICT r04
+    weak #5): null id / out pointer, rank count and rank out of range, null comm or buffers,
+    slot and count out of range -- each BSG_E_INVALID_ARG with a message naming the call."""
+    lib = nat.load_library()
+    E_INVALID = -1
+    idb = (C.c_uint8 * nat.COMM_ID_BYTES)()
+    out = C.c_void_p()
+    err = lambda: lib.bsg_comm_last_error().decode()             # noqa: E731
+    assert lib.bsg_comm_unique_id(None) == E_INVALID and "bsg_comm_unique_id" in err()
+    assert lib.bsg_comm_create(None, 2, 0, 0, C.byref(out)) == E_INVALID and "null" in err()
+    assert lib.bsg_comm_create(idb, 2, 0, 0, None) == E_INVALID
+    for nranks, rank in ((0, 0), (-1, 0), (2, 2), (2, -1), (8, 9)):
+        assert lib.bsg_comm_create(idb, nranks, rank, 0, C.byref(out)) == E_INVALID, (nranks, rank)
+        assert "rank out of range" in err() and not out.value
+    buf = (C.c_float * 4)()
+    assert lib.bsg_comm_all_gather(None, buf, buf, 4, 0, None) == E_INVALID
+    assert "bsg_comm_all_gather: null" in err()
+    # a non-null handle that is never dereferenced: the range checks come first
+    fake = C.c_void_p(8)
+    for slot, count in ((-1, 4), (nat.COMM_SLOTS, 4), (0, -1)):
+        assert lib.bsg_comm_all_gather(fake, buf, buf, count, slot, None) == E_INVALID
+        assert "out of range" in err()
+    assert lib.bsg_comm_all_gather(fake, None, buf, 4, 0, None) == E_INVALID
+    assert lib.bsg_comm_wait(None, 0, None) == E_INVALID and "null comm" in err()
+    assert lib.bsg_comm_wait(fake, nat.COMM_SLOTS, None) == E_INVALID and "slot out of range" in err()
+    info = nat.BsgCommInfo()
+    assert lib.bsg_comm_get_info(None, C.byref(info)) == E_INVALID and "null" in err()
+    assert lib.bsg_comm_destroy(None) == 0
+
+
+def test_error_messages_carry_no_stray_format_arguments():
+    """fail()'s old two-argument printf form appended a stray '0' to every message
+    without a number; the messages end where their text ends."""
+    lib = nat.load_library()
+    assert lib.bsg_step_gather(None, None, None, None, None, None, 0, None) == -1
+    assert lib.bsg_last_error() == b"bsg_step_gather: null ctx/comm"
+    assert lib.bsg_destroy(None) in (0, -1)
+    assert lib.bsg_set_wind(None, None) == -1
+    assert lib.bsg_last_error() == b"bsg_set_wind: null ctx"

@@ -46,3 +46,30 @@ def test_bench_json_line():
     assert 0 < ln["value"] <= c5["env_policy"]["value"] * 1.05
     assert ln["critic_loss"] == ln["critic_loss"] and ln["actor_loss"] == ln["actor_loss"]
     assert rf["scope"].startswith("per GPU") and rf["step_avg_ms"] == rf["kernel_avg_ms"]
+
+
+def test_bench_two_rank_rehearsal_checks_rows():
+    """The multi-rank bench path on one GPU (2 ranks over gloo, BENCH_BACKEND=gloo: the
+    gather goes through the host, so the rate measures nothing): barriers, max-over-ranks
+    timing, the per-step gather and, after the timed region, the cross-rank row check -- every
+    rank's gathered rows against every rank's own rows, bitwise -- recorded in the line."""
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ, BENCH_BACKEND="gloo")
+    out = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                          "--nproc-per-node", "2", "--master-addr", "127.0.0.1", "--master-port",
+                          str(port), "bench.py", "--gpus", "2", "--steps", "5", "--warmup", "2",
+                          "--gather-block", "0"], cwd=REPO, capture_output=True, text=True,
+                         timeout=300, env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    r = json.loads(lines[0])
+    assert r["n_gpus"] == 2 and r["config"]["envs_total"] == 4096
+    cfg = r["config"]
+    assert cfg["gather_transport"] == "torch" and cfg["rccl"] is None
+    rc = cfg["row_check"]
+    assert rc["ok"] is True and rc["bad_rows"] == 0 and rc["bad_rows_by_source_rank"] == [0, 0]

@@ -292,6 +292,8 @@ def test_rccl_transport_rows_match_one_batch(k):
                                                        max_episode_steps=MAXEP, **kw),
                            total, steps_per_gather=k, transport="rccl")
     assert env.transport == "rccl" and env.overlap
+    info = env._rccl.info()                     # RCCL's own view (ncclCommCount / UserRank)
+    assert info["nranks"] == 1 and info["rank"] == 0 and info["gathers"] == 0
     acts = _actions(total)
     got = []
     rows, ready = env.reset()
@@ -307,6 +309,7 @@ def test_rccl_transport_rows_match_one_batch(k):
     if rows is not None:
         ready.wait()
         got += _rows_list(rows, total)
+    assert env._rccl.info()["gathers"] == 1 + -(-T // k)     # the reset's + one per block
     env.close()
     b = core.DeviceBatch(config.merge_config(num_ac=32, max_episode_steps=MAXEP), total,
                          compute_cd=True, seed=SEED, learner=True)
@@ -318,3 +321,37 @@ def test_rccl_transport_rows_match_one_batch(k):
     got, want = np.stack(got), np.stack(want)
     assert got.shape == want.shape
     assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
+
+
+def test_rccl_graph_cache_serves_the_ring(monkeypatch):
+    """BSG_COMM_GRAPHS=1 (the gather as a replayed HIP graph): the cache holds one graph per
+    slot of the fused per-step path's ring, so after one lap every gather is a replay
+    (an 8-entry FIFO missed on every one of the 16 slots).  Rows bit-identical to
+    the plain ncclAllGather path."""
+    from bluesky_gym.parallel import ShardedVectorEnv
+    from bluesky_gym.vector import MergeVectorEnv
+    from bluesky_gym import _native as nat
+    total = E_LOCAL
+    acts = _actions(total)
+    out = {}
+    for graphs in ("0", "1"):
+        monkeypatch.setenv("BSG_COMM_GRAPHS", graphs)
+        env = ShardedVectorEnv(lambda **kw: MergeVectorEnv(num_ac=32, seed=SEED, compute_cd=True,
+                                                           max_episode_steps=MAXEP, **kw),
+                               total, steps_per_gather=1, transport="rccl")
+        assert env._fused
+        env.reset()[1].wait()
+        got = []
+        for t in range(T):
+            rows, ready = env.step(acts[t].cuda())
+            ready.wait()
+            got.append(rows.cpu().numpy().copy())
+        info = env._rccl.info()
+        env.close()
+        out[graphs] = (np.stack(got), info)
+    info = out["1"][1]
+    assert info["use_graphs"] == 1 and info["gathers"] == T + 1
+    # the reset's gather (slot 0, a [1, n, d] block) and one capture per slot of the ring
+    assert info["graph_captures"] <= nat.COMM_SLOTS + 1
+    assert info["graph_hits"] == info["gathers"] - info["graph_captures"] and info["graph_hits"] > 0
+    assert np.array_equal(out["0"][0].view(np.uint32), out["1"][0].view(np.uint32))
