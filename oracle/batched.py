@@ -242,6 +242,12 @@ class _Base:
             if "cd" in res:
                 # a NEXT_STEP reset step reports conflict detection on the fresh state
                 self._cd_into(res, was_reset)
+            # ... and the reset observation's top-K (merge_env.py:124 -> _get_obs's argsort,
+            # :196); no intrusion check runs at a reset (merge_env.py:103-130), so its mask is 0
+            if "topk" in ro and "topk" in res:
+                res["topk"] = np.where(was_reset[:, None], ro["topk"], res["topk"])
+            if "intr_mask" in res:
+                res["intr_mask"] = np.where(was_reset, np.uint64(0), res["intr_mask"]).astype(np.uint64)
         if self.autoreset == AUTORESET_NEXT_STEP:
             self.needs_reset = done.copy()
         elif self.autoreset == AUTORESET_SAME_STEP and done.any():
@@ -371,8 +377,8 @@ class MergeOracle(_Base):
         return obs, drift, wpt_dist, dist, top + 1
 
     def observe(self):
-        obs, *_ = self._obs_core()
-        return {"obs": self._flat(obs, MERGE_OBS_KEYS), "obs_dict": obs}
+        obs, _drift, _wd, _dist, topk = self._obs_core()
+        return {"obs": self._flat(obs, MERGE_OBS_KEYS), "obs_dict": obs, "topk": topk}
 
     def _observe_and_reward(self):
         obs, drift, wpt_dist, dist, topk = self._obs_core()

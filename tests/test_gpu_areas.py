@@ -92,8 +92,8 @@ def _cmp(b, r, t, cd):
     assert np.array_equal(b.terminated.cpu().numpy().astype(bool), r["terminated"]), t
     assert np.array_equal(b.truncated.cpu().numpy().astype(bool), r["truncated"]), t
     if cd:
-        live = ~r["was_reset"]
-        assert np.array_equal(b.intr_mask.cpu().numpy().astype(np.uint64)[live], r["intr_mask"][live]), t
+        # reset steps included (no intrusion check at a reset: mask 0)
+        assert np.array_equal(b.intr_mask.cpu().numpy().astype(np.uint64), r["intr_mask"]), t
         assert np.array_equal(b.conf_mask.cpu().numpy().astype(np.uint64), r["conf_mask"]), t
         assert np.array_equal(b.los_mask.cpu().numpy().astype(np.uint64), r["los_mask"]), t
         close(b.tcpamax.cpu().numpy(), r["tcpamax"], f"tcpamax t={t}", atol=TCPA_ATOL)
