@@ -58,7 +58,11 @@ LOG_KEYS = {
 _DESCENT_SAC_ALT = ("the one statistic the withdrawn VSMAX fit matched: a vsmax cap of ~12.1 m/s "
                     "on the terminal dive brings it in, and puts Descent DDPG's final altitude at "
                     "z = +15 (held-out evidence against the cap); no single vsmax serves both "
-                    "actors' dives (DESIGN.md §5)")
+                    "actors' dives.  The saved Descent / Vertical SAC transitions reproduce the "
+                    "slew, the integration and CAS->TAS exactly at 860-3,270 m "
+                    "(tests/test_last_obs.py), so what is left is the regime below 1,000 ft "
+                    "that no saved state reaches (the DDPG's last saved state dives at -12.5 "
+                    "m/s at 394 m) (DESIGN.md §5)")
 _STATIC = ("logs written by an older StaticObstacleEnv revision (no drift term); not moved by "
            "the A.3 speed envelope")
 _SECTOR = ("the logged runs did not fly this Sector state: the saved SAC transition "
