@@ -580,7 +580,10 @@ def c5_learner_leg(b, W, dev, steps, warm):
     import sac_torch
     torch.backends.cuda.preferred_blas_library("cublas")
     os.environ["DISABLE_ADDMM_CUDA_LT"] = "1"
-    sac = sac_torch.SAC(b.obs_dim, b.act_dim, dev, group=None, seed=0, lr=1e-3)
+    # FusedSAC: the update's forward / backward written out (tools/sac_fused.hip, ~30 launches
+    # per update instead of ~100); SAC_FUSED=0 = the autograd update
+    cls = sac_torch.FusedSAC if os.environ.get("SAC_FUSED", "1") == "1" else sac_torch.SAC
+    sac = cls(b.obs_dim, b.act_dim, dev, group=None, seed=0, lr=1e-3)
     sac.actor.load_sb3(W, "descent")
     rl = sac_torch.RLLoop(b, sac, learn=True, fused_policy=True)
     rl.obs.copy_(b.obs)
@@ -599,7 +602,8 @@ def c5_learner_leg(b, W, dev, steps, warm):
     return {"value": b.E / wall, "ms_per_step": wall * 1e3, "unit": "env_steps/s",
             "critic_loss": float(lq), "actor_loss": float(la),
             "learner": "SB3 SAC restated (tools/sac_torch.py): twin critics + actor 256-256, "
-                       "batch 256, one update per vector step, HIP graph"}
+                       "batch 256, one update per vector step, HIP graph",
+            "update": type(sac).__name__}
 
 
 def bench_descent_sac(args):
@@ -643,7 +647,10 @@ def bench_descent_sac(args):
                          seed=1234, env_offset=rank * E)
     b.reset()
     W = dict(np.load(os.path.join(REPO, "tests", "golden", "sac_actors.npz")))
-    sac = sac_torch.SAC(b.obs_dim, b.act_dim, dev, group=dist.group.WORLD if world > 1 else None,
+    # one rank: FusedSAC (tools/sac_fused.hip); across ranks the autograd update with its
+    # RCCL gradient all-reduce
+    cls = sac_torch.FusedSAC if (world == 1 and os.environ.get("SAC_FUSED", "1") == "1") else sac_torch.SAC
+    sac = cls(b.obs_dim, b.act_dim, dev, group=dist.group.WORLD if world > 1 else None,
                         seed=rank, lr=1e-3)
     sac.actor.load_sb3(W, "descent")
     gen = torch.Generator(device=dev)

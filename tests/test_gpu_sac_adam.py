@@ -203,3 +203,62 @@ def test_squashed_gaussian_matches_autograd():
         assert torch.allclose(m1.grad, m2.grad, rtol=1e-4, atol=1e-4), (m1.grad - m2.grad).abs().max().item()
         assert torch.allclose(l1.grad, l2.grad, rtol=1e-4, atol=1e-4), (l1.grad - l2.grad).abs().max().item()
         assert l1.grad[0, 0] == 0 and l1.grad[1, 0] == 0
+
+
+@pytest.mark.parametrize("obs_dim,act_dim", [(4, 1), (40, 2)])
+def test_fused_sac_update_matches_autograd_update(obs_dim, act_dim):
+    """FusedSAC (tools/sac_fused.hip: the forward / backward written out, rocBLAS for the
+    256 x 256 products) against SAC.update on the autograd + HipAdam path: same seed, same
+    buffer, same RNG draws; after 10 updates every parameter, target parameter and log_alpha
+    within 1e-4 relative + 1e-5 absolute (the column sums and the bias adds associate
+    differently from autograd's), and the losses of the last update close.  Descent's shape
+    (obs 4, action 1) and Merge's (obs 40, action 2)."""
+    dev = torch.device("cuda", 0)
+    out, losses = [], []
+    for cls in (sac_torch.SAC, sac_torch.FusedSAC):
+        s = cls(obs_dim, act_dim, dev, seed=7, lr=1e-3, buffer=4096)
+        assert s.hip_adam and s.actor.fused_dist
+        gen = torch.Generator(device=dev).manual_seed(11)
+        n = 1024
+        o = torch.randn((n, obs_dim), generator=gen, device=dev)
+        a = torch.rand((n, act_dim), generator=gen, device=dev) * 2 - 1
+        r = torch.randn((n,), generator=gen, device=dev)
+        o2 = torch.randn((n, obs_dim), generator=gen, device=dev)
+        d = (torch.rand((n,), generator=gen, device=dev) < 0.1).float()
+        s.insert(o, a, r, o2, d)
+        torch.manual_seed(5)
+        for _ in range(10):
+            lq, la = s.update()
+        torch.cuda.synchronize()
+        losses.append((float(lq), float(la)))
+        out.append([p.detach().clone() for p in
+                    list(s.actor.parameters()) + list(s.q.parameters()) + list(s.qt.parameters()) +
+                    [s.log_alpha]])
+    for x, y in zip(*out):
+        assert torch.allclose(x, y, rtol=1e-4, atol=1e-5), (x - y).abs().max().item()
+    (lq0, la0), (lq1, la1) = losses
+    assert abs(lq0 - lq1) <= 1e-4 * abs(lq0) + 1e-5 and abs(la0 - la1) <= 1e-4 * abs(la0) + 1e-5
+
+
+def test_fused_sac_loop_is_graph_capturable():
+    """The whole C5 iteration with FusedSAC (policy sample, env step, replay insert, update)
+    captured as one HIP graph and replayed: finite losses and parameters that move."""
+    import numpy as np
+    from bluesky_gym import _native as nat, config, core
+    dev = torch.device("cuda", 0)
+    b = core.DeviceBatch(config.descent_config(), 512, autoreset=nat.AUTORESET_SAME_STEP,
+                         compute_cd=False, seed=3)
+    b.reset()
+    s = sac_torch.FusedSAC(b.obs_dim, b.act_dim, dev, seed=0, lr=1e-3)
+    w0 = s.actor.latent[2].weight.detach().clone()
+    rl = sac_torch.RLLoop(b, s, learn=True, fused_policy=True)
+    rl.obs.copy_(b.obs)
+    for _ in range(4):
+        rl.step()
+    rl.capture()
+    for _ in range(10):
+        rl.replay()
+    torch.cuda.synchronize()
+    lq, la = s.update()
+    assert np.isfinite(float(lq)) and np.isfinite(float(la))
+    assert not torch.equal(w0, s.actor.latent[2].weight.detach())

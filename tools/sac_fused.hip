@@ -1,0 +1,500 @@
+// The C5 learner's SAC update with its elementwise work fused (tools/sac_torch.py FusedSAC).
+//
+// SB3's SAC update (scripts/descent_env_sac.py:25-34 -> SB3 2.x SAC.train, one gradient step)
+// at batch 256 through 256-wide MLPs is ~100 small kernels as torch autograd runs it
+// (bias copies, ReLU and its backward, bias-gradient reductions, the loss terms and the
+// squashed Gaussian as separate launches), each paying the ~1.5 us dependent-kernel boundary
+// (MI355X_MICROARCH.md 'boundary').  FusedSAC writes the forward and backward passes out and
+// keeps only the 256 x 256 products as rocBLAS GEMMs (torch.mm / bmm with out=); everything
+// between two GEMMs is one of the kernels below, so an update is ~30 launches:
+//
+//   in_layer     relu(x W + b) for a layer whose K is the observation (+ action) width
+//   actor_head   h1 = relu(p1 + b1), mu / log_std heads, SB3's squashed Gaussian (a, logp)
+//   critic_head  g1 = relu(p1 + b1), q = g1 w2 + b2 for both critics, then per mode the TD
+//                target y, the twin-MSE gradient dq, or the actor loss's dq / dlogp
+//   critic_bwd_head   dg1 = dq w2 (g1 > 0) and the w2 / b2 / b1 gradients (column sums)
+//   critic_bwd_in     the first layer's gradients from dg0 (g0 > 0)
+//   critic_dx         the actor loss's gradient w.r.t. the critics' action inputs
+//   actor_bwd_head    the squashed Gaussian's backward and dh1 = (dmu Wmu + dlsr Wls)(h1 > 0)
+//   actor_bwd_cols    the heads' and b1's gradients and d log_alpha (column sums)
+//   actor_bwd_in      the first layer's gradients from dh0 (h0 > 0)
+//   polyak            target = target (1 - tau) + tau param over every critic tensor
+//
+// Layouts: the actor's torch Linear weights ([out, in]); the twin critics stacked as
+// tools/sac_torch.py TwinQ keeps them (w0 [2, in, H], w1 [2, H, H], w2 [2, H, 1]).  H = 256.
+// Every column sum runs over the rows in order, one thread per column: deterministic.  fp32,
+// -ffp-contract=off; results agree with the autograd path to fp32 rounding (the association
+// of the sums differs), checked by tests/test_gpu_sac_adam.py.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+namespace {
+
+constexpr int H = 256;
+constexpr float LOG_SQRT_2PI = 0.91893853320467274f;
+
+__device__ __forceinline__ float wave_sum(float v) {
+  for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
+  return v;
+}
+
+// out[c][r][u] = relu(b[c][u] + sum_k x[r][k] w[c][k][u])   (w_ku: critic layout [c][k][u])
+// or             relu(b[u] + sum_k x[r][k] w[u][k])         (!w_ku: torch Linear [u][k], c = 0)
+// x[r] = [xa row (Ka) | xb row (Kb)]; rows r >= split read xa_hi instead of xa.
+__global__ __launch_bounds__(256) void in_layer_kernel(
+    const float* __restrict__ xa, const float* __restrict__ xa_hi, int split, int lda, int Ka,
+    const float* __restrict__ xb, int ldb, int Kb, int R, int nC, const float* __restrict__ w,
+    int w_ku, const float* __restrict__ b, float* __restrict__ out) {
+  const int u = threadIdx.x;
+  const int r = blockIdx.x;
+  const int c = blockIdx.y;
+  if (r >= R || c >= nC) return;
+  const float* xr = r < split ? xa + (size_t)r * lda : xa_hi + (size_t)(r - split) * lda;
+  const int K = Ka + Kb;
+  float acc = 0.0f;
+  for (int k = 0; k < K; ++k) {
+    const float xv = k < Ka ? xr[k] : xb[(size_t)r * ldb + (k - Ka)];
+    const float wv = w_ku ? w[((size_t)c * K + k) * H + u] : w[(size_t)u * K + k];
+    acc += xv * wv;
+  }
+  const float z = acc + b[(size_t)c * H + u];
+  out[((size_t)c * R + r) * H + u] = z > 0.0f ? z : 0.0f;
+}
+
+// one wave per row: h1 = relu(p1 + b1); mu = h1 Wmu^T + bmu; lsr = h1 Wls^T + bls;
+// SB3's squashed Gaussian (sac_adam.hip sq_gauss_fwd_kernel): a = tanh(mu + exp(clamp(lsr)) eps)
+__global__ __launch_bounds__(256) void actor_head_kernel(
+    const float* __restrict__ p1, const float* __restrict__ b1, const float* __restrict__ wmu,
+    const float* __restrict__ bmu, const float* __restrict__ wls, const float* __restrict__ bls,
+    const float* __restrict__ eps, int R, int A, float* __restrict__ h1, float* __restrict__ mu,
+    float* __restrict__ lsr, float* __restrict__ a_out, float* __restrict__ logp) {
+  const int lane = threadIdx.x & 63;
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= R) return;
+  float hv[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int u = lane + 64 * i;
+    const float z = p1[(size_t)r * H + u] + b1[u];
+    hv[i] = z > 0.0f ? z : 0.0f;
+    h1[(size_t)r * H + u] = hv[i];
+  }
+  float s1 = 0.0f, s2 = 0.0f;
+  for (int j = 0; j < A; ++j) {
+    float pm = 0.0f, pl = 0.0f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int u = lane + 64 * i;
+      pm += hv[i] * wmu[(size_t)j * H + u];
+      pl += hv[i] * wls[(size_t)j * H + u];
+    }
+    const float m = wave_sum(pm) + bmu[j];
+    const float lr_ = wave_sum(pl) + bls[j];
+    const int ij = r * A + j;
+    const float ls = fminf(fmaxf(lr_, -20.0f), 2.0f);
+    const float sd = expf(ls);
+    const float uu = m + sd * eps[ij];
+    const float a = tanhf(uu);
+    const float z = (uu - m) / sd;
+    s1 += -0.5f * (z * z) - ls - LOG_SQRT_2PI;
+    s2 += logf(1.0f - a * a + 1e-6f);
+    if (lane == 0) {
+      mu[ij] = m;
+      lsr[ij] = lr_;
+      a_out[ij] = a;
+    }
+  }
+  if (lane == 0) logp[r] = s1 - s2;
+}
+
+enum { HEAD_TARGET = 0, HEAD_CRITIC = 1, HEAD_ACTOR_LOSS = 2 };
+
+// one wave per row, both critics: g1 = relu(p1 + b1) (stored unless TARGET), q = g1 w2 + b2.
+//  TARGET:     y[r] = rew + gamma (1 - done) (min_c q - alpha logp2[r])      (sac_td_target)
+//  CRITIC:     dq[c][r] = (1 / B) (2 (q - y[r])); lossp[r] = sum_c (q - y)^2 / B
+//  ACTOR_LOSS: dlogp[r] = alpha / B; dq on the smaller critic -1 / B (split on a tie);
+//              lossp[r] = (alpha logp[r] - min_c q) / B                          (sac_actor_loss)
+__global__ __launch_bounds__(256) void critic_head_kernel(
+    const float* __restrict__ p1, const float* __restrict__ b1, const float* __restrict__ w2,
+    const float* __restrict__ b2, int B, int mode, const float* __restrict__ rows, int W,
+    int col_r, int col_d, float gamma, const float* __restrict__ log_alpha,
+    const float* __restrict__ logp, float* __restrict__ y, float* __restrict__ g1,
+    float* __restrict__ q_out, float* __restrict__ dq, float* __restrict__ dlogp,
+    float* __restrict__ lossp) {
+  const int lane = threadIdx.x & 63;
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= B) return;
+  float q[2];
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    float part = 0.0f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int u = lane + 64 * i;
+      const size_t o = ((size_t)c * B + r) * H + u;
+      const float z = p1[o] + b1[(size_t)c * H + u];
+      const float g = z > 0.0f ? z : 0.0f;
+      if (mode != HEAD_TARGET) g1[o] = g;
+      part += g * w2[(size_t)c * H + u];
+    }
+    q[c] = wave_sum(part) + b2[c];
+  }
+  if (lane != 0) return;
+  const float alpha = expf(log_alpha[0]);
+  q_out[r] = q[0];
+  q_out[B + r] = q[1];
+  const float invB = 1.0f / (float)B;
+  if (mode == HEAD_TARGET) {
+    const float mn = fminf(q[0], q[1]);
+    const float qt = mn - alpha * logp[r];
+    const float d = rows[(size_t)r * W + col_d];
+    const float rw = rows[(size_t)r * W + col_r];
+    y[r] = rw + (gamma * (1.0f - d)) * qt;
+  } else if (mode == HEAD_CRITIC) {
+    float l = 0.0f;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const float df = q[c] - y[r];
+      dq[(size_t)c * B + r] = invB * (2.0f * df);
+      l += df * df / (float)B;
+    }
+    lossp[r] = l;
+  } else {
+    const float gb = invB;
+    dlogp[r] = gb * alpha;
+    const float mn = fminf(q[0], q[1]);
+    const float ng = -gb;
+    if (q[0] == q[1]) {
+      dq[r] = ng / 2.0f;
+      dq[B + r] = ng / 2.0f;
+    } else {
+      dq[r] = q[0] == mn ? ng : 0.0f;
+      dq[B + r] = q[1] == mn ? ng : 0.0f;
+    }
+    lossp[r] = (alpha * logp[r] - mn) / (float)B;
+  }
+}
+
+// one thread per (c, u): dg1[c][r][u] = dq[c][r] w2[c][u] (g1 > 0) for every row; with grads,
+// dw2[c][u] = sum_r g1 dq, db1[c][u] = sum_r dg1, db2[c] = sum_r dq (thread u = 0)
+__global__ __launch_bounds__(256) void critic_bwd_head_kernel(
+    const float* __restrict__ dq, const float* __restrict__ g1, const float* __restrict__ w2, int B,
+    int grads, float* __restrict__ dg1, float* __restrict__ dw2, float* __restrict__ db1,
+    float* __restrict__ db2) {
+  const int u = threadIdx.x;
+  const int c = blockIdx.x;
+  const float wv = w2[(size_t)c * H + u];
+  float sw = 0.0f, sb = 0.0f, sq = 0.0f;
+  for (int r = 0; r < B; ++r) {
+    const size_t o = ((size_t)c * B + r) * H + u;
+    const float d = dq[(size_t)c * B + r];
+    const float g = g1[o];
+    const float v = g > 0.0f ? d * wv : 0.0f;
+    dg1[o] = v;
+    sw += g * d;
+    sb += v;
+    sq += d;
+  }
+  if (grads) {
+    dw2[(size_t)c * H + u] = sw;
+    db1[(size_t)c * H + u] = sb;
+    if (u == 0) db2[c] = sq;
+  }
+}
+
+// one thread per (c, u): m = dg0 (g0 > 0); dw0[c][k][u] = sum_r x[r][k] m, db0[c][u] = sum_r m;
+// x[r] = [xa row (Ka) | xb row (Kb)]
+__global__ __launch_bounds__(256) void critic_bwd_in_kernel(
+    const float* __restrict__ dg0, const float* __restrict__ g0, const float* __restrict__ xa,
+    int lda, int Ka, const float* __restrict__ xb, int ldb, int Kb, int B,
+    float* __restrict__ dw0, float* __restrict__ db0) {
+  const int u = threadIdx.x;
+  const int c = blockIdx.x;
+  const int K = Ka + Kb;
+  float sb = 0.0f;
+  for (int k0 = 0; k0 < K; k0 += 8) {
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int r = 0; r < B; ++r) {
+      const size_t o = ((size_t)c * B + r) * H + u;
+      const float m = g0[o] > 0.0f ? dg0[o] : 0.0f;
+      if (k0 == 0) sb += m;
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        const int k = k0 + t;
+        if (k < K) {
+          const float xv = k < Ka ? xa[(size_t)r * lda + k] : xb[(size_t)r * ldb + (k - Ka)];
+          acc[t] += xv * m;
+        }
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < 8; ++t)
+      if (k0 + t < K) dw0[((size_t)c * K + k0 + t) * H + u] = acc[t];
+  }
+  db0[(size_t)c * H + u] = sb;
+}
+
+// one wave per row: dx[r][j] = sum_c sum_u w0[c][Ka + j][u] (dg0 (g0 > 0))[c][r][u], the
+// gradient w.r.t. the critics' action inputs (columns Ka.. of their input)
+__global__ __launch_bounds__(256) void critic_dx_kernel(
+    const float* __restrict__ dg0, const float* __restrict__ g0, const float* __restrict__ w0,
+    int K, int Ka, int A, int B, float* __restrict__ dx) {
+  const int lane = threadIdx.x & 63;
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= B) return;
+  for (int j = 0; j < A; ++j) {
+    float part = 0.0f;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int u = lane + 64 * i;
+        const size_t o = ((size_t)c * B + r) * H + u;
+        const float m = g0[o] > 0.0f ? dg0[o] : 0.0f;
+        part += w0[((size_t)c * K + Ka + j) * H + u] * m;
+      }
+    }
+    const float s = wave_sum(part);
+    if (lane == 0) dx[(size_t)r * A + j] = s;
+  }
+}
+
+// one wave per row: the squashed Gaussian's backward (sac_adam.hip sq_gauss_bwd_kernel) from
+// (ga = dx, gl = dlogp), then dh1[r][u] = (sum_j dmu Wmu[j][u] + dlsr Wls[j][u]) (h1 > 0)
+__global__ __launch_bounds__(256) void actor_bwd_head_kernel(
+    const float* __restrict__ ga, const float* __restrict__ gl, const float* __restrict__ mu,
+    const float* __restrict__ lsr, const float* __restrict__ eps, const float* __restrict__ a_out,
+    const float* __restrict__ h1, const float* __restrict__ wmu, const float* __restrict__ wls,
+    int R, int A, float* __restrict__ dmu, float* __restrict__ dlsr, float* __restrict__ dh1) {
+  const int lane = threadIdx.x & 63;
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= R) return;
+  float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+  const float g = gl[r];
+  for (int j = 0; j < A; ++j) {
+    const int i = r * A + j;
+    const float x = lsr[i];
+    const float ls = fminf(fmaxf(x, -20.0f), 2.0f);
+    const float sd = expf(ls);
+    const float u = mu[i] + sd * eps[i];
+    const float z = (u - mu[i]) / sd;
+    const float a = a_out[i];
+    const float da = 1.0f - a * a;
+    const float gu = ga[i] * da + g * (-z / sd + (2.0f * a / (da + 1e-6f)) * da);
+    const float gm = gu + g * z / sd;
+    const float gsd = gu * eps[i] + g * (z * z) / sd;
+    const float gls = (x >= -20.0f && x <= 2.0f) ? gsd * sd - g : 0.0f;
+    if (lane == 0) {
+      dmu[i] = gm;
+      dlsr[i] = gls;
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int uu = lane + 64 * t;
+      acc[t] += gm * wmu[(size_t)j * H + uu] + gls * wls[(size_t)j * H + uu];
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int uu = lane + 64 * t;
+    dh1[(size_t)r * H + uu] = h1[(size_t)r * H + uu] > 0.0f ? acc[t] : 0.0f;
+  }
+}
+
+// one thread per u: dWmu[j][u] = sum_r dmu[r][j] h1[r][u], dWls likewise, db1[u] = sum_r dh1;
+// thread j < A: dbmu[j], dbls[j]; thread A: d log_alpha = -mean_r(logp + target_entropy)
+// (SB3's ent_coef_loss = -(log_alpha * (logp + target_entropy).detach()).mean())
+__global__ __launch_bounds__(256) void actor_bwd_cols_kernel(
+    const float* __restrict__ dmu, const float* __restrict__ dlsr, const float* __restrict__ h1,
+    const float* __restrict__ dh1, const float* __restrict__ logp, float target_entropy, int R,
+    int A, float* __restrict__ dwmu, float* __restrict__ dwls, float* __restrict__ db1,
+    float* __restrict__ dbmu, float* __restrict__ dbls, float* __restrict__ dlog_alpha) {
+  const int u = threadIdx.x;
+  float sm[4] = {0, 0, 0, 0}, sl[4] = {0, 0, 0, 0};
+  float sb = 0.0f;
+  for (int r = 0; r < R; ++r) {
+    const float h = h1[(size_t)r * H + u];
+    sb += dh1[(size_t)r * H + u];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (j < A) {
+        sm[j] += dmu[(size_t)r * A + j] * h;
+        sl[j] += dlsr[(size_t)r * A + j] * h;
+      }
+    }
+  }
+  db1[u] = sb;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    if (j < A) {
+      dwmu[(size_t)j * H + u] = sm[j];
+      dwls[(size_t)j * H + u] = sl[j];
+    }
+  }
+  if (u < A) {
+    float bm = 0.0f, bl = 0.0f;
+    for (int r = 0; r < R; ++r) {
+      bm += dmu[(size_t)r * A + u];
+      bl += dlsr[(size_t)r * A + u];
+    }
+    dbmu[u] = bm;
+    dbls[u] = bl;
+  }
+  if (u == A) {
+    float s = 0.0f;
+    for (int r = 0; r < R; ++r) s += logp[r] + target_entropy;
+    dlog_alpha[0] = -(s / (float)R);
+  }
+}
+
+// one thread per u: m = dh0 (h0 > 0); dW0[u][k] = sum_r m x[r][k] (torch layout), db0[u]
+__global__ __launch_bounds__(256) void actor_bwd_in_kernel(
+    const float* __restrict__ dh0, const float* __restrict__ h0, const float* __restrict__ x,
+    int ldx, int K, int R, float* __restrict__ dw0, float* __restrict__ db0) {
+  const int u = threadIdx.x;
+  float sb = 0.0f;
+  for (int k0 = 0; k0 < K; k0 += 8) {
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int r = 0; r < R; ++r) {
+      const float m = h0[(size_t)r * H + u] > 0.0f ? dh0[(size_t)r * H + u] : 0.0f;
+      if (k0 == 0) sb += m;
+#pragma unroll
+      for (int t = 0; t < 8; ++t)
+        if (k0 + t < K) acc[t] += m * x[(size_t)r * ldx + k0 + t];
+    }
+#pragma unroll
+    for (int t = 0; t < 8; ++t)
+      if (k0 + t < K) dw0[(size_t)u * K + k0 + t] = acc[t];
+  }
+  db0[u] = sb;
+}
+
+// target = target * (1 - tau) + tau * src over up to 8 tensors (SB3 polyak_update's
+// mul_ then add_(alpha = tau))
+struct PolyakTable {
+  int32_t n;
+  int32_t start[9];
+  int64_t numel[8];
+  float* tgt[8];
+  const float* src[8];
+};
+
+__global__ __launch_bounds__(256) void polyak_kernel(PolyakTable T, float tau) {
+  const int blk = blockIdx.x;
+  int i = 0;
+  while (i + 1 < T.n && blk >= T.start[i + 1]) ++i;
+  const int64_t k = (int64_t)(blk - T.start[i]) * 256 + threadIdx.x;
+  if (k >= T.numel[i]) return;
+  const float t = T.tgt[i][k] * (1.0f - tau);
+  T.tgt[i][k] = t + tau * T.src[i][k];
+}
+
+}  // namespace
+
+#define SF_LAUNCH(kern, grid, block, ...)                                                    \
+  do {                                                                                       \
+    hipLaunchKernelGGL(kern, grid, block, 0, (hipStream_t)stream, __VA_ARGS__);              \
+    return hipGetLastError() == hipSuccess ? 0 : -2;                                         \
+  } while (0)
+
+extern "C" {
+
+int32_t sf_in_layer(const float* xa, const float* xa_hi, int32_t split, int32_t lda, int32_t Ka,
+                    const float* xb, int32_t ldb, int32_t Kb, int32_t R, int32_t nC, const float* w,
+                    int32_t w_ku, const float* b, float* out, void* stream) {
+  if (!xa || !w || !b || !out || R < 1 || nC < 1 || nC > 2 || Ka < 1 || Kb < 0 || (Kb && !xb) ||
+      (!w_ku && nC != 1))
+    return -1;
+  if (!xa_hi) { xa_hi = xa; split = R; }
+  SF_LAUNCH(in_layer_kernel, dim3(R, nC), dim3(H), xa, xa_hi, split, lda, Ka, xb, ldb, Kb, R, nC, w,
+            w_ku, b, out);
+}
+
+int32_t sf_actor_head(const float* p1, const float* b1, const float* wmu, const float* bmu,
+                      const float* wls, const float* bls, const float* eps, int32_t R, int32_t A,
+                      float* h1, float* mu, float* lsr, float* a_out, float* logp, void* stream) {
+  if (!p1 || !b1 || !wmu || !bmu || !wls || !bls || !eps || !h1 || !mu || !lsr || !a_out || !logp ||
+      R < 1 || A < 1 || A > 4)
+    return -1;
+  SF_LAUNCH(actor_head_kernel, dim3((R + 3) / 4), dim3(256), p1, b1, wmu, bmu, wls, bls, eps, R, A,
+            h1, mu, lsr, a_out, logp);
+}
+
+int32_t sf_critic_head(const float* p1, const float* b1, const float* w2, const float* b2, int32_t B,
+                       int32_t mode, const float* rows, int32_t W, int32_t col_r, int32_t col_d,
+                       float gamma, const float* log_alpha, const float* logp, float* y, float* g1,
+                       float* q_out, float* dq, float* dlogp, float* lossp, void* stream) {
+  if (!p1 || !b1 || !w2 || !b2 || !log_alpha || !q_out || B < 1 || mode < 0 || mode > 2) return -1;
+  if (mode == HEAD_TARGET && (!rows || !logp || !y || col_r < 0 || col_r >= W || col_d < 0 || col_d >= W))
+    return -1;
+  if (mode == HEAD_CRITIC && (!y || !g1 || !dq || !lossp)) return -1;
+  if (mode == HEAD_ACTOR_LOSS && (!logp || !g1 || !dq || !dlogp || !lossp)) return -1;
+  SF_LAUNCH(critic_head_kernel, dim3((B + 3) / 4), dim3(256), p1, b1, w2, b2, B, mode, rows, W, col_r,
+            col_d, gamma, log_alpha, logp, y, g1, q_out, dq, dlogp, lossp);
+}
+
+int32_t sf_critic_bwd_head(const float* dq, const float* g1, const float* w2, int32_t B, int32_t grads,
+                           float* dg1, float* dw2, float* db1, float* db2, void* stream) {
+  if (!dq || !g1 || !w2 || !dg1 || B < 1 || (grads && (!dw2 || !db1 || !db2))) return -1;
+  SF_LAUNCH(critic_bwd_head_kernel, dim3(2), dim3(H), dq, g1, w2, B, grads, dg1, dw2, db1, db2);
+}
+
+int32_t sf_critic_bwd_in(const float* dg0, const float* g0, const float* xa, int32_t lda, int32_t Ka,
+                         const float* xb, int32_t ldb, int32_t Kb, int32_t B, float* dw0, float* db0,
+                         void* stream) {
+  if (!dg0 || !g0 || !xa || !dw0 || !db0 || B < 1 || Ka < 1 || Kb < 0 || (Kb && !xb)) return -1;
+  SF_LAUNCH(critic_bwd_in_kernel, dim3(2), dim3(H), dg0, g0, xa, lda, Ka, xb, ldb, Kb, B, dw0, db0);
+}
+
+int32_t sf_critic_dx(const float* dg0, const float* g0, const float* w0, int32_t K, int32_t Ka,
+                     int32_t A, int32_t B, float* dx, void* stream) {
+  if (!dg0 || !g0 || !w0 || !dx || B < 1 || A < 1 || Ka < 0 || Ka + A > K) return -1;
+  SF_LAUNCH(critic_dx_kernel, dim3((B + 3) / 4), dim3(256), dg0, g0, w0, K, Ka, A, B, dx);
+}
+
+int32_t sf_actor_bwd_head(const float* ga, const float* gl, const float* mu, const float* lsr,
+                          const float* eps, const float* a_out, const float* h1, const float* wmu,
+                          const float* wls, int32_t R, int32_t A, float* dmu, float* dlsr, float* dh1,
+                          void* stream) {
+  if (!ga || !gl || !mu || !lsr || !eps || !a_out || !h1 || !wmu || !wls || !dmu || !dlsr || !dh1 ||
+      R < 1 || A < 1 || A > 4)
+    return -1;
+  SF_LAUNCH(actor_bwd_head_kernel, dim3((R + 3) / 4), dim3(256), ga, gl, mu, lsr, eps, a_out, h1, wmu,
+            wls, R, A, dmu, dlsr, dh1);
+}
+
+int32_t sf_actor_bwd_cols(const float* dmu, const float* dlsr, const float* h1, const float* dh1,
+                          const float* logp, float target_entropy, int32_t R, int32_t A, float* dwmu,
+                          float* dwls, float* db1, float* dbmu, float* dbls, float* dlog_alpha,
+                          void* stream) {
+  if (!dmu || !dlsr || !h1 || !dh1 || !logp || !dwmu || !dwls || !db1 || !dbmu || !dbls || !dlog_alpha ||
+      R < 1 || A < 1 || A > 4)
+    return -1;
+  SF_LAUNCH(actor_bwd_cols_kernel, dim3(1), dim3(H), dmu, dlsr, h1, dh1, logp, target_entropy, R, A,
+            dwmu, dwls, db1, dbmu, dbls, dlog_alpha);
+}
+
+int32_t sf_actor_bwd_in(const float* dh0, const float* h0, const float* x, int32_t ldx, int32_t K,
+                        int32_t R, float* dw0, float* db0, void* stream) {
+  if (!dh0 || !h0 || !x || !dw0 || !db0 || R < 1 || K < 1) return -1;
+  SF_LAUNCH(actor_bwd_in_kernel, dim3(1), dim3(H), dh0, h0, x, ldx, K, R, dw0, db0);
+}
+
+int32_t sf_polyak(int32_t n, float* const* tgt, const float* const* src, const int64_t* numel, float tau,
+                  void* stream) {
+  if (n < 1 || n > 8 || !tgt || !src || !numel) return -1;
+  PolyakTable T{};
+  T.n = n;
+  T.start[0] = 0;
+  for (int i = 0; i < n; ++i) {
+    if (!tgt[i] || !src[i] || numel[i] <= 0) return -1;
+    T.numel[i] = numel[i];
+    T.tgt[i] = tgt[i];
+    T.src[i] = src[i];
+    T.start[i + 1] = T.start[i] + (int32_t)((numel[i] + 255) / 256);
+  }
+  SF_LAUNCH(polyak_kernel, dim3(T.start[n]), dim3(256), T, tau);
+}
+
+}  // extern "C"

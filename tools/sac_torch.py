@@ -435,7 +435,8 @@ class SAC:
             g.copy_(flat[off:off + n].view_as(g))
             off += n
 
-    def update(self):
+    def update(self, losses=True):
+        """One SAC gradient step; returns (critic loss, actor loss) as device scalars."""
         o, a, r, o2, d = self.sample()
         alpha = self.log_alpha.exp().detach()
         # the actor's two evaluations of the update (next obs for the target, obs for the
@@ -496,6 +497,152 @@ class SAC:
         return lq.detach(), la.detach()
 
 
+FUSED_LIB = os.path.join(_HERE, "_lib", "libsacfused.so")
+
+
+class FusedSAC(SAC):
+    """SAC.update with its forward and backward passes written out (one rank, the HIP path):
+    the 256 x 256 products stay rocBLAS GEMMs (torch.mm / bmm into preallocated outputs) and
+    everything between two GEMMs is one launch of tools/sac_fused.hip -- ~30 launches per
+    update instead of autograd's ~100, each of which paid the dependent-kernel boundary.
+    Same parameters, replay buffer, HipAdam optimizers, step count and RNG draws (torch.rand
+    for the sample, torch.randn for the squashed Gaussian, in SAC.update's order), so an
+    update equals SAC.update's to fp32 rounding (tests/test_gpu_sac_adam.py).  Parameter
+    gradients live in persistent .grad buffers the kernels overwrite; every buffer is
+    preallocated, so the update is graph-capturable."""
+
+    _lib = None
+
+    def __init__(self, obs_dim, act_dim, device, **kw):
+        super().__init__(obs_dim, act_dim, device, **kw)
+        if not self.hip_adam or self.world != 1 or self.dev.type != "cuda":
+            raise ValueError("FusedSAC: one rank, the HIP Adam path (SAC_ADAM=hip)")
+        if FusedSAC._lib is None:
+            if not os.path.exists(FUSED_LIB):
+                raise RuntimeError(f"{FUSED_LIB} missing: run __graft_entry__.build()")
+            lib = ctypes.CDLL(FUSED_LIB)
+            for name in ("sf_in_layer", "sf_actor_head", "sf_critic_head", "sf_critic_bwd_head",
+                         "sf_critic_bwd_in", "sf_critic_dx", "sf_actor_bwd_head", "sf_actor_bwd_cols",
+                         "sf_actor_bwd_in", "sf_polyak"):
+                getattr(lib, name).restype = ctypes.c_int32
+            FusedSAC._lib = lib
+        HipAdam([torch.zeros(1, device=self.dev)], 0.0)         # loads sac_adam.hip's library
+        d, B, od, A = self.dev, self.batch, self.od, self.ad
+        H = 256
+        z = lambda *shape: torch.zeros(shape, dtype=torch.float32, device=d)  # noqa: E731
+        self._u = z(B)
+        self._rows = z(B, self.buf.shape[1])
+        self._eps = z(2 * B, A)
+        self._h0, self._p1a, self._h1 = z(2 * B, H), z(2 * B, H), z(2 * B, H)
+        self._mu, self._lsr, self._act, self._logp = z(2 * B, A), z(2 * B, A), z(2 * B, A), z(2 * B)
+        self._g0, self._p1c, self._g1 = z(2, B, H), z(2, B, H), z(2, B, H)
+        self._q, self._y, self._dq = z(2, B), z(B), z(2, B)
+        self._dlogp, self._lossq, self._lossa = z(B), z(B), z(B)
+        self._dg1, self._dg0, self._dx = z(2, B, H), z(2, B, H), z(B, A)
+        self._dh1, self._dh0, self._dmu, self._dlsr = z(B, H), z(B, H), z(B, A), z(B, A)
+        for p in list(self.actor.parameters()) + list(self.q.parameters()) + [self.log_alpha]:
+            p.grad = torch.zeros_like(p)
+        self._tgt = list(self.qt.parameters())
+        self._src = list(self.q.parameters())
+
+    def _call(self, name, *args):
+        c = []
+        for x in args:
+            if isinstance(x, torch.Tensor):
+                c.append(ctypes.c_void_p(x.data_ptr()))
+            elif x is None:
+                c.append(ctypes.c_void_p(None))
+            elif isinstance(x, float):
+                c.append(ctypes.c_float(x))
+            else:
+                c.append(ctypes.c_int32(int(x)))
+        c.append(ctypes.c_void_p(torch.cuda.current_stream(self.dev).cuda_stream))
+        rc = getattr(self._lib, name)(*c)
+        if rc != 0:
+            raise RuntimeError(f"{name} failed ({rc})")
+
+    def update(self, losses=True):
+        """SAC.update's gradient step (same order of evaluation and RNG draws)."""
+        with torch.no_grad():
+            return self._update(losses)
+
+    def _update(self, losses):
+        B, od, A = self.batch, self.od, self.ad
+        H = 256
+        W = self.buf.shape[1]
+        ic = od + A
+        rows = self._rows
+        L = HipAdam._lib
+        torch.rand(B, device=self.dev, out=self._u)
+        rc = L.sac_replay_sample(ctypes.c_void_p(self.buf.data_ptr()), self.cap, W,
+                                 ctypes.c_void_p(self._u.data_ptr()), B,
+                                 ctypes.c_void_p(self.size.data_ptr()), ctypes.c_void_p(rows.data_ptr()),
+                                 ctypes.c_void_p(torch.cuda.current_stream(self.dev).cuda_stream))
+        if rc != 0:
+            raise RuntimeError(f"sac_replay_sample failed ({rc})")
+        torch.randn((2 * B, A), device=self.dev, out=self._eps)
+        f = self._call
+        o = rows                                    # columns 0..od of the row
+        a = rows[:, od:]                            # the stored action (ld = W)
+        o2 = rows[:, od + A + 1:]                   # next obs
+        act, logp = self._act, self._logp
+        la_, lat = self.actor.latent, self.actor
+        # ---- actor on [o2; o] (one pass: its parameters do not change before its step) ----
+        f("sf_in_layer", o2, o, B, W, od, None, 0, 0, 2 * B, 1, la_[0].weight, 0, la_[0].bias, self._h0)
+        torch.mm(self._h0, la_[2].weight.t(), out=self._p1a)
+        f("sf_actor_head", self._p1a, la_[2].bias, lat.mu.weight, lat.mu.bias, lat.log_std.weight,
+          lat.log_std.bias, self._eps, 2 * B, A, self._h1, self._mu, self._lsr, act, logp)
+        q, qt = self.q, self.qt
+        # ---- TD target from the target critics on [o2, a2] ----
+        f("sf_in_layer", o2, None, B, W, od, act, A, A, B, 2, qt.w0, 1, qt.b0, self._g0)
+        torch.bmm(self._g0, qt.w1, out=self._p1c)
+        f("sf_critic_head", self._p1c, qt.b1, qt.w2, qt.b2, B, 0, rows, W, od + A, W - 1, self.gamma,
+          self.log_alpha, logp, self._y, None, self._q, None, None, None)
+        # ---- critics on [o, a]: twin MSE, its gradient, the critic step -------------------------
+        f("sf_in_layer", o, None, B, W, od, a, W, A, B, 2, q.w0, 1, q.b0, self._g0)
+        torch.bmm(self._g0, q.w1, out=self._p1c)
+        f("sf_critic_head", self._p1c, q.b1, q.w2, q.b2, B, 1, None, W, 0, 0, self.gamma,
+          self.log_alpha, None, self._y, self._g1, self._q, self._dq, None, self._lossq)
+        f("sf_critic_bwd_head", self._dq, self._g1, q.w2, B, 1, self._dg1, q.w2.grad, q.b1.grad, q.b2.grad)
+        torch.bmm(self._g0.transpose(1, 2), self._dg1, out=q.w1.grad)
+        torch.bmm(self._dg1, q.w1.transpose(1, 2), out=self._dg0)
+        f("sf_critic_bwd_in", self._dg0, self._g0, o, W, od, a, W, A, B, q.w0.grad, q.b0.grad)
+        self.opt_q.tick()                            # shared step count: every group steps once
+        self.opt_q.step()
+        # ---- actor loss through the updated critics on [o, ap] (critics frozen) ----------------
+        ap, lp = act[B:], logp[B:]
+        f("sf_in_layer", o, None, B, W, od, ap, A, A, B, 2, q.w0, 1, q.b0, self._g0)
+        torch.bmm(self._g0, q.w1, out=self._p1c)
+        f("sf_critic_head", self._p1c, q.b1, q.w2, q.b2, B, 2, None, W, 0, 0, self.gamma,
+          self.log_alpha, lp, None, self._g1, self._q, self._dq, self._dlogp, self._lossa)
+        f("sf_critic_bwd_head", self._dq, self._g1, q.w2, B, 0, self._dg1, None, None, None)
+        torch.bmm(self._dg1, q.w1.transpose(1, 2), out=self._dg0)
+        f("sf_critic_dx", self._dg0, self._g0, q.w0, ic, od, A, B, self._dx)
+        # ---- actor backward (the o half of the pass), entropy coefficient, their step --------
+        h0b, h1b = self._h0[B:], self._h1[B:]
+        f("sf_actor_bwd_head", self._dx, self._dlogp, self._mu[B:], self._lsr[B:], self._eps[B:], ap,
+          h1b, lat.mu.weight, lat.log_std.weight, B, A, self._dmu, self._dlsr, self._dh1)
+        f("sf_actor_bwd_cols", self._dmu, self._dlsr, h1b, self._dh1, lp, float(self.target_entropy), B, A,
+          lat.mu.weight.grad, lat.log_std.weight.grad, la_[2].bias.grad, lat.mu.bias.grad,
+          lat.log_std.bias.grad, self.log_alpha.grad)
+        torch.mm(self._dh1.t(), h0b, out=la_[2].weight.grad)
+        torch.mm(self._dh1, la_[2].weight, out=self._dh0)
+        f("sf_actor_bwd_in", self._dh0, h0b, o, W, od, B, la_[0].weight.grad, la_[0].bias.grad)
+        self.opt_a.step()                            # actor + log_alpha in one launch
+        # ---- SB3 polyak_update of the target critics ---------------------------------------
+        n = len(self._tgt)
+        T = (ctypes.c_void_p * n)(*[t.data_ptr() for t in self._tgt])
+        S = (ctypes.c_void_p * n)(*[t.data_ptr() for t in self._src])
+        N = (ctypes.c_int64 * n)(*[t.numel() for t in self._tgt])
+        rc = self._lib.sf_polyak(n, T, S, N, ctypes.c_float(self.tau),
+                                 ctypes.c_void_p(torch.cuda.current_stream(self.dev).cuda_stream))
+        if rc != 0:
+            raise RuntimeError(f"sf_polyak failed ({rc})")
+        if losses:
+            return self._lossq.sum(), self._lossa.sum()
+        return None
+
+
 class RLLoop:
     """One RL iteration over a core.DeviceBatch in SAME_STEP mode (final_obs on) with
     the SAC above; step() runs it eagerly, capture() records it as one HIP graph."""
@@ -530,7 +677,7 @@ class RLLoop:
                 done = (b.terminated | b.truncated).bool()
                 nxt = torch.where(done[:, None], b.final_obs, b.obs)
                 s.insert(self.obs, a, b.reward, nxt, b.terminated.float())
-            s.update()
+            s.update(losses=False)
         self.obs.copy_(b.obs)
 
     def capture(self, warm=3):
