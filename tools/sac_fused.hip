@@ -22,7 +22,8 @@
 //
 // Layouts: the actor's torch Linear weights ([out, in]); the twin critics stacked as
 // tools/sac_torch.py TwinQ keeps them (w0 [2, in, H], w1 [2, H, H], w2 [2, H, 1]).  H = 256.
-// Every column sum runs over the rows in order, one thread per column: deterministic.  fp32,
+// Every column sum runs over four row quarters in order and adds them in quarter order:
+// deterministic.  fp32,
 // -ffp-contract=off; results agree with the autograd path to fp32 rounding (the association
 // of the sums differs), checked by tests/test_gpu_sac_adam.py.
 #include <hip/hip_runtime.h>
@@ -176,63 +177,112 @@ __global__ __launch_bounds__(256) void critic_head_kernel(
   }
 }
 
-// one thread per (c, u): dg1[c][r][u] = dq[c][r] w2[c][u] (g1 > 0) for every row; with grads,
-// dw2[c][u] = sum_r g1 dq, db1[c][u] = sum_r dg1, db2[c] = sum_r dq (thread u = 0)
+// The column-sum kernels below: a workgroup of 256 threads takes 64 columns (blockIdx.x) of
+// one critic (blockIdx.y) and splits the rows into four quarters (threadIdx.x / 64); each
+// thread sums its quarter in row order with its loads issued eight rows at a time, and the
+// four partials are added in quarter order through LDS -- deterministic, and enough loads in
+// flight that the loop is not one L2 round trip per row.
+constexpr int QROWS = 4;          // row quarters per workgroup
+constexpr int CPB = 64;           // columns per workgroup
+constexpr int RB = 8;             // rows per batch of loads
+
+// combine the four quarters' partials of NV values per column (in quarter order)
+template <int NV>
+__device__ __forceinline__ void quarter_sum(float (&v)[NV], float (*lds)[QROWS][CPB]) {
+  const int col = threadIdx.x % CPB, qt = threadIdx.x / CPB;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) lds[i][qt][col] = v[i];
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < NV; ++i) v[i] = ((lds[i][0][col] + lds[i][1][col]) + lds[i][2][col]) + lds[i][3][col];
+  __syncthreads();
+}
+
+// dg1[c][r][u] = dq[c][r] w2[c][u] (g1 > 0) for every row; with grads, dw2[c][u] = sum_r g1 dq,
+// db1[c][u] = sum_r dg1, db2[c] = sum_r dq
 __global__ __launch_bounds__(256) void critic_bwd_head_kernel(
     const float* __restrict__ dq, const float* __restrict__ g1, const float* __restrict__ w2, int B,
     int grads, float* __restrict__ dg1, float* __restrict__ dw2, float* __restrict__ db1,
     float* __restrict__ db2) {
-  const int u = threadIdx.x;
-  const int c = blockIdx.x;
+  __shared__ float lds[3][QROWS][CPB];
+  const int u = blockIdx.x * CPB + threadIdx.x % CPB;
+  const int qt = threadIdx.x / CPB;
+  const int c = blockIdx.y;
+  const int r0 = qt * (B / QROWS), r1 = qt == QROWS - 1 ? B : r0 + B / QROWS;
   const float wv = w2[(size_t)c * H + u];
-  float sw = 0.0f, sb = 0.0f, sq = 0.0f;
-  for (int r = 0; r < B; ++r) {
-    const size_t o = ((size_t)c * B + r) * H + u;
-    const float d = dq[(size_t)c * B + r];
-    const float g = g1[o];
-    const float v = g > 0.0f ? d * wv : 0.0f;
-    dg1[o] = v;
-    sw += g * d;
-    sb += v;
-    sq += d;
+  float v[3] = {0.0f, 0.0f, 0.0f};          // sum g1 dq, sum dg1, sum dq
+  for (int rb = r0; rb < r1; rb += RB) {
+    float gg[RB], dd[RB];
+#pragma unroll
+    for (int t = 0; t < RB; ++t) {
+      const int r = rb + t < r1 ? rb + t : r1 - 1;
+      gg[t] = g1[((size_t)c * B + r) * H + u];
+      dd[t] = dq[(size_t)c * B + r];
+    }
+#pragma unroll
+    for (int t = 0; t < RB; ++t) {
+      if (rb + t < r1) {
+        const float val = gg[t] > 0.0f ? dd[t] * wv : 0.0f;
+        dg1[((size_t)c * B + rb + t) * H + u] = val;
+        v[0] += gg[t] * dd[t];
+        v[1] += val;
+        v[2] += dd[t];
+      }
+    }
   }
-  if (grads) {
-    dw2[(size_t)c * H + u] = sw;
-    db1[(size_t)c * H + u] = sb;
-    if (u == 0) db2[c] = sq;
+  quarter_sum<3>(v, lds);
+  if (grads && qt == 0) {
+    dw2[(size_t)c * H + u] = v[0];
+    db1[(size_t)c * H + u] = v[1];
+    if (u == 0) db2[c] = v[2];
   }
 }
 
-// one thread per (c, u): m = dg0 (g0 > 0); dw0[c][k][u] = sum_r x[r][k] m, db0[c][u] = sum_r m;
-// x[r] = [xa row (Ka) | xb row (Kb)]
+// m = dg0 (g0 > 0); dw0[c][k][u] = sum_r x[r][k] m, db0[c][u] = sum_r m;  x[r] = [xa | xb]
 __global__ __launch_bounds__(256) void critic_bwd_in_kernel(
     const float* __restrict__ dg0, const float* __restrict__ g0, const float* __restrict__ xa,
     int lda, int Ka, const float* __restrict__ xb, int ldb, int Kb, int B,
     float* __restrict__ dw0, float* __restrict__ db0) {
-  const int u = threadIdx.x;
-  const int c = blockIdx.x;
+  __shared__ float lds[9][QROWS][CPB];
+  const int u = blockIdx.x * CPB + threadIdx.x % CPB;
+  const int qt = threadIdx.x / CPB;
+  const int c = blockIdx.y;
+  const int r0 = qt * (B / QROWS), r1 = qt == QROWS - 1 ? B : r0 + B / QROWS;
   const int K = Ka + Kb;
-  float sb = 0.0f;
   for (int k0 = 0; k0 < K; k0 += 8) {
-    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (int r = 0; r < B; ++r) {
-      const size_t o = ((size_t)c * B + r) * H + u;
-      const float m = g0[o] > 0.0f ? dg0[o] : 0.0f;
-      if (k0 == 0) sb += m;
+    float v[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};   // 8 weight sums, the bias sum
+    for (int rb = r0; rb < r1; rb += RB) {
+      float mm[RB];
 #pragma unroll
-      for (int t = 0; t < 8; ++t) {
-        const int k = k0 + t;
-        if (k < K) {
-          const float xv = k < Ka ? xa[(size_t)r * lda + k] : xb[(size_t)r * ldb + (k - Ka)];
-          acc[t] += xv * m;
+      for (int t = 0; t < RB; ++t) {
+        const int r = rb + t < r1 ? rb + t : r1 - 1;
+        const size_t o = ((size_t)c * B + r) * H + u;
+        const float g = g0[o], d = dg0[o];
+        mm[t] = (rb + t < r1 && g > 0.0f) ? d : 0.0f;
+      }
+#pragma unroll
+      for (int t = 0; t < RB; ++t) {
+        if (rb + t >= r1) continue;
+        const int r = rb + t;
+        v[8] += mm[t];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int k = k0 + i;
+          if (k < K) {
+            const float xv = k < Ka ? xa[(size_t)r * lda + k] : xb[(size_t)r * ldb + (k - Ka)];
+            v[i] += xv * mm[t];
+          }
         }
       }
     }
+    quarter_sum<9>(v, lds);
+    if (qt == 0) {
 #pragma unroll
-    for (int t = 0; t < 8; ++t)
-      if (k0 + t < K) dw0[((size_t)c * K + k0 + t) * H + u] = acc[t];
+      for (int i = 0; i < 8; ++i)
+        if (k0 + i < K) dw0[((size_t)c * K + k0 + i) * H + u] = v[i];
+      if (k0 == 0) db0[(size_t)c * H + u] = v[8];
+    }
   }
-  db0[(size_t)c * H + u] = sb;
 }
 
 // one wave per row: dx[r][j] = sum_c sum_u w0[c][Ka + j][u] (dg0 (g0 > 0))[c][r][u], the
@@ -302,72 +352,106 @@ __global__ __launch_bounds__(256) void actor_bwd_head_kernel(
   }
 }
 
-// one thread per u: dWmu[j][u] = sum_r dmu[r][j] h1[r][u], dWls likewise, db1[u] = sum_r dh1;
-// thread j < A: dbmu[j], dbls[j]; thread A: d log_alpha = -mean_r(logp + target_entropy)
-// (SB3's ent_coef_loss = -(log_alpha * (logp + target_entropy).detach()).mean())
+// dWmu[j][u] = sum_r dmu[r][j] h1[r][u], dWls likewise, db1[u] = sum_r dh1 (per column, row
+// quarters as above); workgroup 0's threads j < A: dbmu[j], dbls[j]; thread A: d log_alpha =
+// -mean_r(logp + target_entropy) (SB3's ent_coef_loss = -(log_alpha * (logp +
+// target_entropy).detach()).mean())
 __global__ __launch_bounds__(256) void actor_bwd_cols_kernel(
     const float* __restrict__ dmu, const float* __restrict__ dlsr, const float* __restrict__ h1,
     const float* __restrict__ dh1, const float* __restrict__ logp, float target_entropy, int R,
     int A, float* __restrict__ dwmu, float* __restrict__ dwls, float* __restrict__ db1,
     float* __restrict__ dbmu, float* __restrict__ dbls, float* __restrict__ dlog_alpha) {
-  const int u = threadIdx.x;
-  float sm[4] = {0, 0, 0, 0}, sl[4] = {0, 0, 0, 0};
-  float sb = 0.0f;
-  for (int r = 0; r < R; ++r) {
-    const float h = h1[(size_t)r * H + u];
-    sb += dh1[(size_t)r * H + u];
+  __shared__ float lds[9][QROWS][CPB];
+  const int u = blockIdx.x * CPB + threadIdx.x % CPB;
+  const int qt = threadIdx.x / CPB;
+  const int r0 = qt * (R / QROWS), r1 = qt == QROWS - 1 ? R : r0 + R / QROWS;
+  float v[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};      // dWmu[0..3], dWls[0..3], db1
+  for (int rb = r0; rb < r1; rb += RB) {
+    float hh[RB], dh[RB];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      if (j < A) {
-        sm[j] += dmu[(size_t)r * A + j] * h;
-        sl[j] += dlsr[(size_t)r * A + j] * h;
+    for (int t = 0; t < RB; ++t) {
+      const int r = rb + t < r1 ? rb + t : r1 - 1;
+      hh[t] = h1[(size_t)r * H + u];
+      dh[t] = dh1[(size_t)r * H + u];
+    }
+#pragma unroll
+    for (int t = 0; t < RB; ++t) {
+      if (rb + t >= r1) continue;
+      const int r = rb + t;
+      v[8] += dh[t];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (j < A) {
+          v[j] += dmu[(size_t)r * A + j] * hh[t];
+          v[4 + j] += dlsr[(size_t)r * A + j] * hh[t];
+        }
       }
     }
   }
-  db1[u] = sb;
+  quarter_sum<9>(v, lds);
+  if (qt == 0) {
+    db1[u] = v[8];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    if (j < A) {
-      dwmu[(size_t)j * H + u] = sm[j];
-      dwls[(size_t)j * H + u] = sl[j];
+    for (int j = 0; j < 4; ++j) {
+      if (j < A) {
+        dwmu[(size_t)j * H + u] = v[j];
+        dwls[(size_t)j * H + u] = v[4 + j];
+      }
     }
   }
-  if (u < A) {
+  if (blockIdx.x == 0 && threadIdx.x < A) {
+    const int j = threadIdx.x;
     float bm = 0.0f, bl = 0.0f;
     for (int r = 0; r < R; ++r) {
-      bm += dmu[(size_t)r * A + u];
-      bl += dlsr[(size_t)r * A + u];
+      bm += dmu[(size_t)r * A + j];
+      bl += dlsr[(size_t)r * A + j];
     }
-    dbmu[u] = bm;
-    dbls[u] = bl;
+    dbmu[j] = bm;
+    dbls[j] = bl;
   }
-  if (u == A) {
-    float s = 0.0f;
-    for (int r = 0; r < R; ++r) s += logp[r] + target_entropy;
-    dlog_alpha[0] = -(s / (float)R);
+  if (blockIdx.x == 0 && threadIdx.x == A) {
+    float sl = 0.0f;
+    for (int r = 0; r < R; ++r) sl += logp[r] + target_entropy;
+    dlog_alpha[0] = -(sl / (float)R);
   }
 }
 
-// one thread per u: m = dh0 (h0 > 0); dW0[u][k] = sum_r m x[r][k] (torch layout), db0[u]
+// m = dh0 (h0 > 0); dW0[u][k] = sum_r m x[r][k] (torch layout), db0[u] = sum_r m
 __global__ __launch_bounds__(256) void actor_bwd_in_kernel(
     const float* __restrict__ dh0, const float* __restrict__ h0, const float* __restrict__ x,
     int ldx, int K, int R, float* __restrict__ dw0, float* __restrict__ db0) {
-  const int u = threadIdx.x;
-  float sb = 0.0f;
+  __shared__ float lds[9][QROWS][CPB];
+  const int u = blockIdx.x * CPB + threadIdx.x % CPB;
+  const int qt = threadIdx.x / CPB;
+  const int r0 = qt * (R / QROWS), r1 = qt == QROWS - 1 ? R : r0 + R / QROWS;
   for (int k0 = 0; k0 < K; k0 += 8) {
-    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (int r = 0; r < R; ++r) {
-      const float m = h0[(size_t)r * H + u] > 0.0f ? dh0[(size_t)r * H + u] : 0.0f;
-      if (k0 == 0) sb += m;
+    float v[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    for (int rb = r0; rb < r1; rb += RB) {
+      float mm[RB];
 #pragma unroll
-      for (int t = 0; t < 8; ++t)
-        if (k0 + t < K) acc[t] += m * x[(size_t)r * ldx + k0 + t];
+      for (int t = 0; t < RB; ++t) {
+        const int r = rb + t < r1 ? rb + t : r1 - 1;
+        const float h = h0[(size_t)r * H + u], d = dh0[(size_t)r * H + u];
+        mm[t] = (rb + t < r1 && h > 0.0f) ? d : 0.0f;
+      }
+#pragma unroll
+      for (int t = 0; t < RB; ++t) {
+        if (rb + t >= r1) continue;
+        const int r = rb + t;
+        v[8] += mm[t];
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+          if (k0 + i < K) v[i] += mm[t] * x[(size_t)r * ldx + k0 + i];
+      }
     }
+    quarter_sum<9>(v, lds);
+    if (qt == 0) {
 #pragma unroll
-    for (int t = 0; t < 8; ++t)
-      if (k0 + t < K) dw0[(size_t)u * K + k0 + t] = acc[t];
+      for (int i = 0; i < 8; ++i)
+        if (k0 + i < K) dw0[(size_t)u * K + k0 + i] = v[i];
+      if (k0 == 0) db0[u] = v[8];
+    }
   }
-  db0[u] = sb;
 }
 
 // target = target * (1 - tau) + tau * src over up to 8 tensors (SB3 polyak_update's
@@ -437,14 +521,14 @@ int32_t sf_critic_head(const float* p1, const float* b1, const float* w2, const 
 int32_t sf_critic_bwd_head(const float* dq, const float* g1, const float* w2, int32_t B, int32_t grads,
                            float* dg1, float* dw2, float* db1, float* db2, void* stream) {
   if (!dq || !g1 || !w2 || !dg1 || B < 1 || (grads && (!dw2 || !db1 || !db2))) return -1;
-  SF_LAUNCH(critic_bwd_head_kernel, dim3(2), dim3(H), dq, g1, w2, B, grads, dg1, dw2, db1, db2);
+  SF_LAUNCH(critic_bwd_head_kernel, dim3(H / CPB, 2), dim3(256), dq, g1, w2, B, grads, dg1, dw2, db1, db2);
 }
 
 int32_t sf_critic_bwd_in(const float* dg0, const float* g0, const float* xa, int32_t lda, int32_t Ka,
                          const float* xb, int32_t ldb, int32_t Kb, int32_t B, float* dw0, float* db0,
                          void* stream) {
   if (!dg0 || !g0 || !xa || !dw0 || !db0 || B < 1 || Ka < 1 || Kb < 0 || (Kb && !xb)) return -1;
-  SF_LAUNCH(critic_bwd_in_kernel, dim3(2), dim3(H), dg0, g0, xa, lda, Ka, xb, ldb, Kb, B, dw0, db0);
+  SF_LAUNCH(critic_bwd_in_kernel, dim3(H / CPB, 2), dim3(256), dg0, g0, xa, lda, Ka, xb, ldb, Kb, B, dw0, db0);
 }
 
 int32_t sf_critic_dx(const float* dg0, const float* g0, const float* w0, int32_t K, int32_t Ka,
@@ -471,14 +555,14 @@ int32_t sf_actor_bwd_cols(const float* dmu, const float* dlsr, const float* h1, 
   if (!dmu || !dlsr || !h1 || !dh1 || !logp || !dwmu || !dwls || !db1 || !dbmu || !dbls || !dlog_alpha ||
       R < 1 || A < 1 || A > 4)
     return -1;
-  SF_LAUNCH(actor_bwd_cols_kernel, dim3(1), dim3(H), dmu, dlsr, h1, dh1, logp, target_entropy, R, A,
+  SF_LAUNCH(actor_bwd_cols_kernel, dim3(H / CPB), dim3(256), dmu, dlsr, h1, dh1, logp, target_entropy, R, A,
             dwmu, dwls, db1, dbmu, dbls, dlog_alpha);
 }
 
 int32_t sf_actor_bwd_in(const float* dh0, const float* h0, const float* x, int32_t ldx, int32_t K,
                         int32_t R, float* dw0, float* db0, void* stream) {
   if (!dh0 || !h0 || !x || !dw0 || !db0 || R < 1 || K < 1) return -1;
-  SF_LAUNCH(actor_bwd_in_kernel, dim3(1), dim3(H), dh0, h0, x, ldx, K, R, dw0, db0);
+  SF_LAUNCH(actor_bwd_in_kernel, dim3(H / CPB), dim3(256), dh0, h0, x, ldx, K, R, dw0, db0);
 }
 
 int32_t sf_polyak(int32_t n, float* const* tgt, const float* const* src, const int64_t* numel, float tau,
