@@ -205,39 +205,52 @@ def test_squashed_gaussian_matches_autograd():
         assert l1.grad[0, 0] == 0 and l1.grad[1, 0] == 0
 
 
+def _sac_pair(cls, obs_dim, act_dim, dev):
+    s = cls(obs_dim, act_dim, dev, seed=7, lr=1e-3, buffer=4096)
+    assert s.hip_adam and s.actor.fused_dist
+    gen = torch.Generator(device=dev).manual_seed(11)
+    n = 1024
+    o = torch.randn((n, obs_dim), generator=gen, device=dev)
+    a = torch.rand((n, act_dim), generator=gen, device=dev) * 2 - 1
+    r = torch.randn((n,), generator=gen, device=dev)
+    o2 = torch.randn((n, obs_dim), generator=gen, device=dev)
+    d = (torch.rand((n,), generator=gen, device=dev) < 0.1).float()
+    s.insert(o, a, r, o2, d)
+    return s
+
+
 @pytest.mark.parametrize("obs_dim,act_dim", [(4, 1), (40, 2)])
 def test_fused_sac_update_matches_autograd_update(obs_dim, act_dim):
     """FusedSAC (tools/sac_fused.hip: the forward / backward written out, rocBLAS for the
     256 x 256 products) against SAC.update on the autograd + HipAdam path: same seed, same
-    buffer, same RNG draws; after 10 updates every parameter, target parameter and log_alpha
-    within 1e-4 relative + 1e-5 absolute (the column sums and the bias adds associate
-    differently from autograd's), and the losses of the last update close.  Descent's shape
-    (obs 4, action 1) and Merge's (obs 40, action 2)."""
+    buffer, same RNG draws.  (1) The first update's gradients of every parameter and of
+    log_alpha within 1e-4 of the tensor's largest gradient (the column sums and bias adds
+    associate differently from autograd's).  (2) After 10 updates every parameter, target
+    parameter and log_alpha within 1e-4 relative + 1e-4 absolute -- a tenth of one Adam step
+    (lr 1e-3): Adam's m / sqrt(v) turns a rounding-level difference of a near-zero gradient
+    into up to a step's difference of its parameter.  (3) The losses of the last update close.
+    Descent's shape (obs 4, action 1) and Merge's (obs 40, action 2)."""
     dev = torch.device("cuda", 0)
-    out, losses = [], []
+    grads, out, losses = [], [], []
     for cls in (sac_torch.SAC, sac_torch.FusedSAC):
-        s = cls(obs_dim, act_dim, dev, seed=7, lr=1e-3, buffer=4096)
-        assert s.hip_adam and s.actor.fused_dist
-        gen = torch.Generator(device=dev).manual_seed(11)
-        n = 1024
-        o = torch.randn((n, obs_dim), generator=gen, device=dev)
-        a = torch.rand((n, act_dim), generator=gen, device=dev) * 2 - 1
-        r = torch.randn((n,), generator=gen, device=dev)
-        o2 = torch.randn((n, obs_dim), generator=gen, device=dev)
-        d = (torch.rand((n,), generator=gen, device=dev) < 0.1).float()
-        s.insert(o, a, r, o2, d)
+        s = _sac_pair(cls, obs_dim, act_dim, dev)
+        params = list(s.actor.parameters()) + list(s.q.parameters()) + [s.log_alpha]
         torch.manual_seed(5)
-        for _ in range(10):
+        s.update()
+        torch.cuda.synchronize()
+        grads.append([p.grad.detach().clone() for p in params])
+        for _ in range(9):
             lq, la = s.update()
         torch.cuda.synchronize()
         losses.append((float(lq), float(la)))
-        out.append([p.detach().clone() for p in
-                    list(s.actor.parameters()) + list(s.q.parameters()) + list(s.qt.parameters()) +
-                    [s.log_alpha]])
+        out.append([p.detach().clone() for p in params + list(s.qt.parameters())])
+    for gx, gy in zip(*grads):
+        scale = float(gx.abs().max())
+        assert float((gx - gy).abs().max()) <= 1e-4 * scale + 1e-7, (gx - gy).abs().max().item()
     for x, y in zip(*out):
-        assert torch.allclose(x, y, rtol=1e-4, atol=1e-5), (x - y).abs().max().item()
+        assert torch.allclose(x, y, rtol=1e-4, atol=1e-4), (x - y).abs().max().item()
     (lq0, la0), (lq1, la1) = losses
-    assert abs(lq0 - lq1) <= 1e-4 * abs(lq0) + 1e-5 and abs(la0 - la1) <= 1e-4 * abs(la0) + 1e-5
+    assert abs(lq0 - lq1) <= 1e-3 * abs(lq0) + 1e-4 and abs(la0 - la1) <= 1e-3 * abs(la0) + 1e-4
 
 
 def test_fused_sac_loop_is_graph_capturable():
