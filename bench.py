@@ -589,12 +589,16 @@ def c5_learner_leg(b, W, dev, steps, warm):
     rl.obs.copy_(b.obs)
     for _ in range(8):                                # fill the buffer past one batch
         rl.step()
-    rl.capture()
-    for _ in range(warm):
+    # C5_GRAPH_ITERS RL iterations per graph replay (the timed region still runs `steps`
+    # iterations: steps // iters replays)
+    iters = max(1, int(os.environ.get("C5_GRAPH_ITERS", "1")))
+    steps = max(iters, steps - steps % iters)
+    rl.capture(iters=iters)
+    for _ in range(max(1, warm // iters)):
         rl.replay()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(steps):
+    for _ in range(steps // iters):
         rl.replay()
     torch.cuda.synchronize()
     wall = (time.perf_counter() - t0) / steps
@@ -603,7 +607,7 @@ def c5_learner_leg(b, W, dev, steps, warm):
             "critic_loss": float(lq), "actor_loss": float(la),
             "learner": "SB3 SAC restated (tools/sac_torch.py): twin critics + actor 256-256, "
                        "batch 256, one update per vector step, HIP graph",
-            "update": type(sac).__name__}
+            "update": type(sac).__name__, "iters_per_graph": iters, "timed_iterations": steps}
 
 
 def bench_descent_sac(args):

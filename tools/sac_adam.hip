@@ -33,8 +33,16 @@ namespace {
 
 constexpr int BLOCK = 256;
 
+struct polyak_targets {
+  float* t[SAC_ADAM_MAX_TENSORS];
+};
+
+// tgt (optional): SB3's polyak_update of a target copy of each parameter, fused behind its Adam
+// step -- target = target (1 - tau) + tau * p_new (FusedSAC: the critic's parameters change only
+// in this step of an update, so the target update may follow it directly)
 __global__ __launch_bounds__(BLOCK) void adam_kernel(sac_adam_table T, const float* __restrict__ step,
-                                                      float lr, float b1, float b2, float eps) {
+                                                      float lr, float b1, float b2, float eps,
+                                                      polyak_targets tgt, float tau, int has_tgt) {
   const int blk = blockIdx.x;
   int i = 0;
   while (i + 1 < T.n && blk >= T.start[i + 1]) ++i;   // <= 16 tensors: a short scan
@@ -49,7 +57,12 @@ __global__ __launch_bounds__(BLOCK) void adam_kernel(sac_adam_table T, const flo
   T.m[i][k] = m;
   T.v[i][k] = v;
   const float denom = sqrtf(v) / sqrtf(bc2) + eps;
-  T.p[i][k] -= (lr / bc1) * m / denom;
+  const float pn = T.p[i][k] - (lr / bc1) * m / denom;
+  T.p[i][k] = pn;
+  if (has_tgt) {
+    const float t0 = tgt.t[i][k] * (1.0f - tau);
+    tgt.t[i][k] = t0 + tau * pn;
+  }
 }
 
 }  // namespace
@@ -62,8 +75,26 @@ extern "C" int32_t sac_adam_step(const sac_adam_table* T, const float* step, flo
     if (T->start[i + 1] - T->start[i] != (int32_t)((T->numel[i] + BLOCK - 1) / BLOCK)) return -1;
   }
   if (T->start[0] != 0) return -1;
+  polyak_targets none{};
   hipLaunchKernelGGL(adam_kernel, dim3(T->start[T->n]), dim3(BLOCK), 0, (hipStream_t)stream, *T,
-                     step, lr, b1, b2, eps);
+                     step, lr, b1, b2, eps, none, 0.0f, 0);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+// the Adam step above with each parameter's target copy polyak-updated behind it (tgt[i] has
+// T->numel[i] elements)
+extern "C" int32_t sac_adam_step_polyak(const sac_adam_table* T, const float* step, float lr, float b1,
+                                        float b2, float eps, float* const* tgt, float tau, void* stream) {
+  if (!T || !step || !tgt || T->n < 1 || T->n > SAC_ADAM_MAX_TENSORS) return -1;
+  polyak_targets pt{};
+  for (int i = 0; i < T->n; ++i) {
+    if (!T->p[i] || !T->g[i] || !T->m[i] || !T->v[i] || !tgt[i] || T->numel[i] <= 0) return -1;
+    if (T->start[i + 1] - T->start[i] != (int32_t)((T->numel[i] + BLOCK - 1) / BLOCK)) return -1;
+    pt.t[i] = tgt[i];
+  }
+  if (T->start[0] != 0) return -1;
+  hipLaunchKernelGGL(adam_kernel, dim3(T->start[T->n]), dim3(BLOCK), 0, (hipStream_t)stream, *T,
+                     step, lr, b1, b2, eps, pt, tau, 1);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 

@@ -12,17 +12,21 @@
 //   actor_head   h1 = relu(p1 + b1), mu / log_std heads, SB3's squashed Gaussian (a, logp)
 //   critic_head  g1 = relu(p1 + b1), q = g1 w2 + b2 for both critics, then per mode the TD
 //                target y, the twin-MSE gradient dq, or the actor loss's dq / dlogp
+//   td_critic_head  the target critics and the online critics of one [4, B, H] product: y,
+//                then the online heads' dq (one launch for both)
 //   critic_bwd_head   dg1 = dq w2 (g1 > 0) and the w2 / b2 / b1 gradients (column sums)
 //   critic_bwd_in     the first layer's gradients from dg0 (g0 > 0)
 //   critic_dx         the actor loss's gradient w.r.t. the critics' action inputs
-//   actor_bwd_head    the squashed Gaussian's backward and dh1 = (dmu Wmu + dlsr Wls)(h1 > 0)
+//   actor_bwd_head    the critics' action gradient, the squashed Gaussian's backward and
+//                     dh1 = (dmu Wmu + dlsr Wls)(h1 > 0)
 //   actor_bwd_cols    the heads' and b1's gradients and d log_alpha (column sums)
 //   actor_bwd_in      the first layer's gradients from dh0 (h0 > 0)
-//   polyak            target = target (1 - tau) + tau param over every critic tensor
+//   polyak            target = target (1 - tau) + tau param over every critic tensor (FusedSAC
+//                     fuses it into the critic's Adam launch, sac_adam_step_polyak)
 //
 // Layouts: the actor's torch Linear weights ([out, in]); the twin critics stacked as
 // tools/sac_torch.py TwinQ keeps them (w0 [2, in, H], w1 [2, H, H], w2 [2, H, 1]).  H = 256.
-// Every column sum runs over four row quarters in order and adds them in quarter order:
+// Every column sum runs over 16 row groups in row order and adds them in group order:
 // deterministic.  fp32,
 // -ffp-contract=off; results agree with the autograd path to fp32 rounding (the association
 // of the sums differs), checked by tests/test_gpu_sac_adam.py.
@@ -109,7 +113,7 @@ __global__ __launch_bounds__(256) void actor_head_kernel(
   if (lane == 0) logp[r] = s1 - s2;
 }
 
-enum { HEAD_TARGET = 0, HEAD_CRITIC = 1, HEAD_ACTOR_LOSS = 2 };
+enum { HEAD_TARGET = 0, HEAD_CRITIC = 1, HEAD_ACTOR_LOSS = 2, HEAD_TD_CRITIC = 3 };
 
 // one wave per row, both critics: g1 = relu(p1 + b1) (stored unless TARGET), q = g1 w2 + b2.
 //  TARGET:     y[r] = rew + gamma (1 - done) (min_c q - alpha logp2[r])      (sac_td_target)
@@ -177,25 +181,88 @@ __global__ __launch_bounds__(256) void critic_head_kernel(
   }
 }
 
-// The column-sum kernels below: a workgroup of 256 threads takes 64 columns (blockIdx.x) of
-// one critic (blockIdx.y) and splits the rows into four quarters (threadIdx.x / 64); each
-// thread sums its quarter in row order with its loads issued eight rows at a time, and the
-// four partials are added in quarter order through LDS -- deterministic, and enough loads in
-// flight that the loop is not one L2 round trip per row.
-constexpr int QROWS = 4;          // row quarters per workgroup
-constexpr int CPB = 64;           // columns per workgroup
-constexpr int RB = 8;             // rows per batch of loads
+// one wave per row, the target critics and the online critics of one [4, B, H] product (p1[0:2]
+// the targets' on [o2, a2], p1[2:4] the online critics' on [o, a]): the TD target y (as
+// HEAD_TARGET), then the online heads' g1 (stored, [2, B, H]), q and the twin-MSE gradient dq
+// and loss terms (as HEAD_CRITIC) -- both heads in one launch
+__global__ __launch_bounds__(256) void td_critic_head_kernel(
+    const float* __restrict__ p1, const float* __restrict__ tb1, const float* __restrict__ tw2,
+    const float* __restrict__ tb2, const float* __restrict__ b1, const float* __restrict__ w2,
+    const float* __restrict__ b2, int B, const float* __restrict__ rows, int W, int col_r,
+    int col_d, float gamma, const float* __restrict__ log_alpha, const float* __restrict__ logp,
+    float* __restrict__ y, float* __restrict__ g1, float* __restrict__ q_out,
+    float* __restrict__ dq, float* __restrict__ lossp) {
+  const int lane = threadIdx.x & 63;
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= B) return;
+  float q[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const int cc = c & 1;
+    const float* bb = c < 2 ? tb1 : b1;
+    const float* ww = c < 2 ? tw2 : w2;
+    float part = 0.0f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int u = lane + 64 * i;
+      const float z = p1[((size_t)c * B + r) * H + u] + bb[(size_t)cc * H + u];
+      const float g = z > 0.0f ? z : 0.0f;
+      if (c >= 2) g1[((size_t)cc * B + r) * H + u] = g;
+      part += g * ww[(size_t)cc * H + u];
+    }
+    q[c] = wave_sum(part) + (c < 2 ? tb2 : b2)[cc];
+  }
+  if (lane != 0) return;
+  const float alpha = expf(log_alpha[0]);
+  const float mn = fminf(q[0], q[1]);
+  const float qt = mn - alpha * logp[r];
+  const float d = rows[(size_t)r * W + col_d];
+  const float rw = rows[(size_t)r * W + col_r];
+  const float yr = rw + (gamma * (1.0f - d)) * qt;
+  y[r] = yr;
+  const float invB = 1.0f / (float)B;
+  float l = 0.0f;
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    q_out[(size_t)c * B + r] = q[2 + c];
+    const float df = q[2 + c] - yr;
+    dq[(size_t)c * B + r] = invB * (2.0f * df);
+    l += df * df / (float)B;
+  }
+  lossp[r] = l;
+}
 
-// combine the four quarters' partials of NV values per column (in quarter order)
+// The column-sum kernels below: a workgroup of 256 threads takes 16 columns (blockIdx.x) of
+// one critic (blockIdx.y) and splits the rows into 16 groups (threadIdx.x / 16); each thread
+// loads its group's rows (16 at B = 256) up front, sums them in row order, and the 16
+// partials are added in group order through LDS -- deterministic, every load of a thread in
+// flight at once, and 16-32 workgroups instead of a few long serial loops (a one-thread-per-
+// column loop over 256 rows took 25-45 us: profiles/r05/c5_kernel_stats_before.csv).
+constexpr int NRG = 16;           // row groups per workgroup
+constexpr int CPB = 16;           // columns per workgroup
+constexpr int RPG = 16;           // rows per group held in registers at once
+
+// combine the row groups' partials of NV values per column (in group order)
 template <int NV>
-__device__ __forceinline__ void quarter_sum(float (&v)[NV], float (*lds)[QROWS][CPB]) {
-  const int col = threadIdx.x % CPB, qt = threadIdx.x / CPB;
+__device__ __forceinline__ void group_sum(float (&v)[NV], float (*lds)[NRG][CPB]) {
+  const int col = threadIdx.x % CPB, grp = threadIdx.x / CPB;
 #pragma unroll
-  for (int i = 0; i < NV; ++i) lds[i][qt][col] = v[i];
+  for (int i = 0; i < NV; ++i) lds[i][grp][col] = v[i];
   __syncthreads();
 #pragma unroll
-  for (int i = 0; i < NV; ++i) v[i] = ((lds[i][0][col] + lds[i][1][col]) + lds[i][2][col]) + lds[i][3][col];
+  for (int i = 0; i < NV; ++i) {
+    float t = 0.0f;
+#pragma unroll
+    for (int q = 0; q < NRG; ++q) t += lds[i][q][col];
+    v[i] = t;
+  }
   __syncthreads();
+}
+
+__device__ __forceinline__ void group_rows(int R, int& r0, int& r1) {
+  const int per = (R + NRG - 1) / NRG;
+  r0 = (int)(threadIdx.x / CPB) * per;
+  r1 = min(R, r0 + per);
 }
 
 // dg1[c][r][u] = dq[c][r] w2[c][u] (g1 > 0) for every row; with grads, dw2[c][u] = sum_r g1 dq,
@@ -204,23 +271,23 @@ __global__ __launch_bounds__(256) void critic_bwd_head_kernel(
     const float* __restrict__ dq, const float* __restrict__ g1, const float* __restrict__ w2, int B,
     int grads, float* __restrict__ dg1, float* __restrict__ dw2, float* __restrict__ db1,
     float* __restrict__ db2) {
-  __shared__ float lds[3][QROWS][CPB];
+  __shared__ float lds[3][NRG][CPB];
   const int u = blockIdx.x * CPB + threadIdx.x % CPB;
-  const int qt = threadIdx.x / CPB;
   const int c = blockIdx.y;
-  const int r0 = qt * (B / QROWS), r1 = qt == QROWS - 1 ? B : r0 + B / QROWS;
+  int r0, r1;
+  group_rows(B, r0, r1);
   const float wv = w2[(size_t)c * H + u];
   float v[3] = {0.0f, 0.0f, 0.0f};          // sum g1 dq, sum dg1, sum dq
-  for (int rb = r0; rb < r1; rb += RB) {
-    float gg[RB], dd[RB];
+  for (int rb = r0; rb < r1; rb += RPG) {
+    float gg[RPG], dd[RPG];
 #pragma unroll
-    for (int t = 0; t < RB; ++t) {
-      const int r = rb + t < r1 ? rb + t : r1 - 1;
+    for (int t = 0; t < RPG; ++t) {
+      const int r = min(rb + t, r1 - 1);
       gg[t] = g1[((size_t)c * B + r) * H + u];
       dd[t] = dq[(size_t)c * B + r];
     }
 #pragma unroll
-    for (int t = 0; t < RB; ++t) {
+    for (int t = 0; t < RPG; ++t) {
       if (rb + t < r1) {
         const float val = gg[t] > 0.0f ? dd[t] * wv : 0.0f;
         dg1[((size_t)c * B + rb + t) * H + u] = val;
@@ -230,8 +297,8 @@ __global__ __launch_bounds__(256) void critic_bwd_head_kernel(
       }
     }
   }
-  quarter_sum<3>(v, lds);
-  if (grads && qt == 0) {
+  group_sum<3>(v, lds);
+  if (grads && threadIdx.x < CPB) {
     dw2[(size_t)c * H + u] = v[0];
     db1[(size_t)c * H + u] = v[1];
     if (u == 0) db2[c] = v[2];
@@ -243,40 +310,38 @@ __global__ __launch_bounds__(256) void critic_bwd_in_kernel(
     const float* __restrict__ dg0, const float* __restrict__ g0, const float* __restrict__ xa,
     int lda, int Ka, const float* __restrict__ xb, int ldb, int Kb, int B,
     float* __restrict__ dw0, float* __restrict__ db0) {
-  __shared__ float lds[9][QROWS][CPB];
+  __shared__ float lds[9][NRG][CPB];
   const int u = blockIdx.x * CPB + threadIdx.x % CPB;
-  const int qt = threadIdx.x / CPB;
   const int c = blockIdx.y;
-  const int r0 = qt * (B / QROWS), r1 = qt == QROWS - 1 ? B : r0 + B / QROWS;
+  int r0, r1;
+  group_rows(B, r0, r1);
   const int K = Ka + Kb;
   for (int k0 = 0; k0 < K; k0 += 8) {
     float v[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};   // 8 weight sums, the bias sum
-    for (int rb = r0; rb < r1; rb += RB) {
-      float mm[RB];
+    for (int rb = r0; rb < r1; rb += RPG) {
+      float mm[RPG];
+      float xs[RPG][8];
 #pragma unroll
-      for (int t = 0; t < RB; ++t) {
-        const int r = rb + t < r1 ? rb + t : r1 - 1;
+      for (int t = 0; t < RPG; ++t) {
+        const int r = min(rb + t, r1 - 1);
         const size_t o = ((size_t)c * B + r) * H + u;
         const float g = g0[o], d = dg0[o];
         mm[t] = (rb + t < r1 && g > 0.0f) ? d : 0.0f;
-      }
-#pragma unroll
-      for (int t = 0; t < RB; ++t) {
-        if (rb + t >= r1) continue;
-        const int r = rb + t;
-        v[8] += mm[t];
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-          const int k = k0 + i;
-          if (k < K) {
-            const float xv = k < Ka ? xa[(size_t)r * lda + k] : xb[(size_t)r * ldb + (k - Ka)];
-            v[i] += xv * mm[t];
-          }
+          const int k = min(k0 + i, K - 1);
+          xs[t][i] = k < Ka ? xa[(size_t)r * lda + k] : xb[(size_t)r * ldb + (k - Ka)];
         }
       }
+#pragma unroll
+      for (int t = 0; t < RPG; ++t) {
+        v[8] += mm[t];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] += xs[t][i] * mm[t];
+      }
     }
-    quarter_sum<9>(v, lds);
-    if (qt == 0) {
+    group_sum<9>(v, lds);
+    if (threadIdx.x < CPB) {
 #pragma unroll
       for (int i = 0; i < 8; ++i)
         if (k0 + i < K) dw0[((size_t)c * K + k0 + i) * H + u] = v[i];
@@ -312,11 +377,15 @@ __global__ __launch_bounds__(256) void critic_dx_kernel(
 
 // one wave per row: the squashed Gaussian's backward (sac_adam.hip sq_gauss_bwd_kernel) from
 // (ga = dx, gl = dlogp), then dh1[r][u] = (sum_j dmu Wmu[j][u] + dlsr Wls[j][u]) (h1 > 0)
+// ga == nullptr: the action gradient is the critics' (critic_dx's sum, computed here from
+// dg0 / g0 / w0 -- one launch less)
 __global__ __launch_bounds__(256) void actor_bwd_head_kernel(
     const float* __restrict__ ga, const float* __restrict__ gl, const float* __restrict__ mu,
     const float* __restrict__ lsr, const float* __restrict__ eps, const float* __restrict__ a_out,
     const float* __restrict__ h1, const float* __restrict__ wmu, const float* __restrict__ wls,
-    int R, int A, float* __restrict__ dmu, float* __restrict__ dlsr, float* __restrict__ dh1) {
+    int R, int A, float* __restrict__ dmu, float* __restrict__ dlsr, float* __restrict__ dh1,
+    const float* __restrict__ dg0, const float* __restrict__ g0, const float* __restrict__ w0,
+    int K, int Ka) {
   const int lane = threadIdx.x & 63;
   const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (r >= R) return;
@@ -324,6 +393,23 @@ __global__ __launch_bounds__(256) void actor_bwd_head_kernel(
   const float g = gl[r];
   for (int j = 0; j < A; ++j) {
     const int i = r * A + j;
+    float gaj;
+    if (ga) {
+      gaj = ga[i];
+    } else {
+      float part = 0.0f;
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const int uu = lane + 64 * t;
+          const size_t o = ((size_t)c * R + r) * H + uu;
+          const float m = g0[o] > 0.0f ? dg0[o] : 0.0f;
+          part += w0[((size_t)c * K + Ka + j) * H + uu] * m;
+        }
+      }
+      gaj = wave_sum(part);
+    }
     const float x = lsr[i];
     const float ls = fminf(fmaxf(x, -20.0f), 2.0f);
     const float sd = expf(ls);
@@ -331,7 +417,7 @@ __global__ __launch_bounds__(256) void actor_bwd_head_kernel(
     const float z = (u - mu[i]) / sd;
     const float a = a_out[i];
     const float da = 1.0f - a * a;
-    const float gu = ga[i] * da + g * (-z / sd + (2.0f * a / (da + 1e-6f)) * da);
+    const float gu = gaj * da + g * (-z / sd + (2.0f * a / (da + 1e-6f)) * da);
     const float gm = gu + g * z / sd;
     const float gsd = gu * eps[i] + g * (z * z) / sd;
     const float gls = (x >= -20.0f && x <= 2.0f) ? gsd * sd - g : 0.0f;
@@ -353,43 +439,46 @@ __global__ __launch_bounds__(256) void actor_bwd_head_kernel(
 }
 
 // dWmu[j][u] = sum_r dmu[r][j] h1[r][u], dWls likewise, db1[u] = sum_r dh1 (per column, row
-// quarters as above); workgroup 0's threads j < A: dbmu[j], dbls[j]; thread A: d log_alpha =
-// -mean_r(logp + target_entropy) (SB3's ent_coef_loss = -(log_alpha * (logp +
-// target_entropy).detach()).mean())
+// groups as above); workgroup 0's waves 1-3 reduce the per-row terms, 4 rows per lane and a
+// fixed shuffle tree: dbmu[j], dbls[j] and d log_alpha = -mean_r(logp + target_entropy) (SB3's
+// ent_coef_loss = -(log_alpha * (logp + target_entropy).detach()).mean())
 __global__ __launch_bounds__(256) void actor_bwd_cols_kernel(
     const float* __restrict__ dmu, const float* __restrict__ dlsr, const float* __restrict__ h1,
     const float* __restrict__ dh1, const float* __restrict__ logp, float target_entropy, int R,
     int A, float* __restrict__ dwmu, float* __restrict__ dwls, float* __restrict__ db1,
     float* __restrict__ dbmu, float* __restrict__ dbls, float* __restrict__ dlog_alpha) {
-  __shared__ float lds[9][QROWS][CPB];
+  __shared__ float lds[9][NRG][CPB];
   const int u = blockIdx.x * CPB + threadIdx.x % CPB;
-  const int qt = threadIdx.x / CPB;
-  const int r0 = qt * (R / QROWS), r1 = qt == QROWS - 1 ? R : r0 + R / QROWS;
+  int r0, r1;
+  group_rows(R, r0, r1);
   float v[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};      // dWmu[0..3], dWls[0..3], db1
-  for (int rb = r0; rb < r1; rb += RB) {
-    float hh[RB], dh[RB];
+  for (int rb = r0; rb < r1; rb += RPG) {
+    float hh[RPG], dh[RPG], dm[RPG][4], dl[RPG][4];
 #pragma unroll
-    for (int t = 0; t < RB; ++t) {
-      const int r = rb + t < r1 ? rb + t : r1 - 1;
+    for (int t = 0; t < RPG; ++t) {
+      const int r = min(rb + t, r1 - 1);
+      const bool in = rb + t < r1;
       hh[t] = h1[(size_t)r * H + u];
-      dh[t] = dh1[(size_t)r * H + u];
+      dh[t] = in ? dh1[(size_t)r * H + u] : 0.0f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int jj = min(j, A - 1);
+        dm[t][j] = in ? dmu[(size_t)r * A + jj] : 0.0f;
+        dl[t][j] = in ? dlsr[(size_t)r * A + jj] : 0.0f;
+      }
     }
 #pragma unroll
-    for (int t = 0; t < RB; ++t) {
-      if (rb + t >= r1) continue;
-      const int r = rb + t;
+    for (int t = 0; t < RPG; ++t) {
       v[8] += dh[t];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        if (j < A) {
-          v[j] += dmu[(size_t)r * A + j] * hh[t];
-          v[4 + j] += dlsr[(size_t)r * A + j] * hh[t];
-        }
+        v[j] += dm[t][j] * hh[t];
+        v[4 + j] += dl[t][j] * hh[t];
       }
     }
   }
-  quarter_sum<9>(v, lds);
-  if (qt == 0) {
+  group_sum<9>(v, lds);
+  if (threadIdx.x < CPB) {
     db1[u] = v[8];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -399,20 +488,21 @@ __global__ __launch_bounds__(256) void actor_bwd_cols_kernel(
       }
     }
   }
-  if (blockIdx.x == 0 && threadIdx.x < A) {
-    const int j = threadIdx.x;
-    float bm = 0.0f, bl = 0.0f;
-    for (int r = 0; r < R; ++r) {
-      bm += dmu[(size_t)r * A + j];
-      bl += dlsr[(size_t)r * A + j];
+  if (blockIdx.x != 0 || threadIdx.x < 64) return;
+  const int wv = (int)(threadIdx.x >> 6), lane = threadIdx.x & 63;   // waves 1..3
+  for (int j = 0; j < (wv == 3 ? 1 : A); ++j) {
+    float part = 0.0f;
+    for (int r = lane; r < R; r += 64) {
+      if (wv == 1) part += dmu[(size_t)r * A + j];
+      else if (wv == 2) part += dlsr[(size_t)r * A + j];
+      else part += logp[r] + target_entropy;
     }
-    dbmu[j] = bm;
-    dbls[j] = bl;
-  }
-  if (blockIdx.x == 0 && threadIdx.x == A) {
-    float sl = 0.0f;
-    for (int r = 0; r < R; ++r) sl += logp[r] + target_entropy;
-    dlog_alpha[0] = -(sl / (float)R);
+    const float sum = wave_sum(part);
+    if (lane == 0) {
+      if (wv == 1) dbmu[j] = sum;
+      else if (wv == 2) dbls[j] = sum;
+      else dlog_alpha[0] = -(sum / (float)R);
+    }
   }
 }
 
@@ -420,32 +510,32 @@ __global__ __launch_bounds__(256) void actor_bwd_cols_kernel(
 __global__ __launch_bounds__(256) void actor_bwd_in_kernel(
     const float* __restrict__ dh0, const float* __restrict__ h0, const float* __restrict__ x,
     int ldx, int K, int R, float* __restrict__ dw0, float* __restrict__ db0) {
-  __shared__ float lds[9][QROWS][CPB];
+  __shared__ float lds[9][NRG][CPB];
   const int u = blockIdx.x * CPB + threadIdx.x % CPB;
-  const int qt = threadIdx.x / CPB;
-  const int r0 = qt * (R / QROWS), r1 = qt == QROWS - 1 ? R : r0 + R / QROWS;
+  int r0, r1;
+  group_rows(R, r0, r1);
   for (int k0 = 0; k0 < K; k0 += 8) {
     float v[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-    for (int rb = r0; rb < r1; rb += RB) {
-      float mm[RB];
+    for (int rb = r0; rb < r1; rb += RPG) {
+      float mm[RPG];
+      float xs[RPG][8];
 #pragma unroll
-      for (int t = 0; t < RB; ++t) {
-        const int r = rb + t < r1 ? rb + t : r1 - 1;
+      for (int t = 0; t < RPG; ++t) {
+        const int r = min(rb + t, r1 - 1);
         const float h = h0[(size_t)r * H + u], d = dh0[(size_t)r * H + u];
         mm[t] = (rb + t < r1 && h > 0.0f) ? d : 0.0f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) xs[t][i] = x[(size_t)r * ldx + min(k0 + i, K - 1)];
       }
 #pragma unroll
-      for (int t = 0; t < RB; ++t) {
-        if (rb + t >= r1) continue;
-        const int r = rb + t;
+      for (int t = 0; t < RPG; ++t) {
         v[8] += mm[t];
 #pragma unroll
-        for (int i = 0; i < 8; ++i)
-          if (k0 + i < K) v[i] += mm[t] * x[(size_t)r * ldx + k0 + i];
+        for (int i = 0; i < 8; ++i) v[i] += mm[t] * xs[t][i];
       }
     }
-    quarter_sum<9>(v, lds);
-    if (qt == 0) {
+    group_sum<9>(v, lds);
+    if (threadIdx.x < CPB) {
 #pragma unroll
       for (int i = 0; i < 8; ++i)
         if (k0 + i < K) dw0[(size_t)u * K + k0 + i] = v[i];
@@ -540,12 +630,26 @@ int32_t sf_critic_dx(const float* dg0, const float* g0, const float* w0, int32_t
 int32_t sf_actor_bwd_head(const float* ga, const float* gl, const float* mu, const float* lsr,
                           const float* eps, const float* a_out, const float* h1, const float* wmu,
                           const float* wls, int32_t R, int32_t A, float* dmu, float* dlsr, float* dh1,
+                          const float* dg0, const float* g0, const float* w0, int32_t K, int32_t Ka,
                           void* stream) {
-  if (!ga || !gl || !mu || !lsr || !eps || !a_out || !h1 || !wmu || !wls || !dmu || !dlsr || !dh1 ||
+  if (!gl || !mu || !lsr || !eps || !a_out || !h1 || !wmu || !wls || !dmu || !dlsr || !dh1 ||
       R < 1 || A < 1 || A > 4)
     return -1;
+  if (!ga && (!dg0 || !g0 || !w0 || Ka < 0 || Ka + A > K)) return -1;
   SF_LAUNCH(actor_bwd_head_kernel, dim3((R + 3) / 4), dim3(256), ga, gl, mu, lsr, eps, a_out, h1, wmu,
-            wls, R, A, dmu, dlsr, dh1);
+            wls, R, A, dmu, dlsr, dh1, dg0, g0, w0, K, Ka);
+}
+
+int32_t sf_td_critic_head(const float* p1, const float* tb1, const float* tw2, const float* tb2,
+                          const float* b1, const float* w2, const float* b2, int32_t B, const float* rows,
+                          int32_t W, int32_t col_r, int32_t col_d, float gamma, const float* log_alpha,
+                          const float* logp, float* y, float* g1, float* q_out, float* dq, float* lossp,
+                          void* stream) {
+  if (!p1 || !tb1 || !tw2 || !tb2 || !b1 || !w2 || !b2 || !rows || !log_alpha || !logp || !y || !g1 ||
+      !q_out || !dq || !lossp || B < 1 || col_r < 0 || col_r >= W || col_d < 0 || col_d >= W)
+    return -1;
+  SF_LAUNCH(td_critic_head_kernel, dim3((B + 3) / 4), dim3(256), p1, tb1, tw2, tb2, b1, w2, b2, B, rows,
+            W, col_r, col_d, gamma, log_alpha, logp, y, g1, q_out, dq, lossp);
 }
 
 int32_t sf_actor_bwd_cols(const float* dmu, const float* dlsr, const float* h1, const float* dh1,

@@ -55,7 +55,7 @@ class HipAdam:
 
     _lib = None
 
-    def __init__(self, params, lr, betas=(0.9, 0.999), eps=1e-8, step=None):
+    def __init__(self, params, lr, betas=(0.9, 0.999), eps=1e-8, step=None, targets=None, tau=0.0):
         if HipAdam._lib is None:
             if not os.path.exists(ADAM_LIB):
                 raise RuntimeError(f"{ADAM_LIB} missing: run __graft_entry__.build()")
@@ -63,6 +63,10 @@ class HipAdam:
             lib.sac_adam_step.restype = ctypes.c_int32
             lib.sac_adam_step.argtypes = [ctypes.POINTER(_AdamTable), ctypes.c_void_p, ctypes.c_float,
                                           ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_void_p]
+            lib.sac_adam_step_polyak.restype = ctypes.c_int32
+            lib.sac_adam_step_polyak.argtypes = [ctypes.POINTER(_AdamTable), ctypes.c_void_p, ctypes.c_float,
+                                                 ctypes.c_float, ctypes.c_float, ctypes.c_float,
+                                                 ctypes.c_void_p * _MAXT, ctypes.c_float, ctypes.c_void_p]
             lib.sac_replay_insert.restype = ctypes.c_int32
             lib.sac_replay_insert.argtypes = ([ctypes.c_void_p, ctypes.c_longlong, ctypes.c_int32,
                                                ctypes.c_int32] + [ctypes.c_void_p] * 7 +
@@ -100,6 +104,16 @@ class HipAdam:
         self.lr, self.b1, self.b2, self.eps = float(lr), float(betas[0]), float(betas[1]), float(eps)
         self.t = step if step is not None else torch.zeros((), dtype=torch.float32,
                                                              device=self.params[0].device)
+        # targets: a target copy per parameter, polyak-updated in the same launch behind the
+        # parameter's Adam step (target = target (1 - tau) + tau p_new, SB3's polyak_update)
+        self.targets, self.tau = None, float(tau)
+        if targets is not None:
+            targets = list(targets)
+            if len(targets) != len(self.params) or any(
+                    t.shape != p.shape or t.dtype != p.dtype or not t.is_contiguous()
+                    for t, p in zip(targets, self.params)):
+                raise ValueError("HipAdam: one contiguous target per parameter, of its shape")
+            self.targets = targets
 
     def tick(self):
         self.t.add_(1.0)
@@ -122,8 +136,13 @@ class HipAdam:
             T.start[i + 1] = acc
             T.p[i], T.g[i], T.m[i], T.v[i] = p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr()
         stream = ctypes.c_void_p(torch.cuda.current_stream(self.params[0].device).cuda_stream)
-        rc = self._lib.sac_adam_step(ctypes.byref(T), ctypes.c_void_p(self.t.data_ptr()), self.lr,
-                                     self.b1, self.b2, self.eps, stream)
+        if self.targets is not None:
+            tg = (ctypes.c_void_p * _MAXT)(*[t.data_ptr() for t in self.targets])
+            rc = self._lib.sac_adam_step_polyak(ctypes.byref(T), ctypes.c_void_p(self.t.data_ptr()),
+                                                self.lr, self.b1, self.b2, self.eps, tg, self.tau, stream)
+        else:
+            rc = self._lib.sac_adam_step(ctypes.byref(T), ctypes.c_void_p(self.t.data_ptr()), self.lr,
+                                         self.b1, self.b2, self.eps, stream)
         if rc != 0:
             raise RuntimeError(f"sac_adam_step failed ({rc})")
 
@@ -523,27 +542,37 @@ class FusedSAC(SAC):
             lib = ctypes.CDLL(FUSED_LIB)
             for name in ("sf_in_layer", "sf_actor_head", "sf_critic_head", "sf_critic_bwd_head",
                          "sf_critic_bwd_in", "sf_critic_dx", "sf_actor_bwd_head", "sf_actor_bwd_cols",
-                         "sf_actor_bwd_in", "sf_polyak"):
+                         "sf_actor_bwd_in", "sf_polyak", "sf_td_critic_head"):
                 getattr(lib, name).restype = ctypes.c_int32
             FusedSAC._lib = lib
         HipAdam([torch.zeros(1, device=self.dev)], 0.0)         # loads sac_adam.hip's library
         d, B, od, A = self.dev, self.batch, self.od, self.ad
         H = 256
         z = lambda *shape: torch.zeros(shape, dtype=torch.float32, device=d)  # noqa: E731
+        # the target critics' and the online critics' second layers in one [4, H, H] tensor
+        # (qt.w1 = [0:2], q.w1 = [2:4], views): the TD target's and the critic loss's hidden
+        # products are one bmm and one head launch
+        self._w1 = torch.cat([self.qt.w1.detach(), self.q.w1.detach()]).contiguous()
+        self.qt.w1 = nn.Parameter(self._w1[0:2], requires_grad=self.qt.w1.requires_grad)
+        self.q.w1 = nn.Parameter(self._w1[2:4])
+        # the critic's optimizer is rebuilt over the new q.w1 (fresh moments, as at creation)
+        # with SB3's polyak_update of the targets fused behind its Adam step: the critics'
+        # parameters do not change between their step and the update's polyak
+        self.opt_q = HipAdam(self.q.parameters(), self.opt_q.lr, step=self.opt_q.t,
+                             targets=self.qt.parameters(), tau=self.tau)
         self._u = z(B)
         self._rows = z(B, self.buf.shape[1])
         self._eps = z(2 * B, A)
         self._h0, self._p1a, self._h1 = z(2 * B, H), z(2 * B, H), z(2 * B, H)
         self._mu, self._lsr, self._act, self._logp = z(2 * B, A), z(2 * B, A), z(2 * B, A), z(2 * B)
-        self._g0, self._p1c, self._g1 = z(2, B, H), z(2, B, H), z(2, B, H)
+        self._g04, self._p14, self._g1 = z(4, B, H), z(4, B, H), z(2, B, H)
+        self._g0, self._p1c = self._g04[2:4], self._p14[2:4]
         self._q, self._y, self._dq = z(2, B), z(B), z(2, B)
         self._dlogp, self._lossq, self._lossa = z(B), z(B), z(B)
         self._dg1, self._dg0, self._dx = z(2, B, H), z(2, B, H), z(B, A)
         self._dh1, self._dh0, self._dmu, self._dlsr = z(B, H), z(B, H), z(B, A), z(B, A)
         for p in list(self.actor.parameters()) + list(self.q.parameters()) + [self.log_alpha]:
             p.grad = torch.zeros_like(p)
-        self._tgt = list(self.qt.parameters())
-        self._src = list(self.q.parameters())
 
     def _call(self, name, *args):
         c = []
@@ -593,16 +622,14 @@ class FusedSAC(SAC):
         f("sf_actor_head", self._p1a, la_[2].bias, lat.mu.weight, lat.mu.bias, lat.log_std.weight,
           lat.log_std.bias, self._eps, 2 * B, A, self._h1, self._mu, self._lsr, act, logp)
         q, qt = self.q, self.qt
-        # ---- TD target from the target critics on [o2, a2] ----
-        f("sf_in_layer", o2, None, B, W, od, act, A, A, B, 2, qt.w0, 1, qt.b0, self._g0)
-        torch.bmm(self._g0, qt.w1, out=self._p1c)
-        f("sf_critic_head", self._p1c, qt.b1, qt.w2, qt.b2, B, 0, rows, W, od + A, W - 1, self.gamma,
-          self.log_alpha, logp, self._y, None, self._q, None, None, None)
-        # ---- critics on [o, a]: twin MSE, its gradient, the critic step -------------------------
+        # ---- TD target from the target critics on [o2, a2] and the critics on [o, a]: one
+        # bmm over the four second layers, one head (y, then the twin MSE's gradient) ---------
+        f("sf_in_layer", o2, None, B, W, od, act, A, A, B, 2, qt.w0, 1, qt.b0, self._g04[0:2])
         f("sf_in_layer", o, None, B, W, od, a, W, A, B, 2, q.w0, 1, q.b0, self._g0)
-        torch.bmm(self._g0, q.w1, out=self._p1c)
-        f("sf_critic_head", self._p1c, q.b1, q.w2, q.b2, B, 1, None, W, 0, 0, self.gamma,
-          self.log_alpha, None, self._y, self._g1, self._q, self._dq, None, self._lossq)
+        torch.bmm(self._g04, self._w1, out=self._p14)
+        f("sf_td_critic_head", self._p14, qt.b1, qt.w2, qt.b2, q.b1, q.w2, q.b2, B, rows, W, od + A,
+          W - 1, self.gamma, self.log_alpha, logp, self._y, self._g1, self._q, self._dq, self._lossq)
+        # ---- the critics' backward and step (polyak of the targets in the same launch) ---------
         f("sf_critic_bwd_head", self._dq, self._g1, q.w2, B, 1, self._dg1, q.w2.grad, q.b1.grad, q.b2.grad)
         torch.bmm(self._g0.transpose(1, 2), self._dg1, out=q.w1.grad)
         torch.bmm(self._dg1, q.w1.transpose(1, 2), out=self._dg0)
@@ -617,11 +644,12 @@ class FusedSAC(SAC):
           self.log_alpha, lp, None, self._g1, self._q, self._dq, self._dlogp, self._lossa)
         f("sf_critic_bwd_head", self._dq, self._g1, q.w2, B, 0, self._dg1, None, None, None)
         torch.bmm(self._dg1, q.w1.transpose(1, 2), out=self._dg0)
-        f("sf_critic_dx", self._dg0, self._g0, q.w0, ic, od, A, B, self._dx)
-        # ---- actor backward (the o half of the pass), entropy coefficient, their step --------
+        # ---- actor backward (the o half of the pass; the critics' action gradient computed in
+        # its head launch), entropy coefficient, their step ----------------------------------
         h0b, h1b = self._h0[B:], self._h1[B:]
-        f("sf_actor_bwd_head", self._dx, self._dlogp, self._mu[B:], self._lsr[B:], self._eps[B:], ap,
-          h1b, lat.mu.weight, lat.log_std.weight, B, A, self._dmu, self._dlsr, self._dh1)
+        f("sf_actor_bwd_head", None, self._dlogp, self._mu[B:], self._lsr[B:], self._eps[B:], ap,
+          h1b, lat.mu.weight, lat.log_std.weight, B, A, self._dmu, self._dlsr, self._dh1,
+          self._dg0, self._g0, q.w0, ic, od)
         f("sf_actor_bwd_cols", self._dmu, self._dlsr, h1b, self._dh1, lp, float(self.target_entropy), B, A,
           lat.mu.weight.grad, lat.log_std.weight.grad, la_[2].bias.grad, lat.mu.bias.grad,
           lat.log_std.bias.grad, self.log_alpha.grad)
@@ -629,15 +657,6 @@ class FusedSAC(SAC):
         torch.mm(self._dh1, la_[2].weight, out=self._dh0)
         f("sf_actor_bwd_in", self._dh0, h0b, o, W, od, B, la_[0].weight.grad, la_[0].bias.grad)
         self.opt_a.step()                            # actor + log_alpha in one launch
-        # ---- SB3 polyak_update of the target critics ---------------------------------------
-        n = len(self._tgt)
-        T = (ctypes.c_void_p * n)(*[t.data_ptr() for t in self._tgt])
-        S = (ctypes.c_void_p * n)(*[t.data_ptr() for t in self._src])
-        N = (ctypes.c_int64 * n)(*[t.numel() for t in self._tgt])
-        rc = self._lib.sf_polyak(n, T, S, N, ctypes.c_float(self.tau),
-                                 ctypes.c_void_p(torch.cuda.current_stream(self.dev).cuda_stream))
-        if rc != 0:
-            raise RuntimeError(f"sf_polyak failed ({rc})")
         if losses:
             return self._lossq.sum(), self._lossa.sum()
         return None
@@ -651,7 +670,7 @@ class RLLoop:
         self.b, self.sac, self.learn = batch, sac, learn
         self.obs = batch.obs.clone()
         self.act = torch.zeros((batch.E, batch.act_dim), dtype=torch.float64, device=batch.device)
-        self.graph = None
+        self.graph, self.iters = None, 1
         # fused_policy: the action sample is one HIP kernel (bluesky_gym.policy.SACPolicy,
         # bsg_policy_sac) reading the live actor's parameters, instead of ~25 torch kernels
         self.pol = None
@@ -680,7 +699,10 @@ class RLLoop:
             s.update(losses=False)
         self.obs.copy_(b.obs)
 
-    def capture(self, warm=3):
+    def capture(self, warm=3, iters=1):
+        """iters: RL iterations per graph (each replay runs that many, in order, each with its
+        own RNG offsets).  A replay costs host-side submission and torch's two RNG-state fills
+        ahead of the graph -- gaps on the GPU that more iterations per graph amortise."""
         side = torch.cuda.Stream(device=self.b.device)
         side.wait_stream(torch.cuda.current_stream(self.b.device))
         with torch.cuda.stream(side):
@@ -689,8 +711,9 @@ class RLLoop:
         torch.cuda.current_stream(self.b.device).wait_stream(side)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
-            self.step()
-        self.graph = g
+            for _ in range(iters):
+                self.step()
+        self.graph, self.iters = g, iters
 
     def replay(self):
         self.graph.replay()
