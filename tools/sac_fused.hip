@@ -16,13 +16,12 @@
 //                then the online heads' dq (one launch for both)
 //   critic_bwd_head   dg1 = dq w2 (g1 > 0) and the w2 / b2 / b1 gradients (column sums)
 //   critic_bwd_in     the first layer's gradients from dg0 (g0 > 0)
-//   critic_dx         the actor loss's gradient w.r.t. the critics' action inputs
 //   actor_bwd_head    the critics' action gradient, the squashed Gaussian's backward and
 //                     dh1 = (dmu Wmu + dlsr Wls)(h1 > 0)
 //   actor_bwd_cols    the heads' and b1's gradients and d log_alpha (column sums)
 //   actor_bwd_in      the first layer's gradients from dh0 (h0 > 0)
-//   polyak            target = target (1 - tau) + tau param over every critic tensor (FusedSAC
-//                     fuses it into the critic's Adam launch, sac_adam_step_polyak)
+//   (SB3's polyak_update of the target critics runs inside the critic's Adam launch,
+//   tools/sac_adam.hip sac_adam_step_polyak)
 //
 // Layouts: the actor's torch Linear weights ([out, in]); the twin critics stacked as
 // tools/sac_torch.py TwinQ keeps them (w0 [2, in, H], w1 [2, H, H], w2 [2, H, 1]).  H = 256.
@@ -352,33 +351,10 @@ __global__ __launch_bounds__(256) void critic_bwd_in_kernel(
 
 // one wave per row: dx[r][j] = sum_c sum_u w0[c][Ka + j][u] (dg0 (g0 > 0))[c][r][u], the
 // gradient w.r.t. the critics' action inputs (columns Ka.. of their input)
-__global__ __launch_bounds__(256) void critic_dx_kernel(
-    const float* __restrict__ dg0, const float* __restrict__ g0, const float* __restrict__ w0,
-    int K, int Ka, int A, int B, float* __restrict__ dx) {
-  const int lane = threadIdx.x & 63;
-  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (r >= B) return;
-  for (int j = 0; j < A; ++j) {
-    float part = 0.0f;
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int u = lane + 64 * i;
-        const size_t o = ((size_t)c * B + r) * H + u;
-        const float m = g0[o] > 0.0f ? dg0[o] : 0.0f;
-        part += w0[((size_t)c * K + Ka + j) * H + u] * m;
-      }
-    }
-    const float s = wave_sum(part);
-    if (lane == 0) dx[(size_t)r * A + j] = s;
-  }
-}
-
 // one wave per row: the squashed Gaussian's backward (sac_adam.hip sq_gauss_bwd_kernel) from
 // (ga = dx, gl = dlogp), then dh1[r][u] = (sum_j dmu Wmu[j][u] + dlsr Wls[j][u]) (h1 > 0)
-// ga == nullptr: the action gradient is the critics' (critic_dx's sum, computed here from
-// dg0 / g0 / w0 -- one launch less)
+// ga == nullptr: the action gradient is the critics' (the sum over both critics of
+// w0's action rows times dg0 (g0 > 0), computed here -- one launch less)
 __global__ __launch_bounds__(256) void actor_bwd_head_kernel(
     const float* __restrict__ ga, const float* __restrict__ gl, const float* __restrict__ mu,
     const float* __restrict__ lsr, const float* __restrict__ eps, const float* __restrict__ a_out,
@@ -544,26 +520,6 @@ __global__ __launch_bounds__(256) void actor_bwd_in_kernel(
   }
 }
 
-// target = target * (1 - tau) + tau * src over up to 8 tensors (SB3 polyak_update's
-// mul_ then add_(alpha = tau))
-struct PolyakTable {
-  int32_t n;
-  int32_t start[9];
-  int64_t numel[8];
-  float* tgt[8];
-  const float* src[8];
-};
-
-__global__ __launch_bounds__(256) void polyak_kernel(PolyakTable T, float tau) {
-  const int blk = blockIdx.x;
-  int i = 0;
-  while (i + 1 < T.n && blk >= T.start[i + 1]) ++i;
-  const int64_t k = (int64_t)(blk - T.start[i]) * 256 + threadIdx.x;
-  if (k >= T.numel[i]) return;
-  const float t = T.tgt[i][k] * (1.0f - tau);
-  T.tgt[i][k] = t + tau * T.src[i][k];
-}
-
 }  // namespace
 
 #define SF_LAUNCH(kern, grid, block, ...)                                                    \
@@ -621,12 +577,6 @@ int32_t sf_critic_bwd_in(const float* dg0, const float* g0, const float* xa, int
   SF_LAUNCH(critic_bwd_in_kernel, dim3(H / CPB, 2), dim3(256), dg0, g0, xa, lda, Ka, xb, ldb, Kb, B, dw0, db0);
 }
 
-int32_t sf_critic_dx(const float* dg0, const float* g0, const float* w0, int32_t K, int32_t Ka,
-                     int32_t A, int32_t B, float* dx, void* stream) {
-  if (!dg0 || !g0 || !w0 || !dx || B < 1 || A < 1 || Ka < 0 || Ka + A > K) return -1;
-  SF_LAUNCH(critic_dx_kernel, dim3((B + 3) / 4), dim3(256), dg0, g0, w0, K, Ka, A, B, dx);
-}
-
 int32_t sf_actor_bwd_head(const float* ga, const float* gl, const float* mu, const float* lsr,
                           const float* eps, const float* a_out, const float* h1, const float* wmu,
                           const float* wls, int32_t R, int32_t A, float* dmu, float* dlsr, float* dh1,
@@ -667,22 +617,6 @@ int32_t sf_actor_bwd_in(const float* dh0, const float* h0, const float* x, int32
                         int32_t R, float* dw0, float* db0, void* stream) {
   if (!dh0 || !h0 || !x || !dw0 || !db0 || R < 1 || K < 1) return -1;
   SF_LAUNCH(actor_bwd_in_kernel, dim3(H / CPB), dim3(256), dh0, h0, x, ldx, K, R, dw0, db0);
-}
-
-int32_t sf_polyak(int32_t n, float* const* tgt, const float* const* src, const int64_t* numel, float tau,
-                  void* stream) {
-  if (n < 1 || n > 8 || !tgt || !src || !numel) return -1;
-  PolyakTable T{};
-  T.n = n;
-  T.start[0] = 0;
-  for (int i = 0; i < n; ++i) {
-    if (!tgt[i] || !src[i] || numel[i] <= 0) return -1;
-    T.numel[i] = numel[i];
-    T.tgt[i] = tgt[i];
-    T.src[i] = src[i];
-    T.start[i + 1] = T.start[i] + (int32_t)((numel[i] + 255) / 256);
-  }
-  SF_LAUNCH(polyak_kernel, dim3(T.start[n]), dim3(256), T, tau);
 }
 
 }  // extern "C"

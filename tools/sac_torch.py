@@ -541,8 +541,8 @@ class FusedSAC(SAC):
                 raise RuntimeError(f"{FUSED_LIB} missing: run __graft_entry__.build()")
             lib = ctypes.CDLL(FUSED_LIB)
             for name in ("sf_in_layer", "sf_actor_head", "sf_critic_head", "sf_critic_bwd_head",
-                         "sf_critic_bwd_in", "sf_critic_dx", "sf_actor_bwd_head", "sf_actor_bwd_cols",
-                         "sf_actor_bwd_in", "sf_polyak", "sf_td_critic_head"):
+                         "sf_critic_bwd_in", "sf_actor_bwd_head", "sf_actor_bwd_cols", "sf_actor_bwd_in",
+                         "sf_td_critic_head"):
                 getattr(lib, name).restype = ctypes.c_int32
             FusedSAC._lib = lib
         HipAdam([torch.zeros(1, device=self.dev)], 0.0)         # loads sac_adam.hip's library
@@ -569,7 +569,7 @@ class FusedSAC(SAC):
         self._g0, self._p1c = self._g04[2:4], self._p14[2:4]
         self._q, self._y, self._dq = z(2, B), z(B), z(2, B)
         self._dlogp, self._lossq, self._lossa = z(B), z(B), z(B)
-        self._dg1, self._dg0, self._dx = z(2, B, H), z(2, B, H), z(B, A)
+        self._dg1, self._dg0 = z(2, B, H), z(2, B, H)
         self._dh1, self._dh0, self._dmu, self._dlsr = z(B, H), z(B, H), z(B, A), z(B, A)
         for p in list(self.actor.parameters()) + list(self.q.parameters()) + [self.log_alpha]:
             p.grad = torch.zeros_like(p)
