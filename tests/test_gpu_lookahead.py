@@ -94,6 +94,55 @@ def test_spawn_cache_serves_the_resets():
     assert hit > 0.9, hit
 
 
+def test_spawn_cache_entries_are_what_the_resets_take():
+    """Not circular: two identical 512-env batches; once the helper waves have
+    filled the cache, B's cached creation latitudes are shifted by 1e-3 deg.  Every env that
+    resets afterwards must come up in B at exactly its A position + 1e-3 in every aircraft
+    whose entry was poisoned -- the resetting launch took the cached entries, not a fresh
+    Philox draw -- and an env that has not reset yet stays bit-identical to A."""
+    E, N = 512, 32
+    A, B = _batch(E, N, True), _batch(E, N, True)
+    g = torch.Generator(device="cuda").manual_seed(3)
+    A.reset()
+    B.reset()
+
+    def act():
+        return torch.rand((E, A.act_dim), dtype=torch.float64, device="cuda", generator=g) * 2 - 1
+
+    for _ in range(45):
+        a = act()
+        A.step(a)
+        B.step(a)
+    torch.cuda.synchronize()
+    EN = E * N
+    sc0 = (2 * 13 + 2) * EN + 8 * E                 # bsg_internal.h la_sc_offset: [3][EN] + tags
+    tags = B._la_buf[sc0 + 3 * EN:sc0 + 3 * EN + E].view(torch.int64)
+    filled = tags == (B.envs["episode"].to(torch.int64) & 0xFFFFFFFF)
+    assert filled.float().mean().item() > 0.9
+    lat = B._la_buf[sc0:sc0 + EN].view(E, N)
+    lat[filled] += 1e-3
+    torch.cuda.synchronize()
+    pending = filled.clone()                        # poisoned envs that have not reset yet
+    served = 0
+    for _ in range(25):
+        ep0 = B.envs["episode"].clone()
+        a = act()
+        A.step(a)
+        B.step(a)
+        torch.cuda.synchronize()
+        reset = B.envs["episode"] != ep0
+        assert torch.equal(reset, A.envs["episode"] != ep0)
+        now = reset & pending
+        if now.any():
+            d = (B.state["lat"] - A.state["lat"])[now]
+            assert torch.allclose(d, torch.full_like(d, 1e-3), rtol=0, atol=1e-9), d.abs().max()
+            served += int(now.sum())
+        pending &= ~reset
+        keep = pending
+        assert torch.equal(B.state["lat"][keep].view(torch.int64), A.state["lat"][keep].view(torch.int64))
+    assert served > E // 2, served
+
+
 @pytest.mark.parametrize("kind", ["merge", "vertical"])
 def test_lookahead_with_host_spawn_rows_and_toggle(kind):
     """Parity mode (host spawn rows for the NEXT_STEP resets) and switching the lookahead
