@@ -178,8 +178,10 @@ namespace {
 __global__ __launch_bounds__(256) void replay_sample_kernel(const float* __restrict__ buf, long long cap,
                                                            int W, const float* __restrict__ u, int B,
                                                            const long long* __restrict__ size,
-                                                           float* __restrict__ out) {
+                                                           float* __restrict__ out,
+                                                           float* __restrict__ tick) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (tick && i == 0) tick[0] += 1.0f;     // HipAdam.tick (t.add_(1.0)) folded in: no reader here
   if (i >= (long long)B * W) return;
   const int b = (int)(i / W), c = (int)(i - (long long)b * W);
   long long idx = (long long)(u[b] * (float)size[0]);
@@ -195,7 +197,19 @@ extern "C" int32_t sac_replay_sample(const float* buf, long long cap, int32_t ro
   if (!buf || cap < 1 || row_width < 1 || !u || batch < 1 || !size || !out) return -1;
   const long long n = (long long)batch * row_width;
   hipLaunchKernelGGL(replay_sample_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
-                     (hipStream_t)stream, buf, cap, row_width, u, batch, size, out);
+                     (hipStream_t)stream, buf, cap, row_width, u, batch, size, out, nullptr);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+// the sample above with the optimizers' device step count advanced in the same launch
+// (FusedSAC: one launch less per update; the count is read only by the Adam launches after it)
+extern "C" int32_t sac_replay_sample_tick(const float* buf, long long cap, int32_t row_width,
+                                          const float* u, int32_t batch, const long long* size,
+                                          float* out, float* step, void* stream) {
+  if (!buf || cap < 1 || row_width < 1 || !u || batch < 1 || !size || !out || !step) return -1;
+  const long long n = (long long)batch * row_width;
+  hipLaunchKernelGGL(replay_sample_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, buf, cap, row_width, u, batch, size, out, step);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 

@@ -75,6 +75,10 @@ class HipAdam:
             lib.sac_replay_sample.argtypes = [ctypes.c_void_p, ctypes.c_longlong, ctypes.c_int32,
                                               ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p,
                                               ctypes.c_void_p, ctypes.c_void_p]
+            lib.sac_replay_sample_tick.restype = ctypes.c_int32
+            lib.sac_replay_sample_tick.argtypes = [ctypes.c_void_p, ctypes.c_longlong, ctypes.c_int32,
+                                                   ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p,
+                                                   ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
             lib.sac_td_target.restype = ctypes.c_int32
             lib.sac_td_target.argtypes = ([ctypes.c_void_p] * 4 + [ctypes.c_int32] * 3 +
                                           [ctypes.c_float, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p])
@@ -603,12 +607,14 @@ class FusedSAC(SAC):
         rows = self._rows
         L = HipAdam._lib
         torch.rand(B, device=self.dev, out=self._u)
-        rc = L.sac_replay_sample(ctypes.c_void_p(self.buf.data_ptr()), self.cap, W,
-                                 ctypes.c_void_p(self._u.data_ptr()), B,
-                                 ctypes.c_void_p(self.size.data_ptr()), ctypes.c_void_p(rows.data_ptr()),
-                                 ctypes.c_void_p(torch.cuda.current_stream(self.dev).cuda_stream))
+        # the sample, with the shared Adam step count advanced in the same launch (opt_q.tick())
+        rc = L.sac_replay_sample_tick(ctypes.c_void_p(self.buf.data_ptr()), self.cap, W,
+                                      ctypes.c_void_p(self._u.data_ptr()), B,
+                                      ctypes.c_void_p(self.size.data_ptr()), ctypes.c_void_p(rows.data_ptr()),
+                                      ctypes.c_void_p(self.opt_q.t.data_ptr()),
+                                      ctypes.c_void_p(torch.cuda.current_stream(self.dev).cuda_stream))
         if rc != 0:
-            raise RuntimeError(f"sac_replay_sample failed ({rc})")
+            raise RuntimeError(f"sac_replay_sample_tick failed ({rc})")
         torch.randn((2 * B, A), device=self.dev, out=self._eps)
         f = self._call
         o = rows                                    # columns 0..od of the row
@@ -634,8 +640,7 @@ class FusedSAC(SAC):
         torch.bmm(self._g0.transpose(1, 2), self._dg1, out=q.w1.grad)
         torch.bmm(self._dg1, q.w1.transpose(1, 2), out=self._dg0)
         f("sf_critic_bwd_in", self._dg0, self._g0, o, W, od, a, W, A, B, q.w0.grad, q.b0.grad)
-        self.opt_q.tick()                            # shared step count: every group steps once
-        self.opt_q.step()
+        self.opt_q.step()                            # (the step count was advanced by the sample)
         # ---- actor loss through the updated critics on [o, ap] (critics frozen) ----------------
         ap, lp = act[B:], logp[B:]
         f("sf_in_layer", o, None, B, W, od, ap, A, A, B, 2, q.w0, 1, q.b0, self._g0)
