@@ -1755,6 +1755,23 @@ __device__ __forceinline__ void hdg_spd_action(const KParams& p, AC& s, double a
 #ifndef BSG_FAST_DEBUG
 #define BSG_FAST_DEBUG 0
 #endif
+// Three passes per block of up to kVB substeps instead of one substep after the other
+// (round 5): the climb/descent chain (vertical speed slew, altitude) never reads the speed
+// chain -- the only coupling, vs_max_with_acc, applies when the commanded |vs| exceeds
+// VSMAX (4,000 fpm), which the env's 12.5 m/s commands and APVSDEF never do (checked) --
+// so (1) the block's altitudes come first, (2) the speed target of each of those altitudes
+// (atmosphere, CAS -> TAS, PerfModel.limits: the long part of a substep) is computed for the
+// whole block at once, kVB independent chains the compiler interleaves, and (3) the speed
+// and position chains run through the block with their targets known.  Every value is the
+// same expression in the same order as substep() evaluates it; only the schedule changes.
+// Speculated besides the conditions above: the CAS -> TAS polynomial's range, as before.
+// kVB: Descent 10 (its launch runs one wave per SIMD at most: registers are free); Vertical
+// 1 (its lookahead instance shares the kernel with the intruder substeps: 8 took it from 237
+// to 255 VGPRs, one wave per SIMD)
+#ifndef BSG_DESCENT_VB
+#define BSG_DESCENT_VB 10
+#endif
+template <int kVB>
 __device__ __forceinline__ bool vert_own_fast(AC& s, int S, double dt, Atmos* at_last,
                                               double* alt_last, int* why = nullptr) {
   const double allow_h = s.selalt > HMAX ? HMAX : s.selalt;
@@ -1766,9 +1783,12 @@ __device__ __forceinline__ bool vert_own_fast(AC& s, int S, double dt, Atmos* at
   ok = ok & (s.hdg >= 0.0) & (s.hdg < 360.0) & (fabs(s.ap_trk) < 360.0) &
        (bits(pymod360_s(s.ap_trk)) == bits(s.hdg));
   if (BSG_FAST_DEBUG && why && !ok) *why |= 2;
-  const AtmosK& k = khi ? kAtmosHMAX_K : kAtmosSL_K;
-  const LimK& lk = khi ? kLimHMAX : kLimSL;
-  const double tmmo = MMO * k.snd;
+  // the limit atmosphere's constants as selected values (a per-lane reference into constant
+  // memory would load them per use)
+  const double l_tvmin = khi ? kLimHMAX.tvmin : kLimSL.tvmin;
+  const double l_tvmax = khi ? kLimHMAX.tvmax : kLimSL.tvmax;
+  const double l_tvmax_gd = khi ? kLimHMAX.tvmax_gd : kLimSL.tvmax_gd;
+  const double tmmo = MMO * (khi ? kAtmosHMAX_K.snd : kAtmosSL_K.snd);
   // cas2tas_at's altitude-independent part (selspd is the CAS target: constant all step)
   const double z = 1.0 + divk_nn(RHO0 * s.selspd * s.selspd, 7.0 * P0);
   const double qdyn = P0 * (poly_3p5(z) - 1.0);
@@ -1776,90 +1796,128 @@ __device__ __forceinline__ bool vert_own_fast(AC& s, int S, double dt, Atmos* at
   ok = ok & in_3p5(z);
   const double ap_vs = fabs(s.selvs) > 0.1 ? s.selvs : APVSDEF;
   const double vs_cmd0 = fabs(ap_vs);
+  // the vertical-speed command without the speed chain: vs_max_with_acc never selected
+  ok = ok & !(vs_cmd0 > 0 && vs_cmd0 > VSMAX);
+  const double vs_cmd = (vs_cmd0 < 0 && vs_cmd0 < VSMIN) ? VSMIN : vs_cmd0;
   double shdg, chdg;
   sincos_t(s.hdg * kD2R, &shdg, &chdg);
   // the latitude's trig carried as substep() carries it (memo_init's seed, sincos_add)
   double latr = s.lat * kD2R;
   SinCos lsc = sincos_dd(latr);
   Atmos at = {0.0, 0.0, 0.0};
-  double h = s.alt;
-  // the on-target limits below are a pure function of (ap_tas, gd) there: kept while equal
-  // (an aircraft that reached the ground stays there with the same ap_tas)
-  uint64_t ot_key = kNoKey;
+  double h_last = s.alt;
+  uint64_t ot_key = kNoKey;         // the on-target limits' key (ap_tas bits, phase)
   bool ot_gd = false;
   double ot_tas = 0.0;
-  for (int it = 0; it < S; ++it) {
-    h = s.alt;
-    const bool gd = ground_phase(h);
-    const double axmax = gd ? AXMAX_GD : AXMAX;
-    // vatmos: the density-ratio polynomial (x stays in its range up to HMAX), times the
-    // stratosphere factor above 11 km (exactly vatmos' (1.225 * pow) * exp; * 1.0 below)
-    at.T = npmax(288.15 - 0.0065 * h, TSTRAT);
-    const double x = divk_nn(at.T, 288.15);
-    const double dhstrat = npmax(0.0, h - 11000.0);
-    // (x > 1: an aircraft a little below the ground within a step, the libm pow as vatmos)
-    double pt = poly_trop(x);
-    if (!in_trop(x)) pt = pow(x, 4.256848030018761);
-    double strat = 1.0;
-    if (dhstrat > 0.0) strat = exp(divk(-dhstrat, 6341.552161));
-    at.rho = 1.225 * pt * strat;
-    at.p = at.rho * RGAS * at.T;
-    // ap_tas = vcas2tas(selspd, h)
-    const double y = 1.0 + qdyn / at.p;
-    const double yp = poly_2o7(y);
-    if (BSG_FAST_DEBUG && why && !in_2o7(y)) *why |= 8;
-    ok = ok & in_2o7(y);
-    const double ap_tas = sqrt(7.0 * at.p / at.rho * (yp - 1.0));
-    // PerfModel.limits at the constant atmosphere (bsg_device.h LimK)
-    const double tvmin = gd ? 0.0 : lk.tvmin, tvmax = gd ? lk.tvmax_gd : lk.tvmax;
-    double allow_tas = ap_tas < tvmin ? tvmin : ap_tas;
-    allow_tas = ap_tas > tvmax ? tvmax : allow_tas;
-    if (allow_tas > tmmo) allow_tas = tmmo;
-    if (bits(h) == hb) {
-      // on its target altitude (a descent that reached the ground): substep()'s limits at
-      // the aircraft's own atmosphere, the CAS/TAS round trip
-      if (bits(ap_tas) != ot_key || gd != ot_gd) {
+  auto block = [&](auto nb_tag) {
+    constexpr int NB = decltype(nb_tag)::value;
+    // (1) the altitude / vertical-speed chain of the block
+    double hk[NB];
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      hk[i] = s.alt;                        // the substep's starting altitude
+      const double delta_alt = allow_h - s.alt;
+      const bool swaltsel = fabs(delta_alt) > npmax(10 * FT, fabs(2 * fabs(dt * s.vs)));
+      const double target_vs = sgnmul(swaltsel, delta_alt, fabs(vs_cmd));
+      const double delta_vs = target_vs - s.vs;
+      const bool need_az = fabs(delta_vs) > 300 * FPM;
+      const double az = sgnmul(need_az, delta_vs, 300 * FPM);
+      s.vs = need_az ? s.vs + az * dt : target_vs;
+      if (!isfinite(s.vs)) s.vs = 0.0;
+      s.alt = swaltsel ? divk(rint((s.alt + s.vs * dt) * 1e6), 1e6) : allow_h;
+    }
+    // (2) each substep's speed target from its altitude: independent chains.  Above 11 km
+    // (a climber) vatmos' stratosphere factor enters, below sea level (a descent reversed
+    // just above the ground overshoots it) the density ratio leaves the polynomial's range
+    // for the libm pow, as vatmos; a wave-uniform branch per block picks the chains with
+    // those branches, so the common block carries no per-chain branch
+    double allow[NB];
+    bool gdk[NB];
+    double ap_last = 0.0;
+    auto chains = [&](auto edge_tag) {
+      constexpr bool EDGE = decltype(edge_tag)::value;
+#pragma unroll
+      for (int i = 0; i < NB; ++i) {
+        const double h = hk[i];
+        const bool gd = ground_phase(h);
+        Atmos a;
+        a.T = npmax(288.15 - 0.0065 * h, TSTRAT);
+        const double x = divk_nn(a.T, 288.15);
+        double pt = poly_trop(x);
+        double strat = 1.0;
+        if constexpr (EDGE) {
+          if (!in_trop(x)) pt = pow(x, 4.256848030018761);
+          const double dhstrat = npmax(0.0, h - 11000.0);
+          if (dhstrat > 0.0) strat = exp(divk(-dhstrat, 6341.552161));
+        }
+        a.rho = 1.225 * pt * strat;         // vatmos: (1.225 * pow) * strat
+        a.p = a.rho * RGAS * a.T;
+        const double y = 1.0 + qdyn / a.p;
+        const double yp = poly_2o7(y);
+        const double ap_tas = sqrt(7.0 * a.p / a.rho * (yp - 1.0));
+        const double tvmin = gd ? 0.0 : l_tvmin, tvmax = gd ? l_tvmax_gd : l_tvmax;
+        double allow_tas = ap_tas < tvmin ? tvmin : ap_tas;
+        allow_tas = ap_tas > tvmax ? tvmax : allow_tas;
+        if (allow_tas > tmmo) allow_tas = tmmo;
+        allow[i] = allow_tas;
+        gdk[i] = gd;
+        const bool oki = (EDGE | in_trop(x)) & in_2o7(y);
+        if (BSG_FAST_DEBUG && why && !oki) *why |= in_trop(x) ? 8 : 32;
+        ok = ok & oki;
+        if (i == NB - 1) { at = a; h_last = h; ap_last = ap_tas; }
+      }
+    };
+    bool hi = false;
+#pragma unroll
+    for (int i = 0; i < NB; ++i) hi = hi | (hk[i] > 11000.0) | !(hk[i] >= 0.0);
+    if (__ballot(hi) != 0) chains(std::true_type{});
+    else chains(std::false_type{});
+    // on its target altitude (a descent that reached the ground): from that substep on the
+    // altitude stays there, so the block's last substep holds the one atmosphere and ap_tas
+    // involved; substep()'s limits at the aircraft's own atmosphere, the CAS/TAS round trip
+    // (a pure function of (ap_tas, gd) there: computed once while they stay the same, as
+    // substep()'s memo keeps it -- an aircraft on the ground sits there all step)
+    if (bits(h_last) == hb) {
+      const bool gd = gdk[NB - 1];
+      if (bits(ap_last) != ot_key || gd != ot_gd) {
         const double vmin = gd ? 0.0 : VMIN_CAS, vmax = gd ? VMAX_GD : VMAX_CAS;
-        const double intent_cas = tas2cas_at(ap_tas, at);
+        const double intent_cas = tas2cas_at(ap_last, at);
         double allow_cas = intent_cas < vmin ? vmin : intent_cas;
         allow_cas = intent_cas > vmax ? vmax : allow_cas;
         ot_tas = cas2tas_at(allow_cas, at);
         const double snd_h = sound_at(at);
         if (ot_tas / snd_h > MMO) ot_tas = MMO * snd_h;
-        ot_key = bits(ap_tas);
+        ot_key = bits(ap_last);
         ot_gd = gd;
       }
-      allow_tas = ot_tas;
+#pragma unroll
+      for (int i = 0; i < NB; ++i)
+        if (bits(hk[i]) == hb) allow[i] = ot_tas;
     }
-    const double vs_max_with_acc = (1 - s.ax * (gd ? 1.0 / AXMAX_GD : 1.0 / AXMAX)) * VSMAX;
-    double vs_cmd = (vs_cmd0 > 0 && vs_cmd0 > VSMAX) ? vs_max_with_acc : vs_cmd0;
-    vs_cmd = (vs_cmd0 < 0 && vs_cmd0 < VSMIN) ? VSMIN : vs_cmd;
-    // update_airspeed
-    const double delta_spd = allow_tas - s.tas;
-    const bool need_ax = fabs(delta_spd) > fabs(dt * axmax);
-    s.ax = sgnmul(need_ax, delta_spd, axmax);
-    s.tas = need_ax ? s.tas + s.ax * dt : allow_tas;
-    // (heading on its command: unchanged)  vertical speed
-    const double delta_alt = allow_h - s.alt;
-    const bool swaltsel = fabs(delta_alt) > npmax(10 * FT, fabs(2 * fabs(dt * s.vs)));
-    const double target_vs = sgnmul(swaltsel, delta_alt, fabs(vs_cmd));
-    const double delta_vs = target_vs - s.vs;
-    const bool need_az = fabs(delta_vs) > 300 * FPM;
-    const double az = sgnmul(need_az, delta_vs, 300 * FPM);
-    s.vs = need_az ? s.vs + az * dt : target_vs;
-    if (!isfinite(s.vs)) s.vs = 0.0;
-    // update_groundspeed + update_pos
-    const double gsnorth = s.tas * chdg;
-    const double gseast = s.tas * shdg;
-    s.alt = swaltsel ? divk(rint((s.alt + s.vs * dt) * 1e6), 1e6) : allow_h;
-    s.lat = s.lat + divk_f(dt * gsnorth, Rearth) * kR2D;
-    const double nlr = s.lat * kD2R;
-    sincos_add(lsc, nlr - latr);
-    latr = nlr;
-    s.lon = s.lon + divk_f(dt * gseast / lsc.c, Rearth) * kR2D;
-  }
+    // (3) the speed and position chains through the block
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const double axmax = gdk[i] ? AXMAX_GD : AXMAX;
+      // update_airspeed
+      const double delta_spd = allow[i] - s.tas;
+      const bool need_ax = fabs(delta_spd) > fabs(dt * axmax);
+      s.ax = sgnmul(need_ax, delta_spd, axmax);
+      s.tas = need_ax ? s.tas + s.ax * dt : allow[i];
+      // (heading on its command: unchanged)  update_groundspeed + update_pos
+      const double gsnorth = s.tas * chdg;
+      const double gseast = s.tas * shdg;
+      s.lat = s.lat + divk_f(dt * gsnorth, Rearth) * kR2D;
+      const double nlr = s.lat * kD2R;
+      sincos_add(lsc, nlr - latr);
+      latr = nlr;
+      s.lon = s.lon + divk_f(dt * gseast / lsc.c, Rearth) * kR2D;
+    }
+  };
+  int it = 0;
+  for (; it + kVB <= S; it += kVB) block(std::integral_constant<int, kVB>{});
+  for (; it < S; ++it) block(std::integral_constant<int, 1>{});
   *at_last = at;
-  *alt_last = h;                    // the altitude `at` belongs to (the last substep's start)
+  *alt_last = h_last;               // the altitude `at` belongs to (the last substep's start)
   return ok & (S > 0);
 }
 
@@ -2001,7 +2059,8 @@ __device__ __forceinline__ void propagate(const KParams& p, int e, int j, size_t
 #define BSG_FAST_ALWAYS 0                 // experiment builds: take the fast loop's result even
 #endif                                    // where its speculation failed (timing only)
       int why = 0;
-      fast_ok = vert_own_fast(s, S, p.cfg.simdt, &at, &alt_last, &why) || BSG_FAST_ALWAYS;
+      fast_ok = vert_own_fast<KIND == BSG_ENV_DESCENT ? BSG_DESCENT_VB : 1>(s, S, p.cfg.simdt, &at, &alt_last, &why) ||
+                BSG_FAST_ALWAYS;
       if (BSG_FAST_DEBUG && p.b.ep_info) p.b.ep_info[(size_t)e * 4 + 3] = (double)why;
       if (fast_ok) {
         s.cas = tas2cas_at(s.tas, at);     // memo_final_cas: the last substep's atmosphere

@@ -107,3 +107,37 @@ def test_merge_ownship_fastpath_bit_identical(memo):
         _same(_snap(gen), _snap(fast), t)
         ends += int((gen.terminated | gen.truncated).sum())
     assert ends >= 2 * E
+
+
+def test_descent_fastpath_edges_bit_identical():
+    """vert_own_fast's blocks (three passes per 10 substeps) at the edges its chains handle
+    by a wave-uniform slow variant or a cached branch: a dive reversed just above the ground
+    (the altitude overshoots below sea level: the libm pow of vatmos), a climber crossing
+    11 km (the stratosphere factor), an aircraft on the ground under a descend command (the
+    on-target limits), mixed in every wave with ordinary lanes -- against substep() alone."""
+    from bluesky_gym import config
+    cfg = config.descent_config(max_episode_steps=300)
+    E = 256
+    gen, fast = _batch(cfg, E, True, 2, False), _batch(cfg, E, False, 2, False)
+    gen.reset()
+    fast.reset()
+    lane = torch.arange(E, device="cuda") % 4
+    for b in (gen, fast):
+        st = b.state
+        st["alt"][:, 0] = torch.where(lane == 0, 22.0, torch.where(lane == 1, 10950.0,
+                                      torch.where(lane == 2, 0.0, st["alt"][:, 0])))
+        st["vs"][:, 0] = torch.where(lane == 0, -12.0, torch.where(lane == 1, 12.0,
+                                     torch.where(lane == 2, 0.0, st["vs"][:, 0])))
+        st["selalt"][:, 0] = torch.where(lane == 1, 1e6, torch.where(lane == 3, st["selalt"][:, 0], 0.0))
+        b.invalidate_caches()
+    g = torch.Generator(device="cuda").manual_seed(9)
+    for t in range(6):
+        a = torch.rand((E, 1), dtype=torch.float64, device="cuda", generator=g) * 2 - 1
+        a[lane == 0] = 1.0 if t == 0 else a[lane == 0]       # reverse the dive at 22 m
+        a[lane == 1] = 1.0                                    # keep climbing through 11 km
+        a[lane == 2] = -1.0                                   # stay on the ground
+        gen.step(a)
+        fast.step(a)
+        _same(_snap(gen), _snap(fast), t)
+    alt = fast.state["alt"][:, 0]
+    assert bool((alt[lane == 1] > 11000.0).all())
