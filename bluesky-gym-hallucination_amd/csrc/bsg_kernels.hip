@@ -1921,6 +1921,245 @@ __device__ __forceinline__ bool vert_own_fast(AC& s, int S, double dt, Atmos* at
   return ok & (S > 0);
 }
 
+// ---- Descent: vert_own_fast's three passes on seven waves of one workgroup ------------
+// DescentEnv's launch is 64 waves on 1,024 SIMDs: each ownship's 30 substeps ran on one
+// wave, alone on its SIMD, and phase A was that wave's chain.  vert_own_fast's passes are
+// independent across blocks (block k's altitude chain, block k-1's speed targets, block k-2's
+// speed / position chain), so step_kernel<DESCENT> runs with kDC_W = 7 waves per workgroup
+// (CDW, the workgroup's 64 envs unchanged; the extra waves idle after phase A) and hands the
+// passes out: wave 0 the altitude chains, waves 1-5 the speed-target chains (two of each
+// block of 10 substeps per wave), wave 6 the speed / position chain -- a five-stage pipeline
+// over the three blocks, LDS between the stages, one workgroup barrier per stage (every wave
+// passes every barrier: the roles are wave-uniform branches between them).  Each value is
+// computed by the expression vert_own_fast uses, in the same order: bit-identical
+// (tests/test_gpu_fastpath.py).  Block size and target waves were measured
+// (profiles/r05/descent_blocks/): (10 substeps, 2 target waves) 24.3 us per 4,096-env step,
+// (5, 2) 26.8, (3, 3) 21.6, (5, 5) 21.3, (10, 5) 20.9, (6, 6) 20.8, (10, 6) 21.0, (15, 5)
+// 22.0; one wave (vert_own_fast) 35.8, round 4's loop 40.2.
+struct DescentCoop {
+  bool valid, ok;
+  double alt, vs, tas, ax, lat, lon, alt_last;
+  Atmos at;
+};
+#ifndef BSG_DC_NB
+#define BSG_DC_NB 10                         // substeps per block
+#endif
+#ifndef BSG_DC_P2W
+#define BSG_DC_P2W 5                         // waves on the speed-target chains
+#endif
+constexpr int kDC_S = 30, kDC_NB = BSG_DC_NB, kDC_NBLK = kDC_S / kDC_NB, kDC_P2W = BSG_DC_P2W;
+constexpr int kDC_W = kDC_P2W + 2;           // waves per workgroup
+static_assert(kDC_S % kDC_NB == 0, "blocks must tile the step");
+struct DescentLds {
+  double hk[kDC_S][64], allow[kDC_S][64];
+  double qdyn[64], tvmin[64], tvmax[64], tvmax_gd[64], tmmo[64], allow_h[64];
+  double tas[64], lat[64], lon[64], chdg[64], shdg[64];
+  double at_p[kDC_NBLK][64], at_rho[kDC_NBLK][64], at_T[kDC_NBLK][64], ap_last[kDC_NBLK][64];
+  double o_tas[64], o_ax[64], o_lat[64], o_lon[64];
+  unsigned char gd[kDC_S][64];
+  unsigned char fail[kDC_P2W][64];
+};
+
+// wv: this thread's wave (0 .. kDC_W - 1); lane: its lane = its env's slot in the
+// workgroup.  Wave 0 passes `elig` (the env steps this launch), its loaded state and its
+// action row; waves 1 .. kDC_P2W run the speed-target chains (substep i of a block on wave
+// 1 + i % kDC_P2W), wave kDC_W - 1 the speed / position chain.
+__device__ __forceinline__ void descent_coop(const KParams& p, int wv, int lane, bool elig,
+                                             const AC& s_in, const double act[2],
+                                             DescentCoop& out) {
+  __shared__ DescentLds D;
+  const double dt = p.cfg.simdt;
+  const bool w_alt = wv == 0, w_spd = wv == kDC_W - 1, w_tgt = !w_alt && !w_spd;
+  const int w2 = wv - 1;                    // (w_tgt) this wave's chain slot
+  // --- wave 0: the action (descent_env.py:155-160), the speculation's conditions, the
+  // altitude-independent terms
+  AC s = s_in;
+  bool ok = false;
+  double vs_cmd = 0.0, allow_h = 0.0;
+  if (w_alt) {
+    const double act0 = act[0] * 12.5;
+    if (act0 >= 0) { s.selalt = 1000000; s.selvs = act0; }
+    else if (act0 < 0) { s.selalt = 0; s.selvs = act0; }
+    allow_h = s.selalt > HMAX ? HMAX : s.selalt;
+    const bool khi = bits(allow_h) == bits(HMAX);
+    ok = elig & ((s.nav & 1) == 0) & (khi | (allow_h == 0.0)) & (fabs(s.selspd) >= 2.0);
+    ok = ok & (s.hdg >= 0.0) & (s.hdg < 360.0) & (fabs(s.ap_trk) < 360.0) &
+         (bits(pymod360_s(s.ap_trk)) == bits(s.hdg));
+    const double z = 1.0 + divk_nn(RHO0 * s.selspd * s.selspd, 7.0 * P0);
+    D.qdyn[lane] = P0 * (poly_3p5(z) - 1.0);
+    ok = ok & in_3p5(z);
+    D.tvmin[lane] = khi ? kLimHMAX.tvmin : kLimSL.tvmin;
+    D.tvmax[lane] = khi ? kLimHMAX.tvmax : kLimSL.tvmax;
+    D.tvmax_gd[lane] = khi ? kLimHMAX.tvmax_gd : kLimSL.tvmax_gd;
+    D.tmmo[lane] = MMO * (khi ? kAtmosHMAX_K.snd : kAtmosSL_K.snd);
+    D.allow_h[lane] = allow_h;
+    const double ap_vs = fabs(s.selvs) > 0.1 ? s.selvs : APVSDEF;
+    const double vs_cmd0 = fabs(ap_vs);
+    ok = ok & !(vs_cmd0 > 0 && vs_cmd0 > VSMAX);
+    vs_cmd = (vs_cmd0 < 0 && vs_cmd0 < VSMIN) ? VSMIN : vs_cmd0;
+    double shdg, chdg;
+    sincos_t(s.hdg * kD2R, &shdg, &chdg);
+    D.tas[lane] = s.tas; D.lat[lane] = s.lat; D.lon[lane] = s.lon;
+    D.chdg[lane] = chdg; D.shdg[lane] = shdg;
+  }
+  auto pass1 = [&](int k) {                 // wave 0: block k's altitude / vs chain
+#pragma unroll
+    for (int i = 0; i < kDC_NB; ++i) {
+      D.hk[k * kDC_NB + i][lane] = s.alt;
+      const double delta_alt = allow_h - s.alt;
+      const bool swaltsel = fabs(delta_alt) > npmax(10 * FT, fabs(2 * fabs(dt * s.vs)));
+      const double target_vs = sgnmul(swaltsel, delta_alt, fabs(vs_cmd));
+      const double delta_vs = target_vs - s.vs;
+      const bool need_az = fabs(delta_vs) > 300 * FPM;
+      const double az = sgnmul(need_az, delta_vs, 300 * FPM);
+      s.vs = need_az ? s.vs + az * dt : target_vs;
+      if (!isfinite(s.vs)) s.vs = 0.0;
+      s.alt = swaltsel ? divk(rint((s.alt + s.vs * dt) * 1e6), 1e6) : allow_h;
+    }
+  };
+  // --- the target waves: block k's substeps w2, w2 + kDC_P2W, ...
+  constexpr int kC = (kDC_NB + kDC_P2W - 1) / kDC_P2W;
+  bool fail = false;
+  double qdyn = 0.0, l_tvmin = 0.0, l_tvmax = 0.0, l_tvmax_gd = 0.0, tmmo = 0.0;
+  auto pass2 = [&](int k) {
+    auto chains = [&](auto edge_tag) {
+      constexpr bool EDGE = decltype(edge_tag)::value;
+#pragma unroll
+      for (int m = 0; m < kC; ++m) {
+        const int i = w2 + m * kDC_P2W;
+        if ((kDC_NB % kDC_P2W) != 0 && i >= kDC_NB) break;      // (wave-uniform)
+        const int ik = k * kDC_NB + i;
+        const double h = D.hk[ik][lane];
+        const bool gd = ground_phase(h);
+        Atmos a;
+        a.T = npmax(288.15 - 0.0065 * h, TSTRAT);
+        const double x = divk_nn(a.T, 288.15);
+        double pt = poly_trop(x);
+        double strat = 1.0;
+        if constexpr (EDGE) {
+          if (!in_trop(x)) pt = pow(x, 4.256848030018761);
+          const double dhstrat = npmax(0.0, h - 11000.0);
+          if (dhstrat > 0.0) strat = exp(divk(-dhstrat, 6341.552161));
+        }
+        a.rho = 1.225 * pt * strat;         // vatmos: (1.225 * pow) * strat
+        a.p = a.rho * RGAS * a.T;
+        const double y = 1.0 + qdyn / a.p;
+        const double yp = poly_2o7(y);
+        const double ap_tas = sqrt(7.0 * a.p / a.rho * (yp - 1.0));
+        const double tvmin = gd ? 0.0 : l_tvmin, tvmax = gd ? l_tvmax_gd : l_tvmax;
+        double allow_tas = ap_tas < tvmin ? tvmin : ap_tas;
+        allow_tas = ap_tas > tvmax ? tvmax : allow_tas;
+        if (allow_tas > tmmo) allow_tas = tmmo;
+        D.allow[ik][lane] = allow_tas;
+        D.gd[ik][lane] = gd ? 1 : 0;
+        fail = fail | !((EDGE | in_trop(x)) & in_2o7(y));
+        if (i == kDC_NB - 1) {              // the block's last substep: its atmosphere, ap_tas
+          D.at_p[k][lane] = a.p; D.at_rho[k][lane] = a.rho; D.at_T[k][lane] = a.T;
+          D.ap_last[k][lane] = ap_tas;
+        }
+      }
+    };
+    bool edge = false;
+#pragma unroll
+    for (int m = 0; m < kC; ++m) {
+      const int i = w2 + m * kDC_P2W;
+      if ((kDC_NB % kDC_P2W) != 0 && i >= kDC_NB) break;
+      const double h = D.hk[k * kDC_NB + i][lane];
+      edge = edge | (h > 11000.0) | !(h >= 0.0);
+    }
+    if (__ballot(edge) != 0) chains(std::true_type{});
+    else chains(std::false_type{});
+  };
+  // --- the last wave: the speed / position chain, the on-target limits (as vert_own_fast)
+  double tas = 0.0, ax = 0.0, lat = 0.0, lon = 0.0, chdg = 0.0, shdg = 0.0, latr = 0.0;
+  SinCos lsc = {0.0, 0.0, 1.0, 0.0};
+  uint64_t ot_key = kNoKey, hb = 0;
+  bool ot_gd = false;
+  double ot_tas = 0.0;
+  auto pass3 = [&](int k) {
+    const int i0 = k * kDC_NB;
+    double allow[kDC_NB];
+#pragma unroll
+    for (int i = 0; i < kDC_NB; ++i) allow[i] = D.allow[i0 + i][lane];
+    if (bits(D.hk[i0 + kDC_NB - 1][lane]) == hb) {
+      const bool gd = D.gd[i0 + kDC_NB - 1][lane] != 0;
+      const double ap_last = D.ap_last[k][lane];
+      if (bits(ap_last) != ot_key || gd != ot_gd) {
+        const Atmos a = {D.at_p[k][lane], D.at_rho[k][lane], D.at_T[k][lane]};
+        const double vmin = gd ? 0.0 : VMIN_CAS, vmax = gd ? VMAX_GD : VMAX_CAS;
+        const double intent_cas = tas2cas_at(ap_last, a);
+        double allow_cas = intent_cas < vmin ? vmin : intent_cas;
+        allow_cas = intent_cas > vmax ? vmax : allow_cas;
+        ot_tas = cas2tas_at(allow_cas, a);
+        const double snd_h = sound_at(a);
+        if (ot_tas / snd_h > MMO) ot_tas = MMO * snd_h;
+        ot_key = bits(ap_last);
+        ot_gd = gd;
+      }
+#pragma unroll
+      for (int i = 0; i < kDC_NB; ++i)
+        if (bits(D.hk[i0 + i][lane]) == hb) allow[i] = ot_tas;
+    }
+#pragma unroll
+    for (int i = 0; i < kDC_NB; ++i) {
+      const double axmax = D.gd[i0 + i][lane] ? AXMAX_GD : AXMAX;
+      const double delta_spd = allow[i] - tas;
+      const bool need_ax = fabs(delta_spd) > fabs(dt * axmax);
+      ax = sgnmul(need_ax, delta_spd, axmax);
+      tas = need_ax ? tas + ax * dt : allow[i];
+      const double gsnorth = tas * chdg;
+      const double gseast = tas * shdg;
+      lat = lat + divk_f(dt * gsnorth, Rearth) * kR2D;
+      const double nlr = lat * kD2R;
+      sincos_add(lsc, nlr - latr);
+      latr = nlr;
+      lon = lon + divk_f(dt * gseast / lsc.c, Rearth) * kR2D;
+    }
+  };
+  // --- the pipeline: stage t runs pass1(t) (wave 0), pass2(t - 1) (the target waves) and
+  // pass3(t - 2) (the last wave); one barrier after each stage, passed by every wave
+#pragma unroll
+  for (int t = 0; t < kDC_NBLK + 2; ++t) {
+    if (t == 1) {                           // wave 0's inputs are in LDS from stage 0 on
+      if (w_tgt) {
+        qdyn = D.qdyn[lane]; l_tvmin = D.tvmin[lane]; l_tvmax = D.tvmax[lane];
+        l_tvmax_gd = D.tvmax_gd[lane]; tmmo = D.tmmo[lane];
+      } else if (w_spd) {
+        tas = D.tas[lane]; lat = D.lat[lane]; lon = D.lon[lane];
+        chdg = D.chdg[lane]; shdg = D.shdg[lane];
+        hb = bits(D.allow_h[lane]);
+        latr = lat * kD2R;
+        lsc = sincos_dd(latr);
+      }
+    }
+    if (w_alt) {
+      if (t < kDC_NBLK) pass1(t);
+    } else if (w_tgt) {
+      if (t >= 1 && t <= kDC_NBLK) pass2(t - 1);
+    } else {
+      if (t >= 2) pass3(t - 2);
+    }
+    __syncthreads();
+  }
+  if (w_spd) { D.o_tas[lane] = tas; D.o_ax[lane] = ax; D.o_lat[lane] = lat; D.o_lon[lane] = lon; }
+  else if (w_tgt) D.fail[w2][lane] = fail ? 1 : 0;
+  __syncthreads();
+  if (w_alt) {
+    bool f = false;
+#pragma unroll
+    for (int w = 0; w < kDC_P2W; ++w) f = f | (D.fail[w][lane] != 0);
+    out.valid = elig;
+    out.ok = ok & !f;
+    out.alt = s.alt;
+    out.vs = s.vs;
+    out.tas = D.o_tas[lane]; out.ax = D.o_ax[lane];
+    out.lat = D.o_lat[lane]; out.lon = D.o_lon[lane];
+    out.alt_last = D.hk[kDC_S - 1][lane];
+    out.at = Atmos{D.at_p[kDC_NBLK - 1][lane], D.at_rho[kDC_NBLK - 1][lane],
+                   D.at_T[kDC_NBLK - 1][lane]};
+  }
+}
+
 // ---- Merge ownship with the lookahead on: the substep loop for level HDG/SPD flight ------
 // With the lookahead (C4's per-GPU shards) a main wave propagates only its two ownships, and
 // their ten substeps were ~40 k of the main wave's ~58 k cycles at 512 envs
@@ -2022,7 +2261,8 @@ __device__ __forceinline__ void propagate(const KParams& p, int e, int j, size_t
                                           EnvScalars& ev, double& sub_reward, bool& sub_done,
                                           const double act[2], const double mc[MC_FIELDS],
                                           const double oat[4], double* mcache,
-                                          bool spawned = false) {
+                                          bool spawned = false,
+                                          const DescentCoop* coop = nullptr) {
   const Buffers& b = p.b;
   const int N = p.N;
   const AC s0 = s;                  // as loaded: the cross-step memo's keys (memo_load)
@@ -2059,8 +2299,20 @@ __device__ __forceinline__ void propagate(const KParams& p, int e, int j, size_t
 #define BSG_FAST_ALWAYS 0                 // experiment builds: take the fast loop's result even
 #endif                                    // where its speculation failed (timing only)
       int why = 0;
-      fast_ok = vert_own_fast<KIND == BSG_ENV_DESCENT ? BSG_DESCENT_VB : 1>(s, S, p.cfg.simdt, &at, &alt_last, &why) ||
-                BSG_FAST_ALWAYS;
+      if (coop && coop->valid) {
+        // step_kernel<DESCENT, 1, false, kDC_W> ran the loop on kDC_W waves (descent_coop)
+        fast_ok = coop->ok;
+        if (fast_ok) {
+          s.alt = coop->alt; s.vs = coop->vs; s.tas = coop->tas; s.ax = coop->ax;
+          s.lat = coop->lat; s.lon = coop->lon;
+          at = coop->at;
+          alt_last = coop->alt_last;
+        }
+      } else {
+        fast_ok = vert_own_fast<KIND == BSG_ENV_DESCENT ? BSG_DESCENT_VB : 1>(s, S, p.cfg.simdt, &at,
+                                                                             &alt_last, &why) ||
+                  BSG_FAST_ALWAYS;
+      }
       if (BSG_FAST_DEBUG && p.b.ep_info) p.b.ep_info[(size_t)e * 4 + 3] = (double)why;
       if (fast_ok) {
         s.cas = tas2cas_at(s.tas, at);     // memo_final_cas: the last substep's atmosphere
@@ -2659,6 +2911,13 @@ __global__ __launch_bounds__(64 * CDW) BSG_WPE void step_kernel(KParams p) {
   }
   const bool stepping = env_ok && p.mode == MODE_STEP && !resetting;
   const bool active = resetting || stepping;   // env produces outputs this launch
+  // Descent on kDC_W waves: the ownships' substep loop as a pipeline (descent_coop); every
+  // wave of the workgroup enters (uniform condition), wave 0 keeps the results
+  DescentCoop dco{};
+  if constexpr (KIND == BSG_ENV_DESCENT && CDW == kDC_W && !WIND) {
+    if (p.mode == MODE_STEP && p.cfg.action_frequency == kDC_S && !p.no_fastpath)
+      descent_coop(p, wv, lane, stepping && ok && !BSG_FAST_DEBUG, s_in, act, dco);
+  }
 
   // ---------------- A: spawn or propagate, store state ------------------------------
   double sub_reward = 0.0;          // StaticObstacle: reward / done of the last substep
@@ -2707,7 +2966,8 @@ __global__ __launch_bounds__(64 * CDW) BSG_WPE void step_kernel(KParams p) {
 #if defined(BSG_EXP_NOOWN) && BSG_EXP_NOOWN
           if (j > 0)   // timing experiment only: the ownship does not move (wrong results)
 #endif
-          propagate<KIND, WIND, false, LAK>(p, e, j, a, s, ev, sub_reward, sub_done, act, mc, oat, mcache);
+          propagate<KIND, WIND, false, LAK>(p, e, j, a, s, ev, sub_reward, sub_done, act, mc, oat, mcache,
+                                            false, KIND == BSG_ENV_DESCENT ? &dco : nullptr);
         }
       }
       if (active) store_ac_changed<WIND>(b, a, s, s_in);
@@ -3072,8 +3332,12 @@ static hipError_t launch_kind_w(const KParams& p0, hipStream_t st) {
     }
 #undef BSG_CASE_CD
   }
-  if constexpr (KIND == BSG_ENV_DESCENT || KIND == BSG_ENV_STATIC_OBSTACLE ||
-                KIND == BSG_ENV_PLAN_WAYPOINT) {
+  if constexpr (KIND == BSG_ENV_DESCENT && !WIND) {
+    // kDC_W waves per workgroup: the ownships' substep loop pipelined over them (descent_coop)
+    if (gs != 1) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((step_kernel<KIND, 1, WIND, kDC_W>), dim3(grid), dim3(64 * kDC_W), p.lds_pad, st, p);
+  } else if constexpr (KIND == BSG_ENV_DESCENT || KIND == BSG_ENV_STATIC_OBSTACLE ||
+                       KIND == BSG_ENV_PLAN_WAYPOINT) {
     switch (gs) { BSG_CASE(1) default: return hipErrorInvalidValue; }        // one aircraft
   } else if constexpr (KIND == BSG_ENV_SECTOR_CR) {
     switch (gs) { BSG_CASE(8) BSG_CASE(16) BSG_CASE(32) BSG_CASE(64) default: return hipErrorInvalidValue; }
