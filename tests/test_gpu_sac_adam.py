@@ -205,8 +205,8 @@ def test_squashed_gaussian_matches_autograd():
         assert l1.grad[0, 0] == 0 and l1.grad[1, 0] == 0
 
 
-def _sac_pair(cls, obs_dim, act_dim, dev):
-    s = cls(obs_dim, act_dim, dev, seed=7, lr=1e-3, buffer=4096)
+def _sac_pair(cls, obs_dim, act_dim, dev, **kw):
+    s = cls(obs_dim, act_dim, dev, seed=7, lr=1e-3, buffer=4096, **kw)
     assert s.hip_adam and s.actor.fused_dist
     gen = torch.Generator(device=dev).manual_seed(11)
     n = 1024
@@ -223,7 +223,8 @@ def _sac_pair(cls, obs_dim, act_dim, dev):
 def test_fused_sac_update_matches_autograd_update(obs_dim, act_dim):
     """FusedSAC (tools/sac_fused.hip: the forward / backward written out, rocBLAS for the
     256 x 256 products) against SAC.update on the autograd + HipAdam path: same seed, same
-    buffer, same RNG draws.  (1) The first update's gradients of every parameter and of
+    buffer, same RNG draws (FusedSAC's noise="torch": torch.rand / torch.randn in SAC.update's
+    order; the default Philox draws are checked below).  (1) The first update's gradients of every parameter and of
     log_alpha within 1e-4 of the tensor's largest gradient (the column sums and bias adds
     associate differently from autograd's).  (2) After 10 updates every parameter, target
     parameter and log_alpha within 1e-4 relative + 1e-4 absolute -- a tenth of one Adam step
@@ -232,8 +233,8 @@ def test_fused_sac_update_matches_autograd_update(obs_dim, act_dim):
     Descent's shape (obs 4, action 1) and Merge's (obs 40, action 2)."""
     dev = torch.device("cuda", 0)
     grads, out, losses = [], [], []
-    for cls in (sac_torch.SAC, sac_torch.FusedSAC):
-        s = _sac_pair(cls, obs_dim, act_dim, dev)
+    for cls, kw in ((sac_torch.SAC, {}), (sac_torch.FusedSAC, {"noise": "torch"})):
+        s = _sac_pair(cls, obs_dim, act_dim, dev, **kw)
         params = list(s.actor.parameters()) + list(s.q.parameters()) + [s.log_alpha]
         torch.manual_seed(5)
         s.update()
@@ -275,3 +276,35 @@ def test_fused_sac_loop_is_graph_capturable():
     lq, la = s.update()
     assert np.isfinite(float(lq)) and np.isfinite(float(la))
     assert not torch.equal(w0, s.actor.latent[2].weight.detach())
+
+
+def test_fused_sac_philox_noise():
+    """FusedSAC's default noise (tools/sac_fused.hip noise_kernel: Philox4x32-10, one launch
+    per update for the replay uniforms, the squashed Gaussian's normals and an attached
+    action sample's): the right distributions (moments over many draws), new numbers every
+    update (the launch counter advances on the device, so graph replays draw anew), and the
+    same numbers for the same seed."""
+    dev = torch.device("cuda", 0)
+    draws = []
+    for rep in range(2):
+        s = _sac_pair(sac_torch.FusedSAC, 40, 2, dev)
+        assert s.noise == "philox"
+        pe = torch.zeros((4096, 2), dtype=torch.float32, device=dev)
+        s.attach_policy_noise(pe)
+        us, es, ps = [], [], []
+        for _ in range(20):
+            s.update(losses=False)
+            us.append(s._u.clone())
+            es.append(s._eps.clone())
+            ps.append(pe.clone())
+        torch.cuda.synchronize()
+        draws.append((torch.stack(us), torch.stack(es), torch.stack(ps)))
+    (u, e, pn), (u2, e2, pn2) = draws
+    assert torch.equal(u, u2) and torch.equal(e, e2) and torch.equal(pn, pn2)
+    assert not torch.equal(u[0], u[1]) and not torch.equal(pn[0], pn[1])
+    assert float(u.min()) >= 0.0 and float(u.max()) < 1.0
+    assert abs(float(u.mean()) - 0.5) < 0.01 and abs(float(u.var()) - 1 / 12) < 0.005
+    n = torch.cat([e.flatten(), pn.flatten()]).double()
+    assert abs(float(n.mean())) < 0.01 and abs(float(n.std()) - 1.0) < 0.01
+    assert abs(float(((n - n.mean()) ** 3).mean())) < 0.03              # skew
+    assert abs(float(((n - n.mean()) ** 4).mean()) - 3.0) < 0.1         # kurtosis

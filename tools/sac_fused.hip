@@ -9,7 +9,10 @@
 // between two GEMMs is one of the kernels below, so an update is ~30 launches:
 //
 //   in_layer     relu(x W + b) for a layer whose K is the observation (+ action) width
-//   actor_head   h1 = relu(p1 + b1), mu / log_std heads, SB3's squashed Gaussian (a, logp)
+//   in_layer_pair  the actor's and the online critics' first layers in one launch
+//   noise        the update's uniforms and normals (and the next action sample's), Philox
+//   actor_head   h1 = relu(p1 + b1), mu / log_std heads, SB3's squashed Gaussian (a, logp),
+//                and on the next-observation rows the target critics' first layer
 //   critic_head  g1 = relu(p1 + b1), q = g1 w2 + b2 for both critics, then per mode the TD
 //                target y, the twin-MSE gradient dq, or the actor loss's dq / dlogp
 //   td_critic_head  the target critics and the online critics of one [4, B, H] product: y,
@@ -66,16 +69,101 @@ __global__ __launch_bounds__(256) void in_layer_kernel(
   out[((size_t)c * R + r) * H + u] = z > 0.0f ? z : 0.0f;
 }
 
+// two first layers in one launch: blockIdx.y == 0 the actor's (rows xa / xa_hi, torch
+// Linear layout), y = 1, 2 the online critics' on [ya | yb] (rows < R2, critic layout) --
+// in_layer's sums, k in order
+__global__ __launch_bounds__(256) void in_layer_pair_kernel(
+    const float* __restrict__ xa, const float* __restrict__ xa_hi, int split, int lda, int Ka,
+    int R1, const float* __restrict__ w1, const float* __restrict__ b1, float* __restrict__ out1,
+    const float* __restrict__ ya, int ldya, int Kya, const float* __restrict__ yb, int ldyb,
+    int Kyb, int R2, const float* __restrict__ w2, const float* __restrict__ b2,
+    float* __restrict__ out2) {
+  const int u = threadIdx.x;
+  const int r = blockIdx.x;
+  if (blockIdx.y == 0) {
+    if (r >= R1) return;
+    const float* xr = r < split ? xa + (size_t)r * lda : xa_hi + (size_t)(r - split) * lda;
+    float acc = 0.0f;
+    for (int k = 0; k < Ka; ++k) acc += xr[k] * w1[(size_t)u * Ka + k];
+    const float z = acc + b1[u];
+    out1[(size_t)r * H + u] = z > 0.0f ? z : 0.0f;
+  } else {
+    const int c = blockIdx.y - 1;
+    if (r >= R2) return;
+    const int K = Kya + Kyb;
+    float acc = 0.0f;
+    for (int k = 0; k < K; ++k) {
+      const float xv = k < Kya ? ya[(size_t)r * ldya + k] : yb[(size_t)r * ldyb + (k - Kya)];
+      acc += xv * w2[((size_t)c * K + k) * H + u];
+    }
+    const float z = acc + b2[(size_t)c * H + u];
+    out2[((size_t)c * R2 + r) * H + u] = z > 0.0f ? z : 0.0f;
+  }
+}
+
+// the update's random numbers in one launch, Philox4x32-10 (Salmon et al. 2011) keyed by
+// seed, counter = (launch number, element): u ~ U[0, 1) for the replay sample, the squashed
+// Gaussian's eps ~ N(0, 1) (Box-Muller) for the update and for the next vector step's action
+// sample.  One workgroup; its thread 0 advances the launch number after every thread has
+// read it, so replays of a captured graph draw new numbers.
+__device__ __forceinline__ void philox10(uint32_t c[4], uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c[0];
+    const uint64_t p1 = (uint64_t)0xCD9E8D57u * c[2];
+    const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c[1] ^ k0;
+    const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c[3] ^ k1;
+    c[1] = (uint32_t)p1;
+    c[3] = (uint32_t)p0;
+    c[0] = n0;
+    c[2] = n2;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+}
+__device__ __forceinline__ float u01(uint32_t x) { return (float)(x >> 8) * (1.0f / 16777216.0f); }
+
+__global__ __launch_bounds__(1024) void noise_kernel(unsigned long long* __restrict__ launch,
+                                                     unsigned long long seed,
+                                                     float* __restrict__ u, int nu,
+                                                     float* __restrict__ e1, int n1,
+                                                     float* __restrict__ e2, int n2) {
+  const unsigned long long L = launch[0];
+  const int total = nu + n1 + n2;
+  for (int i = threadIdx.x; 2 * i < total + 1; i += blockDim.x) {
+    uint32_t c[4] = {(uint32_t)L, (uint32_t)(L >> 32), (uint32_t)i, 0x53414331u};
+    philox10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+    // two outputs per counter: uniforms from c[0], c[1]; normals from (c[0], c[1]) and
+    // (c[2], c[3]) by Box-Muller
+    const float v1 = 1.0f - u01(c[0]), v2 = u01(c[1]);
+    const float v3 = 1.0f - u01(c[2]), v4 = u01(c[3]);
+    const float g1 = sqrtf(-2.0f * logf(v1)) * cospif(2.0f * v2);
+    const float g2 = sqrtf(-2.0f * logf(v3)) * cospif(2.0f * v4);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int o = 2 * i + h;
+      if (o < nu) u[o] = h == 0 ? u01(c[0]) : u01(c[1]);
+      else if (o < nu + n1) e1[o - nu] = h == 0 ? g1 : g2;
+      else if (o < total) e2[o - nu - n1] = h == 0 ? g1 : g2;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) launch[0] = L + 1;
+}
+
 // one wave per row: h1 = relu(p1 + b1); mu = h1 Wmu^T + bmu; lsr = h1 Wls^T + bls;
 // SB3's squashed Gaussian (sac_adam.hip sq_gauss_fwd_kernel): a = tanh(mu + exp(clamp(lsr)) eps)
 __global__ __launch_bounds__(256) void actor_head_kernel(
     const float* __restrict__ p1, const float* __restrict__ b1, const float* __restrict__ wmu,
     const float* __restrict__ bmu, const float* __restrict__ wls, const float* __restrict__ bls,
     const float* __restrict__ eps, int R, int A, float* __restrict__ h1, float* __restrict__ mu,
-    float* __restrict__ lsr, float* __restrict__ a_out, float* __restrict__ logp) {
+    float* __restrict__ lsr, float* __restrict__ a_out, float* __restrict__ logp,
+    int RT, const float* __restrict__ xt, int ldxt, int Kxt, const float* __restrict__ tw0,
+    const float* __restrict__ tb0, float* __restrict__ g0t) {
   const int lane = threadIdx.x & 63;
   const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (r >= R) return;
+  float av[4] = {0.0f, 0.0f, 0.0f, 0.0f};
   float hv[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -103,6 +191,7 @@ __global__ __launch_bounds__(256) void actor_head_kernel(
     const float z = (uu - m) / sd;
     s1 += -0.5f * (z * z) - ls - LOG_SQRT_2PI;
     s2 += logf(1.0f - a * a + 1e-6f);
+    av[j & 3] = a;
     if (lane == 0) {
       mu[ij] = m;
       lsr[ij] = lr_;
@@ -110,6 +199,23 @@ __global__ __launch_bounds__(256) void actor_head_kernel(
     }
   }
   if (lane == 0) logp[r] = s1 - s2;
+  // rows r < RT (the next observations): the target critics' first layer on [x_r, a_r]
+  // (in_layer's sum, k in order), so the TD target needs no launch of its own
+  if (g0t && r < RT) {
+    const int K = Kxt + A;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int u = lane + 64 * i;
+        float acc = 0.0f;
+        for (int k = 0; k < Kxt; ++k) acc += xt[(size_t)r * ldxt + k] * tw0[((size_t)c * K + k) * H + u];
+        for (int j = 0; j < A; ++j) acc += av[j & 3] * tw0[((size_t)c * K + Kxt + j) * H + u];
+        const float z = acc + tb0[(size_t)c * H + u];
+        g0t[((size_t)c * RT + r) * H + u] = z > 0.0f ? z : 0.0f;
+      }
+    }
+  }
 }
 
 enum { HEAD_TARGET = 0, HEAD_CRITIC = 1, HEAD_ACTOR_LOSS = 2, HEAD_TD_CRITIC = 3 };
@@ -543,12 +649,33 @@ int32_t sf_in_layer(const float* xa, const float* xa_hi, int32_t split, int32_t 
 
 int32_t sf_actor_head(const float* p1, const float* b1, const float* wmu, const float* bmu,
                       const float* wls, const float* bls, const float* eps, int32_t R, int32_t A,
-                      float* h1, float* mu, float* lsr, float* a_out, float* logp, void* stream) {
+                      float* h1, float* mu, float* lsr, float* a_out, float* logp, int32_t RT,
+                      const float* xt, int32_t ldxt, int32_t Kxt, const float* tw0, const float* tb0,
+                      float* g0t, void* stream) {
   if (!p1 || !b1 || !wmu || !bmu || !wls || !bls || !eps || !h1 || !mu || !lsr || !a_out || !logp ||
       R < 1 || A < 1 || A > 4)
     return -1;
+  if (g0t && (!xt || !tw0 || !tb0 || RT < 1 || RT > R || Kxt < 1 || ldxt < Kxt)) return -1;
   SF_LAUNCH(actor_head_kernel, dim3((R + 3) / 4), dim3(256), p1, b1, wmu, bmu, wls, bls, eps, R, A,
-            h1, mu, lsr, a_out, logp);
+            h1, mu, lsr, a_out, logp, RT, xt, ldxt, Kxt, tw0, tb0, g0t);
+}
+
+int32_t sf_in_layer_pair(const float* xa, const float* xa_hi, int32_t split, int32_t lda, int32_t Ka,
+                         int32_t R1, const float* w1, const float* b1, float* out1, const float* ya,
+                         int32_t ldya, int32_t Kya, const float* yb, int32_t ldyb, int32_t Kyb, int32_t R2,
+                         const float* w2, const float* b2, float* out2, void* stream) {
+  if (!xa || !xa_hi || !w1 || !b1 || !out1 || !ya || !w2 || !b2 || !out2 || R1 < 1 || R2 < 1 ||
+      Ka < 1 || Kya < 1 || Kyb < 0 || (Kyb && !yb) || split < 0 || split > R1)
+    return -1;
+  const int R = R1 > R2 ? R1 : R2;
+  SF_LAUNCH(in_layer_pair_kernel, dim3(R, 3), dim3(H), xa, xa_hi, split, lda, Ka, R1, w1, b1, out1,
+            ya, ldya, Kya, yb, ldyb, Kyb, R2, w2, b2, out2);
+}
+
+int32_t sf_noise(unsigned long long* launch, unsigned long long seed, float* u, int32_t nu, float* e1,
+                 int32_t n1, float* e2, int32_t n2, void* stream) {
+  if (!launch || nu < 0 || n1 < 0 || n2 < 0 || (nu && !u) || (n1 && !e1) || (n2 && !e2)) return -1;
+  SF_LAUNCH(noise_kernel, dim3(1), dim3(1024), launch, seed, u, nu, e1, n1, e2, n2);
 }
 
 int32_t sf_critic_head(const float* p1, const float* b1, const float* w2, const float* b2, int32_t B,

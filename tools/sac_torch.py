@@ -536,8 +536,17 @@ class FusedSAC(SAC):
 
     _lib = None
 
-    def __init__(self, obs_dim, act_dim, device, **kw):
+    def __init__(self, obs_dim, act_dim, device, noise=None, **kw):
         super().__init__(obs_dim, act_dim, device, **kw)
+        # noise: "philox" = the update's uniforms and normals (and an attached action sample's)
+        # from one launch of tools/sac_fused.hip; "torch" = torch.rand / torch.randn in
+        # SAC.update's order (the equivalence test draws both updates' numbers that way)
+        self.noise = noise or os.environ.get("SAC_NOISE", "philox")
+        if self.noise not in ("philox", "torch"):
+            raise ValueError("FusedSAC: noise is 'philox' or 'torch'")
+        self._launch = torch.zeros(1, dtype=torch.int64, device=self.dev)
+        self._seed = int(kw.get("seed", 0)) * 0x9E3779B97F4A7C15 % (1 << 64) ^ 0x5AC0FFEE
+        self._pol_eps = None
         if not self.hip_adam or self.world != 1 or self.dev.type != "cuda":
             raise ValueError("FusedSAC: one rank, the HIP Adam path (SAC_ADAM=hip)")
         if FusedSAC._lib is None:
@@ -546,7 +555,7 @@ class FusedSAC(SAC):
             lib = ctypes.CDLL(FUSED_LIB)
             for name in ("sf_in_layer", "sf_actor_head", "sf_critic_head", "sf_critic_bwd_head",
                          "sf_critic_bwd_in", "sf_actor_bwd_head", "sf_actor_bwd_cols", "sf_actor_bwd_in",
-                         "sf_td_critic_head"):
+                         "sf_td_critic_head", "sf_in_layer_pair", "sf_noise"):
                 getattr(lib, name).restype = ctypes.c_int32
             FusedSAC._lib = lib
         HipAdam([torch.zeros(1, device=self.dev)], 0.0)         # loads sac_adam.hip's library
@@ -578,10 +587,19 @@ class FusedSAC(SAC):
         for p in list(self.actor.parameters()) + list(self.q.parameters()) + [self.log_alpha]:
             p.grad = torch.zeros_like(p)
 
+    def attach_policy_noise(self, eps):
+        """Philox noise: each update also fills `eps` (fp32, contiguous) with N(0, 1) draws for
+        the next vector step's action sample (RLLoop), in the same launch."""
+        if eps.dtype != torch.float32 or not eps.is_contiguous() or eps.device != self.dev:
+            raise ValueError("attach_policy_noise: contiguous fp32 tensor on the learner's device")
+        self._pol_eps = eps
+
     def _call(self, name, *args):
         c = []
         for x in args:
-            if isinstance(x, torch.Tensor):
+            if isinstance(x, ctypes._SimpleCData):
+                c.append(x)
+            elif isinstance(x, torch.Tensor):
                 c.append(ctypes.c_void_p(x.data_ptr()))
             elif x is None:
                 c.append(ctypes.c_void_p(None))
@@ -595,7 +613,8 @@ class FusedSAC(SAC):
             raise RuntimeError(f"{name} failed ({rc})")
 
     def update(self, losses=True):
-        """SAC.update's gradient step (same order of evaluation and RNG draws)."""
+        """SAC.update's gradient step (same order of evaluation; with noise="torch" the same
+        RNG draws)."""
         with torch.no_grad():
             return self._update(losses)
 
@@ -606,7 +625,13 @@ class FusedSAC(SAC):
         ic = od + A
         rows = self._rows
         L = HipAdam._lib
-        torch.rand(B, device=self.dev, out=self._u)
+        f = self._call
+        if self.noise == "philox":
+            pe = self._pol_eps
+            f("sf_noise", self._launch, ctypes.c_uint64(self._seed), self._u, B, self._eps, 2 * B * A,
+              pe, 0 if pe is None else pe.numel())
+        else:
+            torch.rand(B, device=self.dev, out=self._u)
         # the sample, with the shared Adam step count advanced in the same launch (opt_q.tick())
         rc = L.sac_replay_sample_tick(ctypes.c_void_p(self.buf.data_ptr()), self.cap, W,
                                       ctypes.c_void_p(self._u.data_ptr()), B,
@@ -615,23 +640,25 @@ class FusedSAC(SAC):
                                       ctypes.c_void_p(torch.cuda.current_stream(self.dev).cuda_stream))
         if rc != 0:
             raise RuntimeError(f"sac_replay_sample_tick failed ({rc})")
-        torch.randn((2 * B, A), device=self.dev, out=self._eps)
-        f = self._call
+        if self.noise == "torch":
+            torch.randn((2 * B, A), device=self.dev, out=self._eps)
         o = rows                                    # columns 0..od of the row
         a = rows[:, od:]                            # the stored action (ld = W)
         o2 = rows[:, od + A + 1:]                   # next obs
         act, logp = self._act, self._logp
         la_, lat = self.actor.latent, self.actor
         # ---- actor on [o2; o] (one pass: its parameters do not change before its step) ----
-        f("sf_in_layer", o2, o, B, W, od, None, 0, 0, 2 * B, 1, la_[0].weight, 0, la_[0].bias, self._h0)
-        torch.mm(self._h0, la_[2].weight.t(), out=self._p1a)
-        f("sf_actor_head", self._p1a, la_[2].bias, lat.mu.weight, lat.mu.bias, lat.log_std.weight,
-          lat.log_std.bias, self._eps, 2 * B, A, self._h1, self._mu, self._lsr, act, logp)
         q, qt = self.q, self.qt
+        # (the online critics' first layer on [o, a] in the same launch as the actor's)
+        f("sf_in_layer_pair", o2, o, B, W, od, 2 * B, la_[0].weight, la_[0].bias, self._h0,
+          o, W, od, a, W, A, B, q.w0, q.b0, self._g0)
+        torch.mm(self._h0, la_[2].weight.t(), out=self._p1a)
+        # (the target critics' first layer on [o2, a2] inside the actor's head launch)
+        f("sf_actor_head", self._p1a, la_[2].bias, lat.mu.weight, lat.mu.bias, lat.log_std.weight,
+          lat.log_std.bias, self._eps, 2 * B, A, self._h1, self._mu, self._lsr, act, logp,
+          B, o2, W, od, qt.w0, qt.b0, self._g04[0:2])
         # ---- TD target from the target critics on [o2, a2] and the critics on [o, a]: one
         # bmm over the four second layers, one head (y, then the twin MSE's gradient) ---------
-        f("sf_in_layer", o2, None, B, W, od, act, A, A, B, 2, qt.w0, 1, qt.b0, self._g04[0:2])
-        f("sf_in_layer", o, None, B, W, od, a, W, A, B, 2, q.w0, 1, q.b0, self._g0)
         torch.bmm(self._g04, self._w1, out=self._p14)
         f("sf_td_critic_head", self._p14, qt.b1, qt.w2, qt.b2, q.b1, q.w2, q.b2, B, rows, W, od + A,
           W - 1, self.gamma, self.log_alpha, logp, self._y, self._g1, self._q, self._dq, self._lossq)
@@ -679,15 +706,21 @@ class RLLoop:
         # fused_policy: the action sample is one HIP kernel (bluesky_gym.policy.SACPolicy,
         # bsg_policy_sac) reading the live actor's parameters, instead of ~25 torch kernels
         self.pol = None
+        # (FusedSAC with Philox noise draws the next step's eps inside its update: one launch less)
+        self.own_noise = True
         if fused_policy:
             from bluesky_gym.policy import SACPolicy
             self.pol = SACPolicy.from_module(sac.actor)
-            self.eps = torch.zeros((batch.E, batch.act_dim), dtype=torch.float32, device=batch.device)
+            self.eps = torch.randn((batch.E, batch.act_dim), dtype=torch.float32, device=batch.device)
+            if learn and isinstance(sac, FusedSAC) and sac.noise == "philox":
+                sac.attach_policy_noise(self.eps)
+                self.own_noise = False
 
     def step(self):
         b, s = self.b, self.sac
         if self.pol is not None:
-            torch.randn(self.eps.shape, device=self.eps.device, out=self.eps)
+            if self.own_noise:
+                torch.randn(self.eps.shape, device=self.eps.device, out=self.eps)
             a = self.pol(self.obs, self.eps, out=self.act)
         else:
             with torch.no_grad():
