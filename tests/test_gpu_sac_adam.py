@@ -308,3 +308,51 @@ def test_fused_sac_philox_noise():
     assert abs(float(n.mean())) < 0.01 and abs(float(n.std()) - 1.0) < 0.01
     assert abs(float(((n - n.mean()) ** 3).mean())) < 0.03              # skew
     assert abs(float(((n - n.mean()) ** 4).mean()) - 3.0) < 0.1         # kurtosis
+
+
+def _philox10_np(c, k):
+    """Philox4x32-10 (Salmon et al., SC'11) in NumPy uint64 arithmetic: counters c [n, 4],
+    key k (2,) -- the restatement tools/sac_fused.hip philox10 is checked against."""
+    import numpy as np
+    c = c.astype(np.uint64)
+    k0, k1 = np.uint64(k[0]), np.uint64(k[1])
+    M = np.uint64(0xFFFFFFFF)
+    for _ in range(10):
+        p0 = np.uint64(0xD2511F53) * c[:, 0]
+        p1 = np.uint64(0xCD9E8D57) * c[:, 2]
+        n0 = (p1 >> np.uint64(32)) ^ c[:, 1] ^ k0
+        n2 = (p0 >> np.uint64(32)) ^ c[:, 3] ^ k1
+        c = np.stack([n0 & M, p1 & M, n2 & M, p0 & M], 1)
+        k0 = (k0 + np.uint64(0x9E3779B9)) & M
+        k1 = (k1 + np.uint64(0xBB67AE85)) & M
+    return c.astype(np.uint32)
+
+
+def test_philox_noise_matches_numpy_restatement():
+    """The noise kernel's uniforms bit for bit and its Box-Muller normals to fp32 rounding
+    against a NumPy Philox4x32-10 of the same key and counters (launch number, element)."""
+    import ctypes
+    import numpy as np
+    dev = torch.device("cuda", 0)
+    s = _sac_pair(sac_torch.FusedSAC, 4, 1, dev)
+    nu, n1 = 256, 512
+    u = torch.zeros(nu, device=dev)
+    e = torch.zeros(n1, device=dev)
+    launch = torch.tensor([5], dtype=torch.int64, device=dev)
+    seed = 0x0123456789ABCDEF
+    s._call("sf_noise", launch, ctypes.c_uint64(seed), u, nu, e, n1, None, 0)
+    torch.cuda.synchronize()
+    assert int(launch.item()) == 6
+    n = (nu + n1 + 1) // 2
+    ctr = np.zeros((n, 4), np.uint32)
+    ctr[:, 0] = 5
+    ctr[:, 2] = np.arange(n)
+    ctr[:, 3] = 0x53414331
+    r = _philox10_np(ctr, (seed & 0xFFFFFFFF, seed >> 32))
+    u01 = lambda x: (x >> 8).astype(np.float32) * np.float32(1.0 / 16777216.0)  # noqa: E731
+    want_u = np.stack([u01(r[:, 0]), u01(r[:, 1])], 1).reshape(-1)[:nu]
+    assert np.array_equal(u.cpu().numpy(), want_u)
+    g1 = np.sqrt(-2.0 * np.log(1.0 - u01(r[:, 0]).astype(np.float64))) * np.cos(2 * np.pi * u01(r[:, 1]))
+    g2 = np.sqrt(-2.0 * np.log(1.0 - u01(r[:, 2]).astype(np.float64))) * np.cos(2 * np.pi * u01(r[:, 3]))
+    want_e = np.stack([g1, g2], 1).reshape(-1)[nu:nu + n1]
+    assert np.allclose(e.cpu().numpy(), want_e, rtol=2e-6, atol=2e-6)
