@@ -410,40 +410,42 @@ __global__ __launch_bounds__(256) void critic_bwd_head_kernel(
   }
 }
 
-// m = dg0 (g0 > 0); dw0[c][k][u] = sum_r x[r][k] m, db0[c][u] = sum_r m;  x[r] = [xa | xb]
+// m = dg0 (g0 > 0); dw0[c][k][u] = sum_r x[r][k] m, db0[c][u] = sum_r m;  x[r] = [xa | xb].
+// The rows' inputs x (shared by the workgroup's 16 columns) are staged in LDS once, so a
+// thread loads only its rows' dg0 / g0 (the sums and their order are unchanged).
+constexpr int kXR = 256, kXK = 48;       // staged rows / inputs (checked by the launchers)
 __global__ __launch_bounds__(256) void critic_bwd_in_kernel(
     const float* __restrict__ dg0, const float* __restrict__ g0, const float* __restrict__ xa,
     int lda, int Ka, const float* __restrict__ xb, int ldb, int Kb, int B,
     float* __restrict__ dw0, float* __restrict__ db0) {
   __shared__ float lds[9][NRG][CPB];
+  __shared__ float xl[kXR][kXK + 1];
   const int u = blockIdx.x * CPB + threadIdx.x % CPB;
   const int c = blockIdx.y;
   int r0, r1;
   group_rows(B, r0, r1);
   const int K = Ka + Kb;
+  for (int q = threadIdx.x; q < B * K; q += blockDim.x) {
+    const int r = q / K, k = q - r * K;
+    xl[r][k] = k < Ka ? xa[(size_t)r * lda + k] : xb[(size_t)r * ldb + (k - Ka)];
+  }
+  float mm[RPG];
+#pragma unroll
+  for (int t = 0; t < RPG; ++t) {
+    const int r = min(r0 + t, r1 - 1);
+    const size_t o = ((size_t)c * B + r) * H + u;
+    const float g = g0[o], d = dg0[o];
+    mm[t] = (r0 + t < r1 && g > 0.0f) ? d : 0.0f;
+  }
+  __syncthreads();
   for (int k0 = 0; k0 < K; k0 += 8) {
     float v[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};   // 8 weight sums, the bias sum
-    for (int rb = r0; rb < r1; rb += RPG) {
-      float mm[RPG];
-      float xs[RPG][8];
 #pragma unroll
-      for (int t = 0; t < RPG; ++t) {
-        const int r = min(rb + t, r1 - 1);
-        const size_t o = ((size_t)c * B + r) * H + u;
-        const float g = g0[o], d = dg0[o];
-        mm[t] = (rb + t < r1 && g > 0.0f) ? d : 0.0f;
+    for (int t = 0; t < RPG; ++t) {
+      const int r = min(r0 + t, r1 - 1);
+      v[8] += mm[t];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const int k = min(k0 + i, K - 1);
-          xs[t][i] = k < Ka ? xa[(size_t)r * lda + k] : xb[(size_t)r * ldb + (k - Ka)];
-        }
-      }
-#pragma unroll
-      for (int t = 0; t < RPG; ++t) {
-        v[8] += mm[t];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) v[i] += xs[t][i] * mm[t];
-      }
+      for (int i = 0; i < 8; ++i) v[i] += xl[r][min(k0 + i, K - 1)] * mm[t];
     }
     group_sum<9>(v, lds);
     if (threadIdx.x < CPB) {
@@ -588,33 +590,36 @@ __global__ __launch_bounds__(256) void actor_bwd_cols_kernel(
   }
 }
 
-// m = dh0 (h0 > 0); dW0[u][k] = sum_r m x[r][k] (torch layout), db0[u] = sum_r m
+// m = dh0 (h0 > 0); dW0[u][k] = sum_r m x[r][k] (torch layout), db0[u] = sum_r m (x staged
+// in LDS as above)
 __global__ __launch_bounds__(256) void actor_bwd_in_kernel(
     const float* __restrict__ dh0, const float* __restrict__ h0, const float* __restrict__ x,
     int ldx, int K, int R, float* __restrict__ dw0, float* __restrict__ db0) {
   __shared__ float lds[9][NRG][CPB];
+  __shared__ float xl[kXR][kXK + 1];
   const int u = blockIdx.x * CPB + threadIdx.x % CPB;
   int r0, r1;
   group_rows(R, r0, r1);
+  for (int q = threadIdx.x; q < R * K; q += blockDim.x) {
+    const int r = q / K, k = q - r * K;
+    xl[r][k] = x[(size_t)r * ldx + k];
+  }
+  float mm[RPG];
+#pragma unroll
+  for (int t = 0; t < RPG; ++t) {
+    const int r = min(r0 + t, r1 - 1);
+    const float h = h0[(size_t)r * H + u], d = dh0[(size_t)r * H + u];
+    mm[t] = (r0 + t < r1 && h > 0.0f) ? d : 0.0f;
+  }
+  __syncthreads();
   for (int k0 = 0; k0 < K; k0 += 8) {
     float v[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-    for (int rb = r0; rb < r1; rb += RPG) {
-      float mm[RPG];
-      float xs[RPG][8];
 #pragma unroll
-      for (int t = 0; t < RPG; ++t) {
-        const int r = min(rb + t, r1 - 1);
-        const float h = h0[(size_t)r * H + u], d = dh0[(size_t)r * H + u];
-        mm[t] = (rb + t < r1 && h > 0.0f) ? d : 0.0f;
+    for (int t = 0; t < RPG; ++t) {
+      const int r = min(r0 + t, r1 - 1);
+      v[8] += mm[t];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) xs[t][i] = x[(size_t)r * ldx + min(k0 + i, K - 1)];
-      }
-#pragma unroll
-      for (int t = 0; t < RPG; ++t) {
-        v[8] += mm[t];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) v[i] += mm[t] * xs[t][i];
-      }
+      for (int i = 0; i < 8; ++i) v[i] += mm[t] * xl[r][min(k0 + i, K - 1)];
     }
     group_sum<9>(v, lds);
     if (threadIdx.x < CPB) {
@@ -701,6 +706,7 @@ int32_t sf_critic_bwd_in(const float* dg0, const float* g0, const float* xa, int
                          const float* xb, int32_t ldb, int32_t Kb, int32_t B, float* dw0, float* db0,
                          void* stream) {
   if (!dg0 || !g0 || !xa || !dw0 || !db0 || B < 1 || Ka < 1 || Kb < 0 || (Kb && !xb)) return -1;
+  if (B > kXR || Ka + Kb > kXK || B > NRG * RPG) return -1;
   SF_LAUNCH(critic_bwd_in_kernel, dim3(H / CPB, 2), dim3(256), dg0, g0, xa, lda, Ka, xb, ldb, Kb, B, dw0, db0);
 }
 
@@ -743,6 +749,7 @@ int32_t sf_actor_bwd_cols(const float* dmu, const float* dlsr, const float* h1, 
 int32_t sf_actor_bwd_in(const float* dh0, const float* h0, const float* x, int32_t ldx, int32_t K,
                         int32_t R, float* dw0, float* db0, void* stream) {
   if (!dh0 || !h0 || !x || !dw0 || !db0 || R < 1 || K < 1) return -1;
+  if (R > kXR || K > kXK || R > NRG * RPG) return -1;
   SF_LAUNCH(actor_bwd_in_kernel, dim3(H / CPB), dim3(256), dh0, h0, x, ldx, K, R, dw0, db0);
 }
 
