@@ -651,9 +651,9 @@ def bench_descent_sac(args):
                          seed=1234, env_offset=rank * E)
     b.reset()
     W = dict(np.load(os.path.join(REPO, "tests", "golden", "sac_actors.npz")))
-    # one rank: FusedSAC (tools/sac_fused.hip); across ranks the autograd update with its
-    # RCCL gradient all-reduce
-    cls = sac_torch.FusedSAC if (world == 1 and os.environ.get("SAC_FUSED", "1") == "1") else sac_torch.SAC
+    # FusedSAC (tools/sac_fused.hip); across ranks with its RCCL gradient all-reduce before
+    # each Adam launch (eager); SAC_FUSED=0 = the autograd update
+    cls = sac_torch.FusedSAC if os.environ.get("SAC_FUSED", "1") == "1" else sac_torch.SAC
     sac = cls(b.obs_dim, b.act_dim, dev, group=dist.group.WORLD if world > 1 else None,
                         seed=rank, lr=1e-3)
     sac.actor.load_sb3(W, "descent")
@@ -730,7 +730,8 @@ def bench_descent_sac(args):
                        "policy": "fused HIP actor (bsg_policy_sac)" if fused else "torch actor",
                        "adam": "one launch per step (tools/sac_adam.hip)" if sac.hip_adam else
                                "torch " + os.environ.get("SAC_ADAM", "fused"),
-                       "hip_graph": graph, "blas": str(torch.backends.cuda.preferred_blas_library())},
+                       "hip_graph": graph, "blas": str(torch.backends.cuda.preferred_blas_library()),
+                       "update": type(sac).__name__},
             "env_only": {"value": total / el_env, "ms_per_step": el_env * 1e3 / args.steps},
             "env_policy": {"value": total / el_pol, "ms_per_step": el_pol * 1e3 / args.steps,
                            "policy": "fused HIP actor (bsg_policy_sac)" if fused else "torch actor"},

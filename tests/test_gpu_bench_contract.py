@@ -73,3 +73,32 @@ def test_bench_two_rank_rehearsal_checks_rows():
     assert cfg["gather_transport"] == "torch" and cfg["rccl"] is None
     rc = cfg["row_check"]
     assert rc["ok"] is True and rc["bad_rows"] == 0 and rc["bad_rows_by_source_rank"] == [0, 0]
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def test_bench_descent_sac_two_rank_rehearsal():
+    """BASELINE configs[4]'s multi-GPU path on one GPU (2 ranks over gloo): each rank steps
+    its 2,048-env shard with the fused actor and runs FusedSAC on its shard's buffer, the
+    gradients all-reduced before each Adam launch; one JSON line, finite losses."""
+    env = dict(os.environ, BENCH_BACKEND="gloo")
+    out = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                          "--nproc-per-node", "2", "--master-addr", "127.0.0.1", "--master-port",
+                          str(_free_port()), "bench.py", "--workload", "descent-sac", "--gpus", "2",
+                          "--steps", "4", "--warmup", "2"], cwd=REPO, capture_output=True, text=True,
+                         timeout=300, env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    r = json.loads(lines[0])
+    assert r["n_gpus"] == 2 and r["config"]["envs_total"] == 4096 and r["config"]["envs_per_gpu"] == 2048
+    assert r["config"]["update"] == "FusedSAC" and r["config"]["hip_graph"] is False
+    ln = r["env_policy_learner"]
+    assert ln["value"] > 0 and ln["critic_loss"] == ln["critic_loss"] and ln["actor_loss"] == ln["actor_loss"]

@@ -356,3 +356,62 @@ def test_philox_noise_matches_numpy_restatement():
     g2 = np.sqrt(-2.0 * np.log(1.0 - u01(r[:, 2]).astype(np.float64))) * np.cos(2 * np.pi * u01(r[:, 3]))
     want_e = np.stack([g1, g2], 1).reshape(-1)[nu:nu + n1]
     assert np.allclose(e.cpu().numpy(), want_e, rtol=2e-6, atol=2e-6)
+
+
+def _fused_rank(rank, world, port, od, ad, path):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dev = torch.device("cuda", 0)
+    s = sac_torch.FusedSAC(od, ad, dev, seed=7, lr=1e-3, buffer=4096 * world, batch=256 * world,
+                           group=dist.group.WORLD, noise="torch")
+    gen = torch.Generator(device=dev).manual_seed(11)
+    n = 1024
+    s.insert(torch.randn((n, od), generator=gen, device=dev),
+             torch.rand((n, ad), generator=gen, device=dev) * 2 - 1,
+             torch.randn((n,), generator=gen, device=dev), torch.randn((n, od), generator=gen, device=dev),
+             (torch.rand((n,), generator=gen, device=dev) < 0.1).float())
+    for _ in range(5):
+        s.update(losses=False)
+    torch.cuda.synchronize()
+    if rank == 0:
+        torch.save([p.detach().cpu() for p in list(s.actor.parameters()) + list(s.q.parameters()) +
+                    list(s.qt.parameters()) + [s.log_alpha]], path)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_fused_sac_two_ranks_equal_one_rank(tmp_path):
+    """FusedSAC across ranks (gloo, 2 processes on the one GPU): both ranks hold the same
+    buffer and seed, so they sample the same rows, and the all-reduced mean of two equal
+    gradients is that gradient exactly -- the parameters after five updates must equal one
+    rank's bit for bit (the all-reduce sits before each Adam launch; the union-batch semantics
+    of the same SAC._allreduce are tests/test_sac_learner_cpu.py's)."""
+    import torch.multiprocessing as mp
+    path = str(tmp_path / "two.pt")
+    mp.spawn(_fused_rank, args=(2, _free_port(), 4, 1, path), nprocs=2, join=True)
+    two = torch.load(path, weights_only=True)
+    dev = torch.device("cuda", 0)
+    s = sac_torch.FusedSAC(4, 1, dev, seed=7, lr=1e-3, buffer=4096, noise="torch")
+    gen = torch.Generator(device=dev).manual_seed(11)
+    n = 1024
+    s.insert(torch.randn((n, 4), generator=gen, device=dev),
+             torch.rand((n, 1), generator=gen, device=dev) * 2 - 1,
+             torch.randn((n,), generator=gen, device=dev), torch.randn((n, 4), generator=gen, device=dev),
+             (torch.rand((n,), generator=gen, device=dev) < 0.1).float())
+    for _ in range(5):
+        s.update(losses=False)
+    one = [p.detach().cpu() for p in list(s.actor.parameters()) + list(s.q.parameters()) +
+           list(s.qt.parameters()) + [s.log_alpha]]
+    assert len(one) == len(two)
+    for x, y in zip(one, two):
+        assert torch.equal(x, y)
+
+
+def _free_port():
+    import socket
+    so = socket.socket()
+    so.bind(("127.0.0.1", 0))
+    port = so.getsockname()[1]
+    so.close()
+    return port

@@ -547,8 +547,10 @@ class FusedSAC(SAC):
         self._launch = torch.zeros(1, dtype=torch.int64, device=self.dev)
         self._seed = int(kw.get("seed", 0)) * 0x9E3779B97F4A7C15 % (1 << 64) ^ 0x5AC0FFEE
         self._pol_eps = None
-        if not self.hip_adam or self.world != 1 or self.dev.type != "cuda":
-            raise ValueError("FusedSAC: one rank, the HIP Adam path (SAC_ADAM=hip)")
+        if not self.hip_adam or self.dev.type != "cuda":
+            raise ValueError("FusedSAC: the HIP Adam path (SAC_ADAM=hip) on a HIP device")
+        # (several ranks: the gradients are all-reduced before each Adam launch, SAC._allreduce;
+        # that path runs eagerly -- RLLoop.capture is for one rank)
         if FusedSAC._lib is None:
             if not os.path.exists(FUSED_LIB):
                 raise RuntimeError(f"{FUSED_LIB} missing: run __graft_entry__.build()")
@@ -667,6 +669,8 @@ class FusedSAC(SAC):
         torch.bmm(self._g0.transpose(1, 2), self._dg1, out=q.w1.grad)
         torch.bmm(self._dg1, q.w1.transpose(1, 2), out=self._dg0)
         f("sf_critic_bwd_in", self._dg0, self._g0, o, W, od, a, W, A, B, q.w0.grad, q.b0.grad)
+        if self.world > 1:
+            self._allreduce(list(self.q.parameters()))
         self.opt_q.step()                            # (the step count was advanced by the sample)
         # ---- actor loss through the updated critics on [o, ap] (critics frozen) ----------------
         ap, lp = act[B:], logp[B:]
@@ -688,6 +692,8 @@ class FusedSAC(SAC):
         torch.mm(self._dh1.t(), h0b, out=la_[2].weight.grad)
         torch.mm(self._dh1, la_[2].weight, out=self._dh0)
         f("sf_actor_bwd_in", self._dh0, h0b, o, W, od, B, la_[0].weight.grad, la_[0].bias.grad)
+        if self.world > 1:
+            self._allreduce(list(self.actor.parameters()) + [self.log_alpha])
         self.opt_a.step()                            # actor + log_alpha in one launch
         if losses:
             return self._lossq.sum(), self._lossa.sum()
