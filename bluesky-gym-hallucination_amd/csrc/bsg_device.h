@@ -341,7 +341,13 @@ __device__ __forceinline__ bool b_times_dphi_far(double latd1, double latd2, dou
 // longitude gap's sin/cos (sdl, cdl of lond2 * D2R - lond1 * D2R).
 __device__ __forceinline__ void qdr_x_t(double coslat1, double sinlat1, double coslat2, double sinlat2,
                                         double sdl, double cdl, double* qdr, double* x) {
+#if defined(BSG_EXP_FASTATAN) && BSG_EXP_FASTATAN
+  // timing experiment only (wrong results): the bearing's atan2 replaced by a division
+  const double yy = sdl * coslat2, xx = coslat1 * sinlat2 - sinlat1 * coslat2 * cdl;
+  *qdr = (yy / (fabs(xx) + fabs(yy))) * 90.0 + (xx < 0.0 ? 180.0 : 0.0);
+#else
   *qdr = atan2(sdl * coslat2, coslat1 * sinlat2 - sinlat1 * coslat2 * cdl) * kR2D;
+#endif
   *x = coslat1 * coslat2 * cdl + sinlat1 * sinlat2;
 }
 
