@@ -46,12 +46,15 @@ def _same(x, y, t):
 
 
 @pytest.mark.parametrize("kind,autoreset", [("descent", 1), ("descent", 2), ("vertical", 1),
-                                            ("vertical", 2)])
+                                            ("vertical", 2), ("descent25", 2)])
 def test_vertical_ownship_fastpath_bit_identical(kind, autoreset):
+    """descent25: 25 substeps per step -- not the 3 x 10 the seven-wave pipeline takes, so the
+    one-wave blocks (two of 10, then five single substeps) run instead."""
     from bluesky_gym import config
     cfg = (config.descent_config(max_episode_steps=60) if kind == "descent"
+           else config.descent_config(action_frequency=25, max_episode_steps=60) if kind == "descent25"
            else config.vertical_config(num_intruders=31, max_episode_steps=60))
-    E = 1024 if kind == "descent" else 256
+    E = 1024 if kind.startswith("descent") else 256
     cd = kind == "vertical"
     gen, fast = _batch(cfg, E, True, autoreset, cd), _batch(cfg, E, False, autoreset, cd)
     g = torch.Generator(device="cuda").manual_seed(4)
