@@ -17,8 +17,9 @@
 //                target y, the twin-MSE gradient dq, or the actor loss's dq / dlogp
 //   td_critic_head  the target critics and the online critics of one [4, B, H] product: y,
 //                then the online heads' dq (one launch for both)
-//   critic_bwd_head   dg1 = dq w2 (g1 > 0) and the w2 / b2 / b1 gradients (column sums)
-//   critic_bwd_in     the first layer's gradients from dg0 (g0 > 0)
+//   (the heads' backward, dg1 = dq w2 (g1 > 0), in td_critic_head / critic_head's launch)
+//   critic_bwd_in     the first layer's gradients from dg0 (g0 > 0), and the w2 / b2 / b1
+//                     gradients (column sums)
 //   actor_bwd_head    the critics' action gradient, the squashed Gaussian's backward and
 //                     dh1 = (dmu Wmu + dlsr Wls)(h1 > 0)
 //   actor_bwd_cols    the heads' and b1's gradients and d log_alpha (column sums)
@@ -231,11 +232,11 @@ __global__ __launch_bounds__(256) void critic_head_kernel(
     int col_r, int col_d, float gamma, const float* __restrict__ log_alpha,
     const float* __restrict__ logp, float* __restrict__ y, float* __restrict__ g1,
     float* __restrict__ q_out, float* __restrict__ dq, float* __restrict__ dlogp,
-    float* __restrict__ lossp) {
+    float* __restrict__ lossp, float* __restrict__ dg1) {
   const int lane = threadIdx.x & 63;
   const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (r >= B) return;
-  float q[2];
+  float q[2], gk[2][4];
 #pragma unroll
   for (int c = 0; c < 2; ++c) {
     float part = 0.0f;
@@ -245,10 +246,33 @@ __global__ __launch_bounds__(256) void critic_head_kernel(
       const size_t o = ((size_t)c * B + r) * H + u;
       const float z = p1[o] + b1[(size_t)c * H + u];
       const float g = z > 0.0f ? z : 0.0f;
-      if (mode != HEAD_TARGET) g1[o] = g;
+      if (mode != HEAD_TARGET && g1) g1[o] = g;
+      gk[c][i] = g;
       part += g * w2[(size_t)c * H + u];
     }
     q[c] = wave_sum(part) + b2[c];
+  }
+  if (mode == HEAD_ACTOR_LOSS && dg1) {
+    // the actor loss's gradient through the critics' head (dg1), from the
+    // row's dq -- wave-uniform, as lane 0 stores it below
+    const float ng = -(1.0f / (float)B);
+    const float mn = fminf(q[0], q[1]);
+    float dqv[2];
+    if (q[0] == q[1]) {
+      dqv[0] = ng / 2.0f;
+      dqv[1] = ng / 2.0f;
+    } else {
+      dqv[0] = q[0] == mn ? ng : 0.0f;
+      dqv[1] = q[1] == mn ? ng : 0.0f;
+    }
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int u = lane + 64 * i;
+        dg1[((size_t)c * B + r) * H + u] = gk[c][i] > 0.0f ? dqv[c] * w2[(size_t)c * H + u] : 0.0f;
+      }
+    }
   }
   if (lane != 0) return;
   const float alpha = expf(log_alpha[0]);
@@ -296,11 +320,11 @@ __global__ __launch_bounds__(256) void td_critic_head_kernel(
     const float* __restrict__ b2, int B, const float* __restrict__ rows, int W, int col_r,
     int col_d, float gamma, const float* __restrict__ log_alpha, const float* __restrict__ logp,
     float* __restrict__ y, float* __restrict__ g1, float* __restrict__ q_out,
-    float* __restrict__ dq, float* __restrict__ lossp) {
+    float* __restrict__ dq, float* __restrict__ lossp, float* __restrict__ dg1) {
   const int lane = threadIdx.x & 63;
   const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (r >= B) return;
-  float q[4];
+  float q[4], gk[2][4];
 #pragma unroll
   for (int c = 0; c < 4; ++c) {
     const int cc = c & 1;
@@ -312,27 +336,46 @@ __global__ __launch_bounds__(256) void td_critic_head_kernel(
       const int u = lane + 64 * i;
       const float z = p1[((size_t)c * B + r) * H + u] + bb[(size_t)cc * H + u];
       const float g = z > 0.0f ? z : 0.0f;
-      if (c >= 2) g1[((size_t)cc * B + r) * H + u] = g;
+      if (c >= 2) {
+        g1[((size_t)cc * B + r) * H + u] = g;
+        gk[cc][i] = g;
+      }
       part += g * ww[(size_t)cc * H + u];
     }
     q[c] = wave_sum(part) + (c < 2 ? tb2 : b2)[cc];
   }
-  if (lane != 0) return;
+  // (the row's scalars are wave-uniform: every lane evaluates them, lane 0 stores them)
   const float alpha = expf(log_alpha[0]);
   const float mn = fminf(q[0], q[1]);
   const float qt = mn - alpha * logp[r];
   const float d = rows[(size_t)r * W + col_d];
   const float rw = rows[(size_t)r * W + col_r];
   const float yr = rw + (gamma * (1.0f - d)) * qt;
-  y[r] = yr;
   const float invB = 1.0f / (float)B;
-  float l = 0.0f;
+  float dqv[2], l = 0.0f;
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const float df = q[2 + c] - yr;
+    dqv[c] = invB * (2.0f * df);
+    l += df * df / (float)B;
+  }
+  // the critics' backward through their head (dg1 = dq w2 (g1 > 0))
+  if (dg1) {
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int u = lane + 64 * i;
+        dg1[((size_t)c * B + r) * H + u] = gk[c][i] > 0.0f ? dqv[c] * w2[(size_t)c * H + u] : 0.0f;
+      }
+    }
+  }
+  if (lane != 0) return;
+  y[r] = yr;
 #pragma unroll
   for (int c = 0; c < 2; ++c) {
     q_out[(size_t)c * B + r] = q[2 + c];
-    const float df = q[2 + c] - yr;
-    dq[(size_t)c * B + r] = invB * (2.0f * df);
-    l += df * df / (float)B;
+    dq[(size_t)c * B + r] = dqv[c];
   }
   lossp[r] = l;
 }
@@ -370,54 +413,18 @@ __device__ __forceinline__ void group_rows(int R, int& r0, int& r1) {
   r1 = min(R, r0 + per);
 }
 
-// dg1[c][r][u] = dq[c][r] w2[c][u] (g1 > 0) for every row; with grads, dw2[c][u] = sum_r g1 dq,
-// db1[c][u] = sum_r dg1, db2[c] = sum_r dq
-__global__ __launch_bounds__(256) void critic_bwd_head_kernel(
-    const float* __restrict__ dq, const float* __restrict__ g1, const float* __restrict__ w2, int B,
-    int grads, float* __restrict__ dg1, float* __restrict__ dw2, float* __restrict__ db1,
-    float* __restrict__ db2) {
-  __shared__ float lds[3][NRG][CPB];
-  const int u = blockIdx.x * CPB + threadIdx.x % CPB;
-  const int c = blockIdx.y;
-  int r0, r1;
-  group_rows(B, r0, r1);
-  const float wv = w2[(size_t)c * H + u];
-  float v[3] = {0.0f, 0.0f, 0.0f};          // sum g1 dq, sum dg1, sum dq
-  for (int rb = r0; rb < r1; rb += RPG) {
-    float gg[RPG], dd[RPG];
-#pragma unroll
-    for (int t = 0; t < RPG; ++t) {
-      const int r = min(rb + t, r1 - 1);
-      gg[t] = g1[((size_t)c * B + r) * H + u];
-      dd[t] = dq[(size_t)c * B + r];
-    }
-#pragma unroll
-    for (int t = 0; t < RPG; ++t) {
-      if (rb + t < r1) {
-        const float val = gg[t] > 0.0f ? dd[t] * wv : 0.0f;
-        dg1[((size_t)c * B + rb + t) * H + u] = val;
-        v[0] += gg[t] * dd[t];
-        v[1] += val;
-        v[2] += dd[t];
-      }
-    }
-  }
-  group_sum<3>(v, lds);
-  if (grads && threadIdx.x < CPB) {
-    dw2[(size_t)c * H + u] = v[0];
-    db1[(size_t)c * H + u] = v[1];
-    if (u == 0) db2[c] = v[2];
-  }
-}
-
 // m = dg0 (g0 > 0); dw0[c][k][u] = sum_r x[r][k] m, db0[c][u] = sum_r m;  x[r] = [xa | xb].
 // The rows' inputs x (shared by the workgroup's 16 columns) are staged in LDS once, so a
 // thread loads only its rows' dg0 / g0 (the sums and their order are unchanged).
 constexpr int kXR = 256, kXK = 48;       // staged rows / inputs (checked by the launchers)
+// g1 != nullptr: also the head's column sums, dw2[c][u] = sum_r g1 dq,
+// db1[c][u] = sum_r dq w2 (g1 > 0), db2[c] = sum_r dq (the same rows, order and groups)
 __global__ __launch_bounds__(256) void critic_bwd_in_kernel(
     const float* __restrict__ dg0, const float* __restrict__ g0, const float* __restrict__ xa,
     int lda, int Ka, const float* __restrict__ xb, int ldb, int Kb, int B,
-    float* __restrict__ dw0, float* __restrict__ db0) {
+    float* __restrict__ dw0, float* __restrict__ db0, const float* __restrict__ g1,
+    const float* __restrict__ dq, const float* __restrict__ w2, float* __restrict__ dw2,
+    float* __restrict__ db1, float* __restrict__ db2) {
   __shared__ float lds[9][NRG][CPB];
   __shared__ float xl[kXR][kXK + 1];
   const int u = blockIdx.x * CPB + threadIdx.x % CPB;
@@ -425,6 +432,32 @@ __global__ __launch_bounds__(256) void critic_bwd_in_kernel(
   int r0, r1;
   group_rows(B, r0, r1);
   const int K = Ka + Kb;
+  if (g1) {
+    const float wv = w2[(size_t)c * H + u];
+    float gg[RPG], dd[RPG];
+#pragma unroll
+    for (int t = 0; t < RPG; ++t) {
+      const int r = min(r0 + t, r1 - 1);
+      gg[t] = g1[((size_t)c * B + r) * H + u];
+      dd[t] = dq[(size_t)c * B + r];
+    }
+    float v[3] = {0.0f, 0.0f, 0.0f};          // sum g1 dq, sum dg1, sum dq
+#pragma unroll
+    for (int t = 0; t < RPG; ++t) {
+      if (r0 + t < r1) {
+        const float val = gg[t] > 0.0f ? dd[t] * wv : 0.0f;
+        v[0] += gg[t] * dd[t];
+        v[1] += val;
+        v[2] += dd[t];
+      }
+    }
+    group_sum<3>(v, lds);
+    if (threadIdx.x < CPB) {
+      dw2[(size_t)c * H + u] = v[0];
+      db1[(size_t)c * H + u] = v[1];
+      if (u == 0) db2[c] = v[2];
+    }
+  }
   for (int q = threadIdx.x; q < B * K; q += blockDim.x) {
     const int r = q / K, k = q - r * K;
     xl[r][k] = k < Ka ? xa[(size_t)r * lda + k] : xb[(size_t)r * ldb + (k - Ka)];
@@ -686,28 +719,25 @@ int32_t sf_noise(unsigned long long* launch, unsigned long long seed, float* u, 
 int32_t sf_critic_head(const float* p1, const float* b1, const float* w2, const float* b2, int32_t B,
                        int32_t mode, const float* rows, int32_t W, int32_t col_r, int32_t col_d,
                        float gamma, const float* log_alpha, const float* logp, float* y, float* g1,
-                       float* q_out, float* dq, float* dlogp, float* lossp, void* stream) {
+                       float* q_out, float* dq, float* dlogp, float* lossp, float* dg1, void* stream) {
   if (!p1 || !b1 || !w2 || !b2 || !log_alpha || !q_out || B < 1 || mode < 0 || mode > 2) return -1;
   if (mode == HEAD_TARGET && (!rows || !logp || !y || col_r < 0 || col_r >= W || col_d < 0 || col_d >= W))
     return -1;
   if (mode == HEAD_CRITIC && (!y || !g1 || !dq || !lossp)) return -1;
-  if (mode == HEAD_ACTOR_LOSS && (!logp || !g1 || !dq || !dlogp || !lossp)) return -1;
+  if (mode == HEAD_ACTOR_LOSS && (!logp || !(g1 || dg1) || !dq || !dlogp || !lossp)) return -1;
   SF_LAUNCH(critic_head_kernel, dim3((B + 3) / 4), dim3(256), p1, b1, w2, b2, B, mode, rows, W, col_r,
-            col_d, gamma, log_alpha, logp, y, g1, q_out, dq, dlogp, lossp);
-}
-
-int32_t sf_critic_bwd_head(const float* dq, const float* g1, const float* w2, int32_t B, int32_t grads,
-                           float* dg1, float* dw2, float* db1, float* db2, void* stream) {
-  if (!dq || !g1 || !w2 || !dg1 || B < 1 || (grads && (!dw2 || !db1 || !db2))) return -1;
-  SF_LAUNCH(critic_bwd_head_kernel, dim3(H / CPB, 2), dim3(256), dq, g1, w2, B, grads, dg1, dw2, db1, db2);
+            col_d, gamma, log_alpha, logp, y, g1, q_out, dq, dlogp, lossp, dg1);
 }
 
 int32_t sf_critic_bwd_in(const float* dg0, const float* g0, const float* xa, int32_t lda, int32_t Ka,
                          const float* xb, int32_t ldb, int32_t Kb, int32_t B, float* dw0, float* db0,
-                         void* stream) {
+                         const float* g1, const float* dq, const float* w2, float* dw2, float* db1,
+                         float* db2, void* stream) {
+  if (g1 && (!dq || !w2 || !dw2 || !db1 || !db2)) return -1;
   if (!dg0 || !g0 || !xa || !dw0 || !db0 || B < 1 || Ka < 1 || Kb < 0 || (Kb && !xb)) return -1;
   if (B > kXR || Ka + Kb > kXK || B > NRG * RPG) return -1;
-  SF_LAUNCH(critic_bwd_in_kernel, dim3(H / CPB, 2), dim3(256), dg0, g0, xa, lda, Ka, xb, ldb, Kb, B, dw0, db0);
+  SF_LAUNCH(critic_bwd_in_kernel, dim3(H / CPB, 2), dim3(256), dg0, g0, xa, lda, Ka, xb, ldb, Kb, B, dw0, db0,
+            g1, dq, w2, dw2, db1, db2);
 }
 
 int32_t sf_actor_bwd_head(const float* ga, const float* gl, const float* mu, const float* lsr,
@@ -727,12 +757,12 @@ int32_t sf_td_critic_head(const float* p1, const float* tb1, const float* tw2, c
                           const float* b1, const float* w2, const float* b2, int32_t B, const float* rows,
                           int32_t W, int32_t col_r, int32_t col_d, float gamma, const float* log_alpha,
                           const float* logp, float* y, float* g1, float* q_out, float* dq, float* lossp,
-                          void* stream) {
+                          float* dg1, void* stream) {
   if (!p1 || !tb1 || !tw2 || !tb2 || !b1 || !w2 || !b2 || !rows || !log_alpha || !logp || !y || !g1 ||
       !q_out || !dq || !lossp || B < 1 || col_r < 0 || col_r >= W || col_d < 0 || col_d >= W)
     return -1;
   SF_LAUNCH(td_critic_head_kernel, dim3((B + 3) / 4), dim3(256), p1, tb1, tw2, tb2, b1, w2, b2, B, rows,
-            W, col_r, col_d, gamma, log_alpha, logp, y, g1, q_out, dq, lossp);
+            W, col_r, col_d, gamma, log_alpha, logp, y, g1, q_out, dq, lossp, dg1);
 }
 
 int32_t sf_actor_bwd_cols(const float* dmu, const float* dlsr, const float* h1, const float* dh1,

@@ -555,7 +555,7 @@ class FusedSAC(SAC):
             if not os.path.exists(FUSED_LIB):
                 raise RuntimeError(f"{FUSED_LIB} missing: run __graft_entry__.build()")
             lib = ctypes.CDLL(FUSED_LIB)
-            for name in ("sf_in_layer", "sf_actor_head", "sf_critic_head", "sf_critic_bwd_head",
+            for name in ("sf_in_layer", "sf_actor_head", "sf_critic_head",
                          "sf_critic_bwd_in", "sf_actor_bwd_head", "sf_actor_bwd_cols", "sf_actor_bwd_in",
                          "sf_td_critic_head", "sf_in_layer_pair", "sf_noise"):
                 getattr(lib, name).restype = ctypes.c_int32
@@ -663,12 +663,14 @@ class FusedSAC(SAC):
         # bmm over the four second layers, one head (y, then the twin MSE's gradient) ---------
         torch.bmm(self._g04, self._w1, out=self._p14)
         f("sf_td_critic_head", self._p14, qt.b1, qt.w2, qt.b2, q.b1, q.w2, q.b2, B, rows, W, od + A,
-          W - 1, self.gamma, self.log_alpha, logp, self._y, self._g1, self._q, self._dq, self._lossq)
+          W - 1, self.gamma, self.log_alpha, logp, self._y, self._g1, self._q, self._dq, self._lossq,
+          self._dg1)
         # ---- the critics' backward and step (polyak of the targets in the same launch) ---------
-        f("sf_critic_bwd_head", self._dq, self._g1, q.w2, B, 1, self._dg1, q.w2.grad, q.b1.grad, q.b2.grad)
+        # (dg1 came from the TD head's launch; the head's column sums ride in critic_bwd_in)
         torch.bmm(self._g0.transpose(1, 2), self._dg1, out=q.w1.grad)
         torch.bmm(self._dg1, q.w1.transpose(1, 2), out=self._dg0)
-        f("sf_critic_bwd_in", self._dg0, self._g0, o, W, od, a, W, A, B, q.w0.grad, q.b0.grad)
+        f("sf_critic_bwd_in", self._dg0, self._g0, o, W, od, a, W, A, B, q.w0.grad, q.b0.grad,
+          self._g1, self._dq, q.w2, q.w2.grad, q.b1.grad, q.b2.grad)
         if self.world > 1:
             self._allreduce(list(self.q.parameters()))
         self.opt_q.step()                            # (the step count was advanced by the sample)
@@ -676,9 +678,9 @@ class FusedSAC(SAC):
         ap, lp = act[B:], logp[B:]
         f("sf_in_layer", o, None, B, W, od, ap, A, A, B, 2, q.w0, 1, q.b0, self._g0)
         torch.bmm(self._g0, q.w1, out=self._p1c)
+        # (the head's backward, dg1, in the same launch: g1 itself is not needed)
         f("sf_critic_head", self._p1c, q.b1, q.w2, q.b2, B, 2, None, W, 0, 0, self.gamma,
-          self.log_alpha, lp, None, self._g1, self._q, self._dq, self._dlogp, self._lossa)
-        f("sf_critic_bwd_head", self._dq, self._g1, q.w2, B, 0, self._dg1, None, None, None)
+          self.log_alpha, lp, None, None, self._q, self._dq, self._dlogp, self._lossa, self._dg1)
         torch.bmm(self._dg1, q.w1.transpose(1, 2), out=self._dg0)
         # ---- actor backward (the o half of the pass; the critics' action gradient computed in
         # its head launch), entropy coefficient, their step ----------------------------------
