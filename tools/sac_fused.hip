@@ -6,7 +6,7 @@
 // squashed Gaussian as separate launches), each paying the ~1.5 us dependent-kernel boundary
 // (MI355X_MICROARCH.md 'boundary').  FusedSAC writes the forward and backward passes out and
 // keeps only the 256 x 256 products as rocBLAS GEMMs (torch.mm / bmm with out=); everything
-// between two GEMMs is one of the kernels below, so an update is ~30 launches:
+// between two GEMMs is one of the kernels below, so an update is 21 launches:
 //
 //   in_layer     relu(x W + b) for a layer whose K is the observation (+ action) width
 //   in_layer_pair  the actor's and the online critics' first layers in one launch

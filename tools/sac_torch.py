@@ -526,7 +526,7 @@ FUSED_LIB = os.path.join(_HERE, "_lib", "libsacfused.so")
 class FusedSAC(SAC):
     """SAC.update with its forward and backward passes written out (one rank, the HIP path):
     the 256 x 256 products stay rocBLAS GEMMs (torch.mm / bmm into preallocated outputs) and
-    everything between two GEMMs is one launch of tools/sac_fused.hip -- ~30 launches per
+    everything between two GEMMs is one launch of tools/sac_fused.hip -- 21 launches per
     update instead of autograd's ~100, each of which paid the dependent-kernel boundary.
     Same parameters, replay buffer, HipAdam optimizers, step count and RNG draws (torch.rand
     for the sample, torch.randn for the squashed Gaussian, in SAC.update's order), so an
