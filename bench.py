@@ -580,7 +580,7 @@ def c5_learner_leg(b, W, dev, steps, warm):
     import sac_torch
     torch.backends.cuda.preferred_blas_library("cublas")
     os.environ["DISABLE_ADDMM_CUDA_LT"] = "1"
-    # FusedSAC: the update's forward / backward written out (tools/sac_fused.hip, 21 launches
+    # FusedSAC: the update's forward / backward written out (tools/sac_fused.hip, 19 launches
     # per update instead of ~100); SAC_FUSED=0 = the autograd update
     cls = sac_torch.FusedSAC if os.environ.get("SAC_FUSED", "1") == "1" else sac_torch.SAC
     sac = cls(b.obs_dim, b.act_dim, dev, group=None, seed=0, lr=1e-3)

@@ -279,9 +279,10 @@ def test_fused_sac_loop_is_graph_capturable():
 
 
 def test_fused_sac_philox_noise():
-    """FusedSAC's default noise (tools/sac_fused.hip noise_kernel: Philox4x32-10, one launch
-    per update for the replay uniforms, the squashed Gaussian's normals and an attached
-    action sample's): the right distributions (moments over many draws), new numbers every
+    """FusedSAC's default noise (tools/sac_fused.hip noise_sample_kernel: Philox4x32-10, one
+    launch per update for the replay uniforms -- and the replay rows they draw -- the squashed
+    Gaussian's normals and an attached action sample's): the rows torch's gather of those
+    uniforms gives, the right distributions (moments over many draws), new numbers every
     update (the launch counter advances on the device, so graph replays draw anew), and the
     same numbers for the same seed."""
     dev = torch.device("cuda", 0)
@@ -294,6 +295,9 @@ def test_fused_sac_philox_noise():
         us, es, ps = [], [], []
         for _ in range(20):
             s.update(losses=False)
+            # the replay rows the same launch gathered: torch's index arithmetic on its uniforms
+            idx = torch.clamp((s._u * s.size.float()).long(), max=s.cap - 1)
+            assert torch.equal(s._rows, s.buf[idx])
             us.append(s._u.clone())
             es.append(s._eps.clone())
             ps.append(pe.clone())

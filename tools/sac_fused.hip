@@ -6,11 +6,12 @@
 // squashed Gaussian as separate launches), each paying the ~1.5 us dependent-kernel boundary
 // (MI355X_MICROARCH.md 'boundary').  FusedSAC writes the forward and backward passes out and
 // keeps only the 256 x 256 products as rocBLAS GEMMs (torch.mm / bmm with out=); everything
-// between two GEMMs is one of the kernels below, so an update is 21 launches:
+// between two GEMMs is one of the kernels below, so an update is 19 launches:
 //
 //   in_layer     relu(x W + b) for a layer whose K is the observation (+ action) width
 //   in_layer_pair  the actor's and the online critics' first layers in one launch
-//   noise        the update's uniforms and normals (and the next action sample's), Philox
+//   noise_sample the update's uniforms and normals (and the next action sample's), Philox,
+//                then the replay rows the uniforms draw and the Adam step-count tick
 //   actor_head   h1 = relu(p1 + b1), mu / log_std heads, SB3's squashed Gaussian (a, logp),
 //                and on the next-observation rows the target critics' first layer
 //   critic_head  g1 = relu(p1 + b1), q = g1 w2 + b2 for both critics, then per mode the TD
@@ -22,8 +23,8 @@
 //                     gradients (column sums)
 //   actor_bwd_head    the critics' action gradient, the squashed Gaussian's backward and
 //                     dh1 = (dmu Wmu + dlsr Wls)(h1 > 0)
-//   actor_bwd_cols    the heads' and b1's gradients and d log_alpha (column sums)
-//   actor_bwd_in      the first layer's gradients from dh0 (h0 > 0)
+//   actor_bwd_in      the first layer's gradients from dh0 (h0 > 0), then the heads' and b1's
+//                     gradients and d log_alpha (column sums, actor_cols)
 //   (SB3's polyak_update of the target critics runs inside the critic's Adam launch,
 //   tools/sac_adam.hip sac_adam_step_polyak)
 //
@@ -150,6 +151,52 @@ __global__ __launch_bounds__(1024) void noise_kernel(unsigned long long* __restr
   }
   __syncthreads();
   if (threadIdx.x == 0) launch[0] = L + 1;
+}
+
+// noise_kernel followed, in the same workgroup, by the replay sample those uniforms draw
+// (sac_adam.hip replay_sample_kernel's index arithmetic: idx = min(int(u * size), cap - 1))
+// and the optimizers' step-count tick -- the update's first three launches in one
+__global__ __launch_bounds__(1024) void noise_sample_kernel(
+    unsigned long long* __restrict__ launch, unsigned long long seed, float* __restrict__ u, int nu,
+    float* __restrict__ e1, int n1, float* __restrict__ e2, int n2, const float* __restrict__ buf,
+    long long cap, int W, const long long* __restrict__ size, float* __restrict__ rows,
+    float* __restrict__ step) {
+  __shared__ float us[1024];
+  const unsigned long long L = launch[0];
+  const int total = nu + n1 + n2;
+  for (int i = threadIdx.x; 2 * i < total + 1; i += blockDim.x) {
+    uint32_t c[4] = {(uint32_t)L, (uint32_t)(L >> 32), (uint32_t)i, 0x53414331u};
+    philox10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+    const float v1 = 1.0f - u01(c[0]), v2 = u01(c[1]);
+    const float v3 = 1.0f - u01(c[2]), v4 = u01(c[3]);
+    const float g1 = sqrtf(-2.0f * logf(v1)) * cospif(2.0f * v2);
+    const float g2 = sqrtf(-2.0f * logf(v3)) * cospif(2.0f * v4);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int o = 2 * i + h;
+      if (o < nu) {
+        const float uv = h == 0 ? u01(c[0]) : u01(c[1]);
+        u[o] = uv;
+        us[o] = uv;
+      } else if (o < nu + n1) {
+        e1[o - nu] = h == 0 ? g1 : g2;
+      } else if (o < total) {
+        e2[o - nu - n1] = h == 0 ? g1 : g2;
+      }
+    }
+  }
+  __syncthreads();
+  const long long sz = size[0];
+  for (long long i = threadIdx.x; i < (long long)nu * W; i += blockDim.x) {
+    const int b = (int)(i / W), col = (int)(i - (long long)b * W);
+    long long idx = (long long)(us[b] * (float)sz);
+    if (idx > cap - 1) idx = cap - 1;
+    rows[i] = buf[(size_t)idx * W + col];
+  }
+  if (threadIdx.x == 0) {
+    launch[0] = L + 1;
+    step[0] += 1.0f;                         // HipAdam.tick (t.add_(1.0)): read only after this launch
+  }
 }
 
 // one wave per row: h1 = relu(p1 + b1); mu = h1 Wmu^T + bmu; lsr = h1 Wls^T + bls;
@@ -559,12 +606,12 @@ __global__ __launch_bounds__(256) void actor_bwd_head_kernel(
 // groups as above); workgroup 0's waves 1-3 reduce the per-row terms, 4 rows per lane and a
 // fixed shuffle tree: dbmu[j], dbls[j] and d log_alpha = -mean_r(logp + target_entropy) (SB3's
 // ent_coef_loss = -(log_alpha * (logp + target_entropy).detach()).mean())
-__global__ __launch_bounds__(256) void actor_bwd_cols_kernel(
+__device__ __forceinline__ void actor_cols(
     const float* __restrict__ dmu, const float* __restrict__ dlsr, const float* __restrict__ h1,
     const float* __restrict__ dh1, const float* __restrict__ logp, float target_entropy, int R,
     int A, float* __restrict__ dwmu, float* __restrict__ dwls, float* __restrict__ db1,
-    float* __restrict__ dbmu, float* __restrict__ dbls, float* __restrict__ dlog_alpha) {
-  __shared__ float lds[9][NRG][CPB];
+    float* __restrict__ dbmu, float* __restrict__ dbls, float* __restrict__ dlog_alpha,
+    float (*lds)[NRG][CPB]) {
   const int u = blockIdx.x * CPB + threadIdx.x % CPB;
   int r0, r1;
   group_rows(R, r0, r1);
@@ -625,9 +672,15 @@ __global__ __launch_bounds__(256) void actor_bwd_cols_kernel(
 
 // m = dh0 (h0 > 0); dW0[u][k] = sum_r m x[r][k] (torch layout), db0[u] = sum_r m (x staged
 // in LDS as above)
+// dmu != nullptr: then the heads' column sums (actor_cols) in the same launch (its last step: the heads'
+// and b1's column sums, d log_alpha; same rows, order and groups)
 __global__ __launch_bounds__(256) void actor_bwd_in_kernel(
     const float* __restrict__ dh0, const float* __restrict__ h0, const float* __restrict__ x,
-    int ldx, int K, int R, float* __restrict__ dw0, float* __restrict__ db0) {
+    int ldx, int K, int R, float* __restrict__ dw0, float* __restrict__ db0,
+    const float* __restrict__ dmu, const float* __restrict__ dlsr, const float* __restrict__ h1,
+    const float* __restrict__ dh1, const float* __restrict__ logp, float target_entropy, int A,
+    float* __restrict__ dwmu, float* __restrict__ dwls, float* __restrict__ db1,
+    float* __restrict__ dbmu, float* __restrict__ dbls, float* __restrict__ dlog_alpha) {
   __shared__ float lds[9][NRG][CPB];
   __shared__ float xl[kXR][kXK + 1];
   const int u = blockIdx.x * CPB + threadIdx.x % CPB;
@@ -662,6 +715,8 @@ __global__ __launch_bounds__(256) void actor_bwd_in_kernel(
       if (k0 == 0) db0[u] = v[8];
     }
   }
+  if (dmu) actor_cols(dmu, dlsr, h1, dh1, logp, target_entropy, R, A, dwmu, dwls, db1, dbmu, dbls,
+                      dlog_alpha, lds);
 }
 
 }  // namespace
@@ -708,6 +763,16 @@ int32_t sf_in_layer_pair(const float* xa, const float* xa_hi, int32_t split, int
   const int R = R1 > R2 ? R1 : R2;
   SF_LAUNCH(in_layer_pair_kernel, dim3(R, 3), dim3(H), xa, xa_hi, split, lda, Ka, R1, w1, b1, out1,
             ya, ldya, Kya, yb, ldyb, Kyb, R2, w2, b2, out2);
+}
+
+int32_t sf_noise_sample(unsigned long long* launch, unsigned long long seed, float* u, int32_t nu,
+                        float* e1, int32_t n1, float* e2, int32_t n2, const float* buf, long long cap,
+                        int32_t W, const long long* size, float* rows, float* step, void* stream) {
+  if (!launch || nu < 1 || nu > 1024 || n1 < 0 || n2 < 0 || !u || (n1 && !e1) || (n2 && !e2) || !buf ||
+      cap < 1 || W < 1 || !size || !rows || !step)
+    return -1;
+  SF_LAUNCH(noise_sample_kernel, dim3(1), dim3(1024), launch, seed, u, nu, e1, n1, e2, n2, buf, cap, W, size,
+            rows, step);
 }
 
 int32_t sf_noise(unsigned long long* launch, unsigned long long seed, float* u, int32_t nu, float* e1,
@@ -765,22 +830,18 @@ int32_t sf_td_critic_head(const float* p1, const float* tb1, const float* tw2, c
             W, col_r, col_d, gamma, log_alpha, logp, y, g1, q_out, dq, lossp, dg1);
 }
 
-int32_t sf_actor_bwd_cols(const float* dmu, const float* dlsr, const float* h1, const float* dh1,
-                          const float* logp, float target_entropy, int32_t R, int32_t A, float* dwmu,
-                          float* dwls, float* db1, float* dbmu, float* dbls, float* dlog_alpha,
-                          void* stream) {
-  if (!dmu || !dlsr || !h1 || !dh1 || !logp || !dwmu || !dwls || !db1 || !dbmu || !dbls || !dlog_alpha ||
-      R < 1 || A < 1 || A > 4)
-    return -1;
-  SF_LAUNCH(actor_bwd_cols_kernel, dim3(H / CPB), dim3(256), dmu, dlsr, h1, dh1, logp, target_entropy, R, A,
-            dwmu, dwls, db1, dbmu, dbls, dlog_alpha);
-}
-
 int32_t sf_actor_bwd_in(const float* dh0, const float* h0, const float* x, int32_t ldx, int32_t K,
-                        int32_t R, float* dw0, float* db0, void* stream) {
+                        int32_t R, float* dw0, float* db0, const float* dmu, const float* dlsr,
+                        const float* h1, const float* dh1, const float* logp, float target_entropy,
+                        int32_t A, float* dwmu, float* dwls, float* db1, float* dbmu, float* dbls,
+                        float* dlog_alpha, void* stream) {
+  if (dmu && (!dlsr || !h1 || !dh1 || !logp || !dwmu || !dwls || !db1 || !dbmu || !dbls || !dlog_alpha ||
+              A < 1 || A > 4))
+    return -1;
   if (!dh0 || !h0 || !x || !dw0 || !db0 || R < 1 || K < 1) return -1;
   if (R > kXR || K > kXK || R > NRG * RPG) return -1;
-  SF_LAUNCH(actor_bwd_in_kernel, dim3(H / CPB), dim3(256), dh0, h0, x, ldx, K, R, dw0, db0);
+  SF_LAUNCH(actor_bwd_in_kernel, dim3(H / CPB), dim3(256), dh0, h0, x, ldx, K, R, dw0, db0, dmu, dlsr, h1,
+            dh1, logp, target_entropy, A, dwmu, dwls, db1, dbmu, dbls, dlog_alpha);
 }
 
 }  // extern "C"

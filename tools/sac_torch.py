@@ -526,7 +526,7 @@ FUSED_LIB = os.path.join(_HERE, "_lib", "libsacfused.so")
 class FusedSAC(SAC):
     """SAC.update with its forward and backward passes written out (one rank, the HIP path):
     the 256 x 256 products stay rocBLAS GEMMs (torch.mm / bmm into preallocated outputs) and
-    everything between two GEMMs is one launch of tools/sac_fused.hip -- 21 launches per
+    everything between two GEMMs is one launch of tools/sac_fused.hip -- 19 launches per
     update instead of autograd's ~100, each of which paid the dependent-kernel boundary.
     Same parameters, replay buffer, HipAdam optimizers, step count and RNG draws (torch.rand
     for the sample, torch.randn for the squashed Gaussian, in SAC.update's order), so an
@@ -556,8 +556,8 @@ class FusedSAC(SAC):
                 raise RuntimeError(f"{FUSED_LIB} missing: run __graft_entry__.build()")
             lib = ctypes.CDLL(FUSED_LIB)
             for name in ("sf_in_layer", "sf_actor_head", "sf_critic_head",
-                         "sf_critic_bwd_in", "sf_actor_bwd_head", "sf_actor_bwd_cols", "sf_actor_bwd_in",
-                         "sf_td_critic_head", "sf_in_layer_pair", "sf_noise"):
+                         "sf_critic_bwd_in", "sf_actor_bwd_head", "sf_actor_bwd_in",
+                         "sf_td_critic_head", "sf_in_layer_pair", "sf_noise", "sf_noise_sample"):
                 getattr(lib, name).restype = ctypes.c_int32
             FusedSAC._lib = lib
         HipAdam([torch.zeros(1, device=self.dev)], 0.0)         # loads sac_adam.hip's library
@@ -629,20 +629,23 @@ class FusedSAC(SAC):
         L = HipAdam._lib
         f = self._call
         if self.noise == "philox":
+            # the update's random numbers, the replay sample they draw and the shared Adam step
+            # count's tick (opt_q.tick()) in one launch
             pe = self._pol_eps
-            f("sf_noise", self._launch, ctypes.c_uint64(self._seed), self._u, B, self._eps, 2 * B * A,
-              pe, 0 if pe is None else pe.numel())
+            f("sf_noise_sample", self._launch, ctypes.c_uint64(self._seed), self._u, B, self._eps,
+              2 * B * A, pe, 0 if pe is None else pe.numel(), self.buf, ctypes.c_longlong(self.cap), W,
+              self.size, rows, self.opt_q.t)
         else:
             torch.rand(B, device=self.dev, out=self._u)
-        # the sample, with the shared Adam step count advanced in the same launch (opt_q.tick())
-        rc = L.sac_replay_sample_tick(ctypes.c_void_p(self.buf.data_ptr()), self.cap, W,
-                                      ctypes.c_void_p(self._u.data_ptr()), B,
-                                      ctypes.c_void_p(self.size.data_ptr()), ctypes.c_void_p(rows.data_ptr()),
-                                      ctypes.c_void_p(self.opt_q.t.data_ptr()),
-                                      ctypes.c_void_p(torch.cuda.current_stream(self.dev).cuda_stream))
-        if rc != 0:
-            raise RuntimeError(f"sac_replay_sample_tick failed ({rc})")
-        if self.noise == "torch":
+            # the sample, with the shared Adam step count advanced in the same launch
+            rc = L.sac_replay_sample_tick(ctypes.c_void_p(self.buf.data_ptr()), self.cap, W,
+                                          ctypes.c_void_p(self._u.data_ptr()), B,
+                                          ctypes.c_void_p(self.size.data_ptr()),
+                                          ctypes.c_void_p(rows.data_ptr()),
+                                          ctypes.c_void_p(self.opt_q.t.data_ptr()),
+                                          ctypes.c_void_p(torch.cuda.current_stream(self.dev).cuda_stream))
+            if rc != 0:
+                raise RuntimeError(f"sac_replay_sample_tick failed ({rc})")
             torch.randn((2 * B, A), device=self.dev, out=self._eps)
         o = rows                                    # columns 0..od of the row
         a = rows[:, od:]                            # the stored action (ld = W)
@@ -688,12 +691,13 @@ class FusedSAC(SAC):
         f("sf_actor_bwd_head", None, self._dlogp, self._mu[B:], self._lsr[B:], self._eps[B:], ap,
           h1b, lat.mu.weight, lat.log_std.weight, B, A, self._dmu, self._dlsr, self._dh1,
           self._dg0, self._g0, q.w0, ic, od)
-        f("sf_actor_bwd_cols", self._dmu, self._dlsr, h1b, self._dh1, lp, float(self.target_entropy), B, A,
-          lat.mu.weight.grad, lat.log_std.weight.grad, la_[2].bias.grad, lat.mu.bias.grad,
-          lat.log_std.bias.grad, self.log_alpha.grad)
         torch.mm(self._dh1.t(), h0b, out=la_[2].weight.grad)
         torch.mm(self._dh1, la_[2].weight, out=self._dh0)
-        f("sf_actor_bwd_in", self._dh0, h0b, o, W, od, B, la_[0].weight.grad, la_[0].bias.grad)
+        # (with the heads' and b1's column sums and d log_alpha in the same launch)
+        f("sf_actor_bwd_in", self._dh0, h0b, o, W, od, B, la_[0].weight.grad, la_[0].bias.grad,
+          self._dmu, self._dlsr, h1b, self._dh1, lp, float(self.target_entropy), A,
+          lat.mu.weight.grad, lat.log_std.weight.grad, la_[2].bias.grad, lat.mu.bias.grad,
+          lat.log_std.bias.grad, self.log_alpha.grad)
         if self.world > 1:
             self._allreduce(list(self.actor.parameters()) + [self.log_alpha])
         self.opt_a.step()                            # actor + log_alpha in one launch
