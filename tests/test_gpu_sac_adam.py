@@ -219,8 +219,8 @@ def _sac_pair(cls, obs_dim, act_dim, dev, **kw):
     return s
 
 
-@pytest.mark.parametrize("obs_dim,act_dim", [(4, 1), (40, 2)])
-def test_fused_sac_update_matches_autograd_update(obs_dim, act_dim):
+@pytest.mark.parametrize("obs_dim,act_dim,gemm", [(4, 1, "mfma"), (40, 2, "mfma"), (4, 1, "blas")])
+def test_fused_sac_update_matches_autograd_update(obs_dim, act_dim, gemm):
     """FusedSAC (tools/sac_fused.hip: the forward / backward written out, rocBLAS for the
     256 x 256 products) against SAC.update on the autograd + HipAdam path: same seed, same
     buffer, same RNG draws (FusedSAC's noise="torch": torch.rand / torch.randn in SAC.update's
@@ -230,11 +230,14 @@ def test_fused_sac_update_matches_autograd_update(obs_dim, act_dim):
     parameter and log_alpha within 1e-4 relative + 1e-4 absolute -- a tenth of one Adam step
     (lr 1e-3): Adam's m / sqrt(v) turns a rounding-level difference of a near-zero gradient
     into up to a step's difference of its parameter.  (3) The losses of the last update close.
-    Descent's shape (obs 4, action 1) and Merge's (obs 40, action 2)."""
+    Descent's shape (obs 4, action 1) and Merge's (obs 40, action 2); the products on the
+    MFMA kernel (default) and on rocBLAS."""
     dev = torch.device("cuda", 0)
     grads, out, losses = [], [], []
     for cls, kw in ((sac_torch.SAC, {}), (sac_torch.FusedSAC, {"noise": "torch"})):
         s = _sac_pair(cls, obs_dim, act_dim, dev, **kw)
+        if cls is sac_torch.FusedSAC:
+            s.gemm = gemm
         params = list(s.actor.parameters()) + list(s.q.parameters()) + [s.log_alpha]
         torch.manual_seed(5)
         s.update()
@@ -419,3 +422,26 @@ def _free_port():
     port = so.getsockname()[1]
     so.close()
     return port
+
+
+@pytest.mark.parametrize("ta,tb", [(0, 0), (1, 0), (0, 1), (1, 1)])
+def test_mfma_gemm256_matches_float64(ta, tb):
+    """tools/sac_fused.hip gemm256_kernel (v_mfma_f32_16x16x4_f32, K split over four waves):
+    every transpose form, batched, M = 256 and 512, against float64 products -- within fp32
+    accumulation error (2e-6 of the sum of |terms| per entry)."""
+    import ctypes
+    dev = torch.device("cuda", 0)
+    s = _sac_pair(sac_torch.FusedSAC, 4, 1, dev)
+    g = torch.Generator(device=dev).manual_seed(3)
+    for M, batch in ((256, 1), (512, 1), (256, 4)):
+        a = torch.randn((batch, 256, M) if ta else (batch, M, 256), generator=g, device=dev)
+        b = torch.randn((batch, 256, 256), generator=g, device=dev)
+        c = torch.zeros((batch, M, 256), device=dev)
+        s._call("sf_gemm", ta, tb, a, b, c, M, batch, ctypes.c_longlong(a[0].numel()),
+                ctypes.c_longlong(b[0].numel()), ctypes.c_longlong(c[0].numel()))
+        torch.cuda.synchronize()
+        x = (a.transpose(1, 2) if ta else a).double()
+        y = (b.transpose(1, 2) if tb else b).double()
+        want = torch.bmm(x, y)
+        bound = torch.bmm(x.abs(), y.abs()) * 2e-6 + 1e-30
+        assert bool(((c.double() - want).abs() <= bound).all()), float(((c.double() - want).abs() / bound).max())

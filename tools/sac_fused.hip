@@ -4,8 +4,8 @@
 // at batch 256 through 256-wide MLPs is ~100 small kernels as torch autograd runs it
 // (bias copies, ReLU and its backward, bias-gradient reductions, the loss terms and the
 // squashed Gaussian as separate launches), each paying the ~1.5 us dependent-kernel boundary
-// (MI355X_MICROARCH.md 'boundary').  FusedSAC writes the forward and backward passes out and
-// keeps only the 256 x 256 products as rocBLAS GEMMs (torch.mm / bmm with out=); everything
+// (MI355X_MICROARCH.md 'boundary').  FusedSAC writes the forward and backward passes out; the
+// 256 x 256 products are gemm256_kernel launches (below; rocBLAS with SAC_GEMM=blas); everything
 // between two GEMMs is one of the kernels below, so an update is 19 launches:
 //
 //   in_layer     relu(x W + b) for a layer whose K is the observation (+ action) width
@@ -719,6 +719,47 @@ __global__ __launch_bounds__(256) void actor_bwd_in_kernel(
                       dlog_alpha, lds);
 }
 
+// C[b] = op(A[b]) op(B[b]) for the update's 256-wide products: op(A) is M x 256 (A row-major
+// [M][256], or [256][M] transposed: TA), op(B) 256 x 256 (B row-major [256][256], or its
+// transpose: TB), K = 256.  v_mfma_f32_16x16x4_f32 (f32 in, exact products, f32 accumulate):
+// a workgroup of four waves takes one 16 x 16 tile of C, wave w the k range [64 w, 64 w + 64)
+// in 16 steps (lane l: row l & 15 of op(A) / column l & 15 of op(B), k = 64 w + 16 (l >> 4)
+// + step), then the four partial tiles are added in wave order through LDS -- M / 16 x 16
+// tiles x batch workgroups, a short dependent chain per wave instead of rocBLAS's K loop.
+template <bool TA, bool TB>
+__global__ __launch_bounds__(256) void gemm256_kernel(const float* __restrict__ A,
+                                                      const float* __restrict__ Bm,
+                                                      float* __restrict__ C, int M, long long sA,
+                                                      long long sB, long long sC) {
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  __shared__ float red[4][64][4];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int col0 = blockIdx.x * 16, row0 = blockIdx.y * 16;
+  const float* a = A + (size_t)blockIdx.z * sA;
+  const float* b = Bm + (size_t)blockIdx.z * sB;
+  const int i = lane & 15, g = lane >> 4;
+  const int k0 = 64 * w + 16 * g;
+  float av[16], bv[16];
+#pragma unroll
+  for (int m = 0; m < 16; ++m) {
+    av[m] = TA ? a[(size_t)(k0 + m) * M + row0 + i] : a[(size_t)(row0 + i) * H + k0 + m];
+    bv[m] = TB ? b[(size_t)(col0 + i) * H + k0 + m] : b[(size_t)(k0 + m) * H + col0 + i];
+  }
+  f4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+  for (int m = 0; m < 16; ++m) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[m], bv[m], acc, 0, 0, 0);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) red[w][lane][r] = acc[r];
+  __syncthreads();
+  if (w != 0) return;
+  float* c = C + (size_t)blockIdx.z * sC;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const float v = ((red[0][lane][r] + red[1][lane][r]) + red[2][lane][r]) + red[3][lane][r];
+    c[(size_t)(row0 + g * 4 + r) * H + col0 + i] = v;
+  }
+}
+
 }  // namespace
 
 #define SF_LAUNCH(kern, grid, block, ...)                                                    \
@@ -728,6 +769,16 @@ __global__ __launch_bounds__(256) void actor_bwd_in_kernel(
   } while (0)
 
 extern "C" {
+
+int32_t sf_gemm(int32_t ta, int32_t tb, const float* A, const float* B, float* C, int32_t M, int32_t batch,
+                long long sA, long long sB, long long sC, void* stream) {
+  if (!A || !B || !C || M < 16 || (M % 16) != 0 || batch < 1) return -1;
+  const dim3 grid(H / 16, M / 16, batch);
+  if (ta && tb) SF_LAUNCH((gemm256_kernel<true, true>), grid, dim3(256), A, B, C, M, sA, sB, sC);
+  if (ta) SF_LAUNCH((gemm256_kernel<true, false>), grid, dim3(256), A, B, C, M, sA, sB, sC);
+  if (tb) SF_LAUNCH((gemm256_kernel<false, true>), grid, dim3(256), A, B, C, M, sA, sB, sC);
+  SF_LAUNCH((gemm256_kernel<false, false>), grid, dim3(256), A, B, C, M, sA, sB, sC);
+}
 
 int32_t sf_in_layer(const float* xa, const float* xa_hi, int32_t split, int32_t lda, int32_t Ka,
                     const float* xb, int32_t ldb, int32_t Kb, int32_t R, int32_t nC, const float* w,

@@ -525,7 +525,8 @@ FUSED_LIB = os.path.join(_HERE, "_lib", "libsacfused.so")
 
 class FusedSAC(SAC):
     """SAC.update with its forward and backward passes written out (one rank, the HIP path):
-    the 256 x 256 products stay rocBLAS GEMMs (torch.mm / bmm into preallocated outputs) and
+    the 256 x 256 products are MFMA launches of tools/sac_fused.hip gemm256_kernel (SAC_GEMM=blas:
+    rocBLAS, torch.mm / bmm into preallocated outputs) and
     everything between two GEMMs is one launch of tools/sac_fused.hip -- 19 launches per
     update instead of autograd's ~100, each of which paid the dependent-kernel boundary.
     Same parameters, replay buffer, HipAdam optimizers, step count and RNG draws (torch.rand
@@ -541,6 +542,9 @@ class FusedSAC(SAC):
         # noise: "philox" = the update's uniforms and normals (and an attached action sample's)
         # from one launch of tools/sac_fused.hip; "torch" = torch.rand / torch.randn in
         # SAC.update's order (the equivalence test draws both updates' numbers that way)
+        # gemm: "mfma" = the update's 256-wide products by tools/sac_fused.hip gemm256_kernel
+        # (batch 256 only; v_mfma_f32_16x16x4_f32, split K over four waves), "blas" = rocBLAS
+        self.gemm = os.environ.get("SAC_GEMM", "mfma")
         self.noise = noise or os.environ.get("SAC_NOISE", "philox")
         if self.noise not in ("philox", "torch"):
             raise ValueError("FusedSAC: noise is 'philox' or 'torch'")
@@ -557,7 +561,8 @@ class FusedSAC(SAC):
             lib = ctypes.CDLL(FUSED_LIB)
             for name in ("sf_in_layer", "sf_actor_head", "sf_critic_head",
                          "sf_critic_bwd_in", "sf_actor_bwd_head", "sf_actor_bwd_in",
-                         "sf_td_critic_head", "sf_in_layer_pair", "sf_noise", "sf_noise_sample"):
+                         "sf_td_critic_head", "sf_in_layer_pair", "sf_noise", "sf_noise_sample",
+                         "sf_gemm"):
                 getattr(lib, name).restype = ctypes.c_int32
             FusedSAC._lib = lib
         HipAdam([torch.zeros(1, device=self.dev)], 0.0)         # loads sac_adam.hip's library
@@ -614,6 +619,21 @@ class FusedSAC(SAC):
         if rc != 0:
             raise RuntimeError(f"{name} failed ({rc})")
 
+    def _mm(self, ta, tb, a, b, c, M, batch=1):
+        """c[i] = op(a[i]) op(b[i]) for the update's products (K = N = 256): gemm256_kernel at
+        batch 256, rocBLAS (torch.mm / bmm into c) otherwise.  a, b, c: the operands as stored
+        (op = transpose where ta / tb)."""
+        if self.gemm == "mfma" and self.batch == 256:
+            sa = a.shape[-2] * a.shape[-1] if batch > 1 else 0
+            sb = b.shape[-2] * b.shape[-1] if batch > 1 else 0
+            sc = c.shape[-2] * c.shape[-1] if batch > 1 else 0
+            self._call("sf_gemm", int(ta), int(tb), a, b, c, M, batch, ctypes.c_longlong(sa),
+                       ctypes.c_longlong(sb), ctypes.c_longlong(sc))
+            return
+        x = a.transpose(-2, -1) if ta else a
+        y = b.transpose(-2, -1) if tb else b
+        (torch.bmm if batch > 1 else torch.mm)(x, y, out=c)
+
     def update(self, losses=True):
         """SAC.update's gradient step (same order of evaluation; with noise="torch" the same
         RNG draws)."""
@@ -657,21 +677,21 @@ class FusedSAC(SAC):
         # (the online critics' first layer on [o, a] in the same launch as the actor's)
         f("sf_in_layer_pair", o2, o, B, W, od, 2 * B, la_[0].weight, la_[0].bias, self._h0,
           o, W, od, a, W, A, B, q.w0, q.b0, self._g0)
-        torch.mm(self._h0, la_[2].weight.t(), out=self._p1a)
+        self._mm(0, 1, self._h0, la_[2].weight, self._p1a, 2 * B)
         # (the target critics' first layer on [o2, a2] inside the actor's head launch)
         f("sf_actor_head", self._p1a, la_[2].bias, lat.mu.weight, lat.mu.bias, lat.log_std.weight,
           lat.log_std.bias, self._eps, 2 * B, A, self._h1, self._mu, self._lsr, act, logp,
           B, o2, W, od, qt.w0, qt.b0, self._g04[0:2])
         # ---- TD target from the target critics on [o2, a2] and the critics on [o, a]: one
         # bmm over the four second layers, one head (y, then the twin MSE's gradient) ---------
-        torch.bmm(self._g04, self._w1, out=self._p14)
+        self._mm(0, 0, self._g04, self._w1, self._p14, B, 4)
         f("sf_td_critic_head", self._p14, qt.b1, qt.w2, qt.b2, q.b1, q.w2, q.b2, B, rows, W, od + A,
           W - 1, self.gamma, self.log_alpha, logp, self._y, self._g1, self._q, self._dq, self._lossq,
           self._dg1)
         # ---- the critics' backward and step (polyak of the targets in the same launch) ---------
         # (dg1 came from the TD head's launch; the head's column sums ride in critic_bwd_in)
-        torch.bmm(self._g0.transpose(1, 2), self._dg1, out=q.w1.grad)
-        torch.bmm(self._dg1, q.w1.transpose(1, 2), out=self._dg0)
+        self._mm(1, 0, self._g0, self._dg1, q.w1.grad, H, 2)
+        self._mm(0, 1, self._dg1, q.w1, self._dg0, B, 2)
         f("sf_critic_bwd_in", self._dg0, self._g0, o, W, od, a, W, A, B, q.w0.grad, q.b0.grad,
           self._g1, self._dq, q.w2, q.w2.grad, q.b1.grad, q.b2.grad)
         if self.world > 1:
@@ -680,19 +700,19 @@ class FusedSAC(SAC):
         # ---- actor loss through the updated critics on [o, ap] (critics frozen) ----------------
         ap, lp = act[B:], logp[B:]
         f("sf_in_layer", o, None, B, W, od, ap, A, A, B, 2, q.w0, 1, q.b0, self._g0)
-        torch.bmm(self._g0, q.w1, out=self._p1c)
+        self._mm(0, 0, self._g0, q.w1, self._p1c, B, 2)
         # (the head's backward, dg1, in the same launch: g1 itself is not needed)
         f("sf_critic_head", self._p1c, q.b1, q.w2, q.b2, B, 2, None, W, 0, 0, self.gamma,
           self.log_alpha, lp, None, None, self._q, self._dq, self._dlogp, self._lossa, self._dg1)
-        torch.bmm(self._dg1, q.w1.transpose(1, 2), out=self._dg0)
+        self._mm(0, 1, self._dg1, q.w1, self._dg0, B, 2)
         # ---- actor backward (the o half of the pass; the critics' action gradient computed in
         # its head launch), entropy coefficient, their step ----------------------------------
         h0b, h1b = self._h0[B:], self._h1[B:]
         f("sf_actor_bwd_head", None, self._dlogp, self._mu[B:], self._lsr[B:], self._eps[B:], ap,
           h1b, lat.mu.weight, lat.log_std.weight, B, A, self._dmu, self._dlsr, self._dh1,
           self._dg0, self._g0, q.w0, ic, od)
-        torch.mm(self._dh1.t(), h0b, out=la_[2].weight.grad)
-        torch.mm(self._dh1, la_[2].weight, out=self._dh0)
+        self._mm(1, 0, self._dh1, h0b, la_[2].weight.grad, H)
+        self._mm(0, 0, self._dh1, la_[2].weight, self._dh0, B)
         # (with the heads' and b1's column sums and d log_alpha in the same launch)
         f("sf_actor_bwd_in", self._dh0, h0b, o, W, od, B, la_[0].weight.grad, la_[0].bias.grad,
           self._dmu, self._dlsr, h1b, self._dh1, lp, float(self.target_entropy), A,
