@@ -607,7 +607,8 @@ def c5_learner_leg(b, W, dev, steps, warm):
             "critic_loss": float(lq), "actor_loss": float(la),
             "learner": "SB3 SAC restated (tools/sac_torch.py): twin critics + actor 256-256, "
                        "batch 256, one update per vector step, HIP graph",
-            "update": type(sac).__name__, "iters_per_graph": iters, "timed_iterations": steps}
+            "update": type(sac).__name__, "products": getattr(sac, "gemm", "torch"),
+            "noise": getattr(sac, "noise", "torch"), "iters_per_graph": iters, "timed_iterations": steps}
 
 
 def bench_descent_sac(args):

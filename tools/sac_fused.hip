@@ -726,28 +726,33 @@ __global__ __launch_bounds__(256) void actor_bwd_in_kernel(
 // in 16 steps (lane l: row l & 15 of op(A) / column l & 15 of op(B), k = 64 w + 16 (l >> 4)
 // + step), then the four partial tiles are added in wave order through LDS -- M / 16 x 16
 // tiles x batch workgroups, a short dependent chain per wave instead of rocBLAS's K loop.
+#ifndef SF_GEMM_WAVES
+#define SF_GEMM_WAVES 4
+#endif
+constexpr int kGW = SF_GEMM_WAVES;           // waves per tile (the K split)
+constexpr int kGS = H / kGW / 4;             // MFMA steps per wave
 template <bool TA, bool TB>
-__global__ __launch_bounds__(256) void gemm256_kernel(const float* __restrict__ A,
-                                                      const float* __restrict__ Bm,
-                                                      float* __restrict__ C, int M, long long sA,
-                                                      long long sB, long long sC) {
+__global__ __launch_bounds__(64 * kGW) void gemm256_kernel(const float* __restrict__ A,
+                                                           const float* __restrict__ Bm,
+                                                           float* __restrict__ C, int M, long long sA,
+                                                           long long sB, long long sC) {
   typedef float f4 __attribute__((ext_vector_type(4)));
-  __shared__ float red[4][64][4];
+  __shared__ float red[kGW][64][4];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int col0 = blockIdx.x * 16, row0 = blockIdx.y * 16;
   const float* a = A + (size_t)blockIdx.z * sA;
   const float* b = Bm + (size_t)blockIdx.z * sB;
   const int i = lane & 15, g = lane >> 4;
-  const int k0 = 64 * w + 16 * g;
-  float av[16], bv[16];
+  const int k0 = (H / kGW) * w + kGS * g;
+  float av[kGS], bv[kGS];
 #pragma unroll
-  for (int m = 0; m < 16; ++m) {
+  for (int m = 0; m < kGS; ++m) {
     av[m] = TA ? a[(size_t)(k0 + m) * M + row0 + i] : a[(size_t)(row0 + i) * H + k0 + m];
     bv[m] = TB ? b[(size_t)(col0 + i) * H + k0 + m] : b[(size_t)(k0 + m) * H + col0 + i];
   }
   f4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
-  for (int m = 0; m < 16; ++m) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[m], bv[m], acc, 0, 0, 0);
+  for (int m = 0; m < kGS; ++m) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[m], bv[m], acc, 0, 0, 0);
 #pragma unroll
   for (int r = 0; r < 4; ++r) red[w][lane][r] = acc[r];
   __syncthreads();
@@ -755,7 +760,9 @@ __global__ __launch_bounds__(256) void gemm256_kernel(const float* __restrict__ 
   float* c = C + (size_t)blockIdx.z * sC;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
-    const float v = ((red[0][lane][r] + red[1][lane][r]) + red[2][lane][r]) + red[3][lane][r];
+    float v = red[0][lane][r];
+#pragma unroll
+    for (int q = 1; q < kGW; ++q) v += red[q][lane][r];
     c[(size_t)(row0 + g * 4 + r) * H + col0 + i] = v;
   }
 }
@@ -774,10 +781,11 @@ int32_t sf_gemm(int32_t ta, int32_t tb, const float* A, const float* B, float* C
                 long long sA, long long sB, long long sC, void* stream) {
   if (!A || !B || !C || M < 16 || (M % 16) != 0 || batch < 1) return -1;
   const dim3 grid(H / 16, M / 16, batch);
-  if (ta && tb) SF_LAUNCH((gemm256_kernel<true, true>), grid, dim3(256), A, B, C, M, sA, sB, sC);
-  if (ta) SF_LAUNCH((gemm256_kernel<true, false>), grid, dim3(256), A, B, C, M, sA, sB, sC);
-  if (tb) SF_LAUNCH((gemm256_kernel<false, true>), grid, dim3(256), A, B, C, M, sA, sB, sC);
-  SF_LAUNCH((gemm256_kernel<false, false>), grid, dim3(256), A, B, C, M, sA, sB, sC);
+  const dim3 blk(64 * kGW);
+  if (ta && tb) SF_LAUNCH((gemm256_kernel<true, true>), grid, blk, A, B, C, M, sA, sB, sC);
+  if (ta) SF_LAUNCH((gemm256_kernel<true, false>), grid, blk, A, B, C, M, sA, sB, sC);
+  if (tb) SF_LAUNCH((gemm256_kernel<false, true>), grid, blk, A, B, C, M, sA, sB, sC);
+  SF_LAUNCH((gemm256_kernel<false, false>), grid, blk, A, B, C, M, sA, sB, sC);
 }
 
 int32_t sf_in_layer(const float* xa, const float* xa_hi, int32_t split, int32_t lda, int32_t Ka,

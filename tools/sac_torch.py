@@ -520,7 +520,7 @@ class SAC:
         return lq.detach(), la.detach()
 
 
-FUSED_LIB = os.path.join(_HERE, "_lib", "libsacfused.so")
+FUSED_LIB = os.environ.get("SAC_FUSED_LIB", os.path.join(_HERE, "_lib", "libsacfused.so"))
 
 
 class FusedSAC(SAC):
