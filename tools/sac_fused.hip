@@ -62,10 +62,17 @@ __global__ __launch_bounds__(256) void in_layer_kernel(
   const float* xr = r < split ? xa + (size_t)r * lda : xa_hi + (size_t)(r - split) * lda;
   const int K = Ka + Kb;
   float acc = 0.0f;
-  for (int k = 0; k < K; ++k) {
-    const float xv = k < Ka ? xr[k] : xb[(size_t)r * ldb + (k - Ka)];
-    const float wv = w_ku ? w[((size_t)c * K + k) * H + u] : w[(size_t)u * K + k];
-    acc += xv * wv;
+  for (int k0 = 0; k0 < K; k0 += 8) {       // (each chunk's loads issued before its FMAs)
+    float xv[8], wv[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      const int k = min(k0 + t, K - 1);
+      xv[t] = k < Ka ? xr[k] : xb[(size_t)r * ldb + (k - Ka)];
+      wv[t] = w_ku ? w[((size_t)c * K + k) * H + u] : w[(size_t)u * K + k];
+    }
+#pragma unroll
+    for (int t = 0; t < 8; ++t)
+      if (k0 + t < K) acc += xv[t] * wv[t];
   }
   const float z = acc + b[(size_t)c * H + u];
   out[((size_t)c * R + r) * H + u] = z > 0.0f ? z : 0.0f;
@@ -86,7 +93,18 @@ __global__ __launch_bounds__(256) void in_layer_pair_kernel(
     if (r >= R1) return;
     const float* xr = r < split ? xa + (size_t)r * lda : xa_hi + (size_t)(r - split) * lda;
     float acc = 0.0f;
-    for (int k = 0; k < Ka; ++k) acc += xr[k] * w1[(size_t)u * Ka + k];
+    for (int k0 = 0; k0 < Ka; k0 += 8) {
+      float xv[8], wv[8];
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        const int k = min(k0 + t, Ka - 1);
+        xv[t] = xr[k];
+        wv[t] = w1[(size_t)u * Ka + k];
+      }
+#pragma unroll
+      for (int t = 0; t < 8; ++t)
+        if (k0 + t < Ka) acc += xv[t] * wv[t];
+    }
     const float z = acc + b1[u];
     out1[(size_t)r * H + u] = z > 0.0f ? z : 0.0f;
   } else {
@@ -94,9 +112,17 @@ __global__ __launch_bounds__(256) void in_layer_pair_kernel(
     if (r >= R2) return;
     const int K = Kya + Kyb;
     float acc = 0.0f;
-    for (int k = 0; k < K; ++k) {
-      const float xv = k < Kya ? ya[(size_t)r * ldya + k] : yb[(size_t)r * ldyb + (k - Kya)];
-      acc += xv * w2[((size_t)c * K + k) * H + u];
+    for (int k0 = 0; k0 < K; k0 += 8) {
+      float xv[8], wv[8];
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        const int k = min(k0 + t, K - 1);
+        xv[t] = k < Kya ? ya[(size_t)r * ldya + k] : yb[(size_t)r * ldyb + (k - Kya)];
+        wv[t] = w2[((size_t)c * K + k) * H + u];
+      }
+#pragma unroll
+      for (int t = 0; t < 8; ++t)
+        if (k0 + t < K) acc += xv[t] * wv[t];
     }
     const float z = acc + b2[(size_t)c * H + u];
     out2[((size_t)c * R2 + r) * H + u] = z > 0.0f ? z : 0.0f;
@@ -250,16 +276,41 @@ __global__ __launch_bounds__(256) void actor_head_kernel(
   // rows r < RT (the next observations): the target critics' first layer on [x_r, a_r]
   // (in_layer's sum, k in order), so the TD target needs no launch of its own
   if (g0t && r < RT) {
+    // (k in chunks of 8 with every load of a chunk issued before its FMAs: a k-at-a-time loop
+    // paid one memory round trip per k; the sums run over k in order either way)
     const int K = Kxt + A;
+    float acc[2][4];
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[c][i] = 0.0f;
+    for (int k0 = 0; k0 < K; k0 += 8) {
+      float xv[8], wv[2][4][8];
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        const int k = min(k0 + t, K - 1);
+        xv[t] = k < Kxt ? xt[(size_t)r * ldxt + k] : av[(k - Kxt) & 3];
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) wv[c][i][t] = tw0[((size_t)c * K + k) * H + lane + 64 * i];
+      }
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        if (k0 + t < K) {
+#pragma unroll
+          for (int c = 0; c < 2; ++c)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) acc[c][i] += xv[t] * wv[c][i][t];
+        }
+      }
+    }
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int u = lane + 64 * i;
-        float acc = 0.0f;
-        for (int k = 0; k < Kxt; ++k) acc += xt[(size_t)r * ldxt + k] * tw0[((size_t)c * K + k) * H + u];
-        for (int j = 0; j < A; ++j) acc += av[j & 3] * tw0[((size_t)c * K + Kxt + j) * H + u];
-        const float z = acc + tb0[(size_t)c * H + u];
+        const float z = acc[c][i] + tb0[(size_t)c * H + u];
         g0t[((size_t)c * RT + r) * H + u] = z > 0.0f ? z : 0.0f;
       }
     }
