@@ -259,7 +259,8 @@ def test_fused_sac_update_matches_autograd_update(obs_dim, act_dim, gemm):
 
 def test_fused_sac_loop_is_graph_capturable():
     """The whole C5 iteration with FusedSAC (policy sample, env step, replay insert, update)
-    captured as one HIP graph and replayed: finite losses and parameters that move."""
+    captured as one HIP graph and replayed: finite losses, parameters that move, and the
+    loop's observation buffer equal to the batch's after each replay."""
     import numpy as np
     from bluesky_gym import _native as nat, config, core
     dev = torch.device("cuda", 0)
@@ -276,6 +277,9 @@ def test_fused_sac_loop_is_graph_capturable():
     for _ in range(10):
         rl.replay()
     torch.cuda.synchronize()
+    # the loop's observation buffer holds the batch's new observations (copied by the replay
+    # insert's launch) and the last insert's rows hold the observations before that step
+    assert torch.equal(rl.obs, b.obs)
     lq, la = s.update()
     assert np.isfinite(float(lq)) and np.isfinite(float(la))
     assert not torch.equal(w0, s.actor.latent[2].weight.detach())

@@ -114,7 +114,8 @@ __global__ __launch_bounds__(256) void replay_insert_kernel(
     float* __restrict__ buf, long long cap, int O, int A, const float* __restrict__ obs,
     const double* __restrict__ act, const float* __restrict__ rew, const uint8_t* __restrict__ term,
     const uint8_t* __restrict__ trunc, const float* __restrict__ next_obs,
-    const float* __restrict__ final_obs, int E, long long* pos, long long* size, unsigned* ticket) {
+    const float* __restrict__ final_obs, int E, long long* pos, long long* size, unsigned* ticket,
+    float* __restrict__ obs_out) {
   const int W = 2 * O + A + 2;
   const long long p0 = __atomic_load_n(pos, __ATOMIC_RELAXED);
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -123,6 +124,9 @@ __global__ __launch_bounds__(256) void replay_insert_kernel(
     float v;
     if (c < O) {
       v = obs[(size_t)e * O + c];
+      // obs_out (the loop's observation buffer, possibly obs itself: this thread alone reads
+      // that element, before it writes it): the post-step observation the next action samples
+      if (obs_out) obs_out[(size_t)e * O + c] = next_obs[(size_t)e * O + c];
     } else if (c < O + A) {
       v = (float)act[(size_t)e * A + (c - O)];
     } else if (c == O + A) {
@@ -163,7 +167,26 @@ extern "C" int32_t sac_replay_insert(float* buf, long long cap, int32_t obs_dim,
   const int grid = (int)((n + 255) / 256);
   hipLaunchKernelGGL(replay_insert_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, buf, cap,
                      obs_dim, act_dim, obs, act, rew, term, trunc, next_obs, final_obs, E, pos, size,
-                     ticket);
+                     ticket, nullptr);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+// the insert above that also copies the post-step observations into obs_out (RLLoop's obs
+// buffer, which may be `obs` itself) -- the loop's separate copy launch folded in
+extern "C" int32_t sac_replay_insert_obs(float* buf, long long cap, int32_t obs_dim, int32_t act_dim,
+                                         const float* obs, const double* act, const float* rew,
+                                         const uint8_t* term, const uint8_t* trunc,
+                                         const float* next_obs, const float* final_obs, int32_t E,
+                                         long long* pos, long long* size, unsigned* ticket,
+                                         float* obs_out, void* stream) {
+  if (!buf || cap < 1 || obs_dim < 1 || act_dim < 1 || E < 1 || E > cap || !obs || !act || !rew ||
+      !term || !trunc || !next_obs || !final_obs || !pos || !size || !ticket || !obs_out)
+    return -1;
+  const long long n = (long long)E * (2 * obs_dim + act_dim + 2);
+  const int grid = (int)((n + 255) / 256);
+  hipLaunchKernelGGL(replay_insert_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, buf, cap,
+                     obs_dim, act_dim, obs, act, rew, term, trunc, next_obs, final_obs, E, pos, size,
+                     ticket, obs_out);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 

@@ -71,6 +71,10 @@ class HipAdam:
             lib.sac_replay_insert.argtypes = ([ctypes.c_void_p, ctypes.c_longlong, ctypes.c_int32,
                                                ctypes.c_int32] + [ctypes.c_void_p] * 7 +
                                               [ctypes.c_int32] + [ctypes.c_void_p] * 4)
+            lib.sac_replay_insert_obs.restype = ctypes.c_int32
+            lib.sac_replay_insert_obs.argtypes = ([ctypes.c_void_p, ctypes.c_longlong, ctypes.c_int32,
+                                                   ctypes.c_int32] + [ctypes.c_void_p] * 7 +
+                                                  [ctypes.c_int32] + [ctypes.c_void_p] * 5)
             lib.sac_replay_sample.restype = ctypes.c_int32
             lib.sac_replay_sample.argtypes = [ctypes.c_void_p, ctypes.c_longlong, ctypes.c_int32,
                                               ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p,
@@ -383,7 +387,7 @@ class SAC:
         self.pos.copy_((self.pos + n) % self.cap)
         self.size.copy_(torch.clamp(self.size + n, max=self.cap))
 
-    def insert_step(self, obs, act, batch):
+    def insert_step(self, obs, act, batch, obs_out=None):
         """The E transitions of one SAME_STEP vector step (obs before the step, fp64 actions,
         the batch's reward / terminated / truncated / obs / final_obs) in one launch of
         tools/sac_adam.hip's replay insert; the same rows and pos/size as insert() with
@@ -399,10 +403,19 @@ class SAC:
                 raise ValueError("insert_step: unexpected tensor layout")
         ptr = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
         stream = ctypes.c_void_p(torch.cuda.current_stream(self.dev).cuda_stream)
-        rc = HipAdam._lib.sac_replay_insert(
-            ptr(self.buf), self.cap, self.od, self.ad, ptr(obs), ptr(act), ptr(batch.reward),
-            ptr(batch.terminated), ptr(batch.truncated), ptr(batch.obs), ptr(batch.final_obs), E,
-            ptr(self.pos), ptr(self.size), ptr(self._ticket), stream)
+        if obs_out is not None:
+            # (and obs_out <- batch.obs in the same launch: RLLoop's copy of the new observations)
+            if obs_out.dtype != torch.float32 or not obs_out.is_contiguous() or obs_out.shape != obs.shape:
+                raise ValueError("insert_step: obs_out must be an fp32 tensor of obs's shape")
+            rc = HipAdam._lib.sac_replay_insert_obs(
+                ptr(self.buf), self.cap, self.od, self.ad, ptr(obs), ptr(act), ptr(batch.reward),
+                ptr(batch.terminated), ptr(batch.truncated), ptr(batch.obs), ptr(batch.final_obs), E,
+                ptr(self.pos), ptr(self.size), ptr(self._ticket), ptr(obs_out), stream)
+        else:
+            rc = HipAdam._lib.sac_replay_insert(
+                ptr(self.buf), self.cap, self.od, self.ad, ptr(obs), ptr(act), ptr(batch.reward),
+                ptr(batch.terminated), ptr(batch.truncated), ptr(batch.obs), ptr(batch.final_obs), E,
+                ptr(self.pos), ptr(self.size), ptr(self._ticket), stream)
         if rc != 0:
             raise RuntimeError(f"sac_replay_insert failed ({rc})")
 
@@ -759,15 +772,19 @@ class RLLoop:
                 a, _ = s.actor(self.obs)
             self.act.copy_(a)
         b.step(self.act)
+        copied = False
         if self.learn:
             if s.hip_adam:
-                s.insert_step(self.obs, self.act, b)       # one launch (tools/sac_adam.hip)
+                # one launch (tools/sac_adam.hip), which also copies the new observations
+                s.insert_step(self.obs, self.act, b, obs_out=self.obs)
+                copied = True
             else:
                 done = (b.terminated | b.truncated).bool()
                 nxt = torch.where(done[:, None], b.final_obs, b.obs)
                 s.insert(self.obs, a, b.reward, nxt, b.terminated.float())
             s.update(losses=False)
-        self.obs.copy_(b.obs)
+        if not copied:
+            self.obs.copy_(b.obs)
 
     def capture(self, warm=3, iters=1):
         """iters: RL iterations per graph (each replay runs that many, in order, each with its
