@@ -163,6 +163,12 @@ def main():
                     help="merge: the BASELINE metric (default); descent-sac: BASELINE configs[4], "
                          "DescentEnv-v0 with the SAC learner in the loop")
     ap.add_argument("--no-graph", action="store_true", help="descent-sac: eager, no HIP graph")
+    ap.add_argument("--learner-reduce", default="auto", choices=("auto", "rccl", "torch"),
+                    help="descent-sac: the learner's gradient all-reduce -- rccl: libbsg's "
+                         "communicator (bsg_comm_all_reduce on the update's stream, inside the "
+                         "iteration's HIP graph; at one rank a one-rank communicator), torch: "
+                         "torch.distributed (eager); auto = rccl over the nccl backend (and at "
+                         "one rank), torch otherwise")
     ap.add_argument("--torch-policy", action="store_true",
                     help="descent-sac: sample actions with the torch actor instead of bsg_policy_sac")
     ap.add_argument("--blas", default="cublas", choices=("default", "cublas", "cublaslt"),
@@ -617,8 +623,8 @@ def bench_descent_sac(args):
     256, buffer 1e6, train_freq 1, gradient_steps 1).  Three rates over the same envs:
     env only (U(-1,1) actions from HBM), env + policy (the reference's saved SAC actor,
     stochastic, forward on the kernel's fp32 obs rows), env + policy + one SAC update per
-    vector step (tools/sac_torch.py; HIP graph of the whole iteration on one GPU, eager with
-    an RCCL gradient all-reduce across ranks).  value = the last, whole job."""
+    vector step (tools/sac_torch.py; the whole iteration one HIP graph, the gradient
+    all-reduce inside it over libbsg's RCCL communicator).  value = the last, whole job."""
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -652,11 +658,20 @@ def bench_descent_sac(args):
                          seed=1234, env_offset=rank * E)
     b.reset()
     W = dict(np.load(os.path.join(REPO, "tests", "golden", "sac_actors.npz")))
-    # FusedSAC (tools/sac_fused.hip); across ranks with its RCCL gradient all-reduce before
-    # each Adam launch (eager); SAC_FUSED=0 = the autograd update
+    # FusedSAC (tools/sac_fused.hip) with the gradients all-reduced before each Adam launch:
+    # over libbsg's RCCL communicator on the update's stream (the iteration stays one HIP
+    # graph at any rank count; at one rank a one-rank communicator, so the reduce is timed)
+    # or torch.distributed (eager: the gloo rehearsal); SAC_FUSED=0 = the autograd update
     cls = sac_torch.FusedSAC if os.environ.get("SAC_FUSED", "1") == "1" else sac_torch.SAC
+    reduce = args.learner_reduce
+    if reduce == "auto":
+        reduce = "rccl" if (world == 1 or backend == "nccl") else "torch"
+    comm = None
+    if reduce == "rccl":
+        from bluesky_gym.parallel import RcclGather
+        comm = RcclGather(dev, dist.group.WORLD if world > 1 else None)
     sac = cls(b.obs_dim, b.act_dim, dev, group=dist.group.WORLD if world > 1 else None,
-                        seed=rank, lr=1e-3)
+              seed=rank, lr=1e-3, comm=comm)
     sac.actor.load_sb3(W, "descent")
     gen = torch.Generator(device=dev)
     gen.manual_seed(17 + rank)
@@ -684,7 +699,8 @@ def bench_descent_sac(args):
         return el
 
     el_env = timed(lambda k: b.step(bank[k % 16]), args.steps)
-    graph = world == 1 and not args.no_graph
+    # (torch.distributed's eager all-reduce cannot sit in the graph; libbsg's can)
+    graph = not args.no_graph and (world == 1 or comm is not None)
     fused = not args.torch_policy
 
     def policy_loop(fused_policy):
@@ -704,6 +720,8 @@ def bench_descent_sac(args):
         rl.capture()
     el_rl = timed((lambda k: rl.replay()) if graph else (lambda k: rl.step()), args.steps)
     lq, la = sac.update()                             # one more update: finite losses
+    torch.cuda.synchronize()
+    reduces = comm.info()["reduces"] if comm is not None else 0
     if rank == 0:
         total = world * E * args.steps
         out = {
@@ -732,7 +750,14 @@ def bench_descent_sac(args):
                        "adam": "one launch per step (tools/sac_adam.hip)" if sac.hip_adam else
                                "torch " + os.environ.get("SAC_ADAM", "fused"),
                        "hip_graph": graph, "blas": str(torch.backends.cuda.preferred_blas_library()),
-                       "update": type(sac).__name__},
+                       "update": type(sac).__name__,
+                       "learner_reduce": ("rccl: bsg_comm_all_reduce (ncclAllReduce avg) of the "
+                                          "critics' and the actor's gradients on the update's "
+                                          f"stream, {comm.world} rank(s), {reduces} calls issued "
+                                          "(a graph replay re-runs its captured ones)"
+                                          if comm is not None else
+                                          "torch.distributed all_reduce (eager)" if world > 1 else
+                                          "none (one rank)")},
             "env_only": {"value": total / el_env, "ms_per_step": el_env * 1e3 / args.steps},
             "env_policy": {"value": total / el_pol, "ms_per_step": el_pol * 1e3 / args.steps,
                            "policy": "fused HIP actor (bsg_policy_sac)" if fused else "torch actor"},
@@ -742,6 +767,8 @@ def bench_descent_sac(args):
                                    "critic_loss": float(lq), "actor_loss": float(la)},
         }
         print(json.dumps(out), flush=True)
+    if comm is not None:
+        comm.close()
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

@@ -94,7 +94,9 @@ EXPORTED_SYMBOLS = (
     "bsg_set_learner", "bsg_policy_sac", "bsg_lookahead_bytes", "bsg_set_lookahead",
     "bsg_comm_last_error", "bsg_comm_unique_id", "bsg_comm_create", "bsg_comm_destroy",
     "bsg_comm_all_gather", "bsg_comm_wait", "bsg_comm_get_info", "bsg_step_gather",
+    "bsg_comm_all_reduce",
 )
+REDUCE_SUM, REDUCE_AVG = 0, 1   # include/bsg.h BSG_REDUCE_*
 COMM_ID_BYTES = 128          # include/bsg.h BSG_COMM_ID_BYTES
 COMM_SLOTS = 16              # BSG_COMM_SLOTS
 
@@ -103,7 +105,7 @@ class BsgCommInfo(C.Structure):
     """include/bsg.h bsg_comm_info."""
     _fields_ = [("nranks", C.c_int32), ("rank", C.c_int32), ("device", C.c_int32),
                 ("use_graphs", C.c_int32), ("gathers", C.c_int64), ("graph_hits", C.c_int64),
-                ("graph_captures", C.c_int64)]
+                ("graph_captures", C.c_int64), ("reduces", C.c_int64)]
 
 
 class BsgSacActor(C.Structure):
@@ -185,6 +187,8 @@ def load_library(path: str | None = None):
                                         C.c_void_p]
     lib.bsg_comm_wait.restype = C.c_int32
     lib.bsg_comm_wait.argtypes = [C.c_void_p, C.c_int32, C.c_void_p]
+    lib.bsg_comm_all_reduce.restype = C.c_int32
+    lib.bsg_comm_all_reduce.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_int32, C.c_void_p]
     lib.bsg_comm_get_info.restype = C.c_int32
     lib.bsg_comm_get_info.argtypes = [C.c_void_p, C.POINTER(BsgCommInfo)]
     lib.bsg_step_gather.restype = C.c_int32

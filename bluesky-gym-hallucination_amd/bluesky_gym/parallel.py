@@ -84,11 +84,17 @@ class RcclGather:
         err = "" if ok else self.lib.bsg_comm_last_error().decode(errors="replace")
         if ok:
             self._comm = comm
-            info = self.info()
-            if info["nranks"] != self.world or info["rank"] != self.rank:
-                ok = False
-                err = (f"RCCL sees {info['nranks']} ranks with this one as rank {info['rank']}, "
-                       f"the process group {self.world} / {self.rank}")
+            # (a failing info() must not keep this rank from the flag all-reduce below, where
+            # the other ranks wait: ADVICE r05)
+            try:
+                info = self.info()
+            except nat.BsgError as ex:
+                ok, err = False, str(ex)
+            else:
+                if info["nranks"] != self.world or info["rank"] != self.rank:
+                    ok = False
+                    err = (f"RCCL sees {info['nranks']} ranks with this one as rank {info['rank']}, "
+                           f"the process group {self.world} / {self.rank}")
         if self.world > 1:
             flag = torch.tensor([1 if ok else 0], dtype=torch.int32)
             flag = flag.to(device) if on_dev else flag
@@ -143,6 +149,18 @@ class RcclGather:
     def wait(self, slot: int):
         self._nat.check_comm(self.lib.bsg_comm_wait(self._comm, int(slot), self._stream()),
                              "bsg_comm_wait")
+
+    def all_reduce(self, t: torch.Tensor, avg: bool = True):
+        """t (contiguous fp32 on this rank's device) <- the mean (avg) or sum over the ranks, in
+        place: bsg_comm_all_reduce, ncclAllReduce on the current stream itself -- ordered
+        with the kernels around it and recorded into a HIP graph when that stream is being
+        captured (the C5 learner's gradient reduction, tools/sac_torch.py)."""
+        if t.dtype != torch.float32 or not t.is_contiguous() or t.device.type != "cuda":
+            raise ValueError("all_reduce: a contiguous fp32 device tensor")
+        op = self._nat.REDUCE_AVG if avg else self._nat.REDUCE_SUM
+        self._nat.check_comm(self.lib.bsg_comm_all_reduce(
+            self._comm, self._C.c_void_p(t.data_ptr()), t.numel(), op, self._stream()),
+            "bsg_comm_all_reduce")
 
     def close(self):
         if self._comm is not None and self._comm.value:

@@ -44,12 +44,15 @@ typedef struct ncclComm* ncclComm_t;
 typedef struct { char internal[BSG_COMM_ID_BYTES]; } ncclUniqueId;
 typedef int ncclResult_t;                 // ncclSuccess = 0
 constexpr int kNcclFloat32 = 7;
+constexpr int kNcclSum = 0, kNcclAvg = 4;   // ncclRedOp_t
 
 struct Rccl {
   void* h = nullptr;
   ncclResult_t (*get_unique_id)(ncclUniqueId*) = nullptr;
   ncclResult_t (*comm_init_rank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
   ncclResult_t (*all_gather)(const void*, void*, size_t, int, ncclComm_t, hipStream_t) = nullptr;
+  // (optional: only bsg_comm_all_reduce needs it)
+  ncclResult_t (*all_reduce)(const void*, void*, size_t, int, int, ncclComm_t, hipStream_t) = nullptr;
   ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
   ncclResult_t (*comm_count)(ncclComm_t, int*) = nullptr;
   ncclResult_t (*comm_user_rank)(ncclComm_t, int*) = nullptr;
@@ -80,6 +83,7 @@ Rccl* rccl() {
   r.get_unique_id = reinterpret_cast<decltype(r.get_unique_id)>(dlsym(r.h, "ncclGetUniqueId"));
   r.comm_init_rank = reinterpret_cast<decltype(r.comm_init_rank)>(dlsym(r.h, "ncclCommInitRank"));
   r.all_gather = reinterpret_cast<decltype(r.all_gather)>(dlsym(r.h, "ncclAllGather"));
+  r.all_reduce = reinterpret_cast<decltype(r.all_reduce)>(dlsym(r.h, "ncclAllReduce"));
   r.comm_destroy = reinterpret_cast<decltype(r.comm_destroy)>(dlsym(r.h, "ncclCommDestroy"));
   r.comm_count = reinterpret_cast<decltype(r.comm_count)>(dlsym(r.h, "ncclCommCount"));
   r.comm_user_rank = reinterpret_cast<decltype(r.comm_user_rank)>(dlsym(r.h, "ncclCommUserRank"));
@@ -142,6 +146,7 @@ struct bsg_comm {
   GatherGraph graphs[kGraphCache];
   int next_graph = 0;
   int64_t graph_hits = 0, graph_captures = 0;
+  int64_t reduces = 0;                  // bsg_comm_all_reduce calls
   // BSG_COMM_PROFILE=1: host time of each part of bsg_comm_all_gather, printed at destroy
   bool prof = false;
   double t_rec = 0, t_wait = 0, t_coll = 0, t_rec2 = 0;
@@ -367,6 +372,26 @@ int32_t bsg_comm_get_info(const bsg_comm* c, bsg_comm_info* out) {
   out->gathers = c->gseq;
   out->graph_hits = c->graph_hits;
   out->graph_captures = c->graph_captures;
+  out->reduces = c->reduces;
+  return BSG_OK;
+}
+
+// The learner's gradients: in place, on the caller's stream (no side stream, no events: the
+// update that follows on that stream needs the result, and a graph capture of the update
+// records the collective as one more node of the same stream)
+int32_t bsg_comm_all_reduce(bsg_comm* c, float* buf, int64_t count, int32_t op, void* stream) {
+  if (!c || !buf) return comm_fail(BSG_E_INVALID_ARG, "bsg_comm_all_reduce: null argument");
+  if (count < 0 || (op != BSG_REDUCE_SUM && op != BSG_REDUCE_AVG))
+    return comm_fail(BSG_E_INVALID_ARG, "bsg_comm_all_reduce: count or op out of range");
+  Rccl* r = rccl();
+  if (!r || !c->nc) return comm_fail(BSG_E_STATE, "bsg_comm_all_reduce: no communicator");
+  if (!r->all_reduce) return comm_fail(BSG_E_UNSUPPORTED, "bsg_comm_all_reduce: RCCL lacks ncclAllReduce");
+  if (count == 0) return BSG_OK;
+  ncclResult_t e = r->all_reduce(buf, buf, (size_t)count, kNcclFloat32,
+                                 op == BSG_REDUCE_AVG ? kNcclAvg : kNcclSum, c->nc,
+                                 reinterpret_cast<hipStream_t>(stream));
+  if (e != 0) return comm_fail(BSG_E_HIP, nccl_msg(r, e, "ncclAllReduce"));
+  ++c->reduces;
   return BSG_OK;
 }
 

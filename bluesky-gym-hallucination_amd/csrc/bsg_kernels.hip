@@ -3332,7 +3332,12 @@ static hipError_t launch_kind_w(const KParams& p0, hipStream_t st) {
     }
 #undef BSG_CASE_CD
   }
+#if defined(BSG_DESCENT_NOCOOP) && BSG_DESCENT_NOCOOP
+  // (counter A/B builds only, tools/pmc_descent_ab.sh: the one-wave instance of round 4)
+  if constexpr (false) {
+#else
   if constexpr (KIND == BSG_ENV_DESCENT && !WIND) {
+#endif
     // kDC_W waves per workgroup: the ownships' substep loop pipelined over them (descent_coop)
     if (gs != 1) return hipErrorInvalidValue;
     hipLaunchKernelGGL((step_kernel<KIND, 1, WIND, kDC_W>), dim3(grid), dim3(64 * kDC_W), p.lds_pad, st, p);

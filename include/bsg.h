@@ -342,8 +342,19 @@ typedef struct bsg_comm_info {
   int64_t gathers;       /* bsg_comm_all_gather calls (bsg_step_gather included) */
   int64_t graph_hits;    /* gathers replayed from the graph cache */
   int64_t graph_captures;/* gathers captured into a new graph */
+  int64_t reduces;       /* bsg_comm_all_reduce calls */
 } bsg_comm_info;
 int32_t bsg_comm_get_info(const bsg_comm* comm, bsg_comm_info* out);
+/* The data-parallel learner's gradient reduction (C5, BASELINE configs[4]: "DescentEnv-v0 +
+ * SB3 SAC learner, 4096 envs on 8 GPUs"; the reference trains one SB3 SAC in one process,
+ * scripts/descent_env_sac.py:25-34, so this is the N-rank form of its gradient step):
+ * buf[count] fp32 <- the sum (op BSG_REDUCE_SUM) or mean (BSG_REDUCE_AVG) over the ranks of
+ * every rank's buf, in place, as ncclAllReduce on `stream` itself (ordered after what
+ * `stream` enqueued and before what it enqueues next), so a learner update that calls it
+ * stays one stream -- and capturable into a HIP graph. */
+#define BSG_REDUCE_SUM 0
+#define BSG_REDUCE_AVG 1
+int32_t bsg_comm_all_reduce(bsg_comm* comm, float* buf, int64_t count, int32_t op, void* stream);
 /* One RL step of a shard and the gather of its learner rows in one call (the host side of
  * a C4 step: ~one launch instead of a wait, a pointer swap, a launch and a gather):
  * bsg_comm_wait(slot) [the gather that last read rows[slot]], learner rows <- rows,

@@ -234,6 +234,12 @@ def test_comm_argument_errors_before_any_device_call():
     assert lib.bsg_comm_all_gather(fake, None, buf, 4, 0, None) == E_INVALID
     assert lib.bsg_comm_wait(None, 0, None) == E_INVALID and "null comm" in err()
     assert lib.bsg_comm_wait(fake, nat.COMM_SLOTS, None) == E_INVALID and "slot out of range" in err()
+    assert lib.bsg_comm_all_reduce(None, buf, 4, nat.REDUCE_AVG, None) == E_INVALID
+    assert "bsg_comm_all_reduce: null" in err()
+    assert lib.bsg_comm_all_reduce(fake, None, 4, nat.REDUCE_SUM, None) == E_INVALID
+    for count, op in ((-1, nat.REDUCE_SUM), (4, 2), (4, -1)):
+        assert lib.bsg_comm_all_reduce(fake, buf, count, op, None) == E_INVALID
+        assert "out of range" in err()
     info = nat.BsgCommInfo()
     assert lib.bsg_comm_get_info(None, C.byref(info)) == E_INVALID and "null" in err()
     assert lib.bsg_comm_destroy(None) == 0

@@ -99,6 +99,24 @@ def test_bench_descent_sac_two_rank_rehearsal():
     assert len(lines) == 1, out.stdout
     r = json.loads(lines[0])
     assert r["n_gpus"] == 2 and r["config"]["envs_total"] == 4096 and r["config"]["envs_per_gpu"] == 2048
+    # (gloo ranks: the torch.distributed reduce, eager; RCCL cannot put two ranks on one GPU)
     assert r["config"]["update"] == "FusedSAC" and r["config"]["hip_graph"] is False
+    assert r["config"]["learner_reduce"].startswith("torch.distributed")
     ln = r["env_policy_learner"]
     assert ln["value"] > 0 and ln["critic_loss"] == ln["critic_loss"] and ln["actor_loss"] == ln["actor_loss"]
+
+
+def test_bench_descent_sac_one_rank_rccl_reduce_in_graph():
+    """the C5 iteration with the learner's gradient all-reduce over
+    libbsg's RCCL communicator (a one-rank communicator here) stays one HIP graph, and the
+    reduce calls were issued (captured, then replayed)."""
+    out = subprocess.run([sys.executable, "bench.py", "--workload", "descent-sac", "--steps", "10",
+                          "--warmup", "3"], cwd=REPO, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    r = json.loads(lines[0])
+    assert r["config"]["hip_graph"] is True
+    assert r["config"]["learner_reduce"].startswith("rccl")
+    ln = r["env_policy_learner"]
+    assert ln["value"] > 0 and ln["critic_loss"] == ln["critic_loss"]

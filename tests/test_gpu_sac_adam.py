@@ -274,12 +274,20 @@ def test_fused_sac_loop_is_graph_capturable():
     for _ in range(4):
         rl.step()
     rl.capture()
-    for _ in range(10):
+    for _ in range(9):
         rl.replay()
     torch.cuda.synchronize()
+    pre = rl.obs.clone()
+    p0 = int(s.pos)
+    rl.replay()
+    torch.cuda.synchronize()
     # the loop's observation buffer holds the batch's new observations (copied by the replay
-    # insert's launch) and the last insert's rows hold the observations before that step
+    # insert's launch, which reads and writes the same buffer: ADVICE r05) and the last
+    # insert's rows hold the observations before that step, bit for bit
     assert torch.equal(rl.obs, b.obs)
+    rows = (p0 + torch.arange(b.E, device=dev)) % s.cap
+    assert torch.equal(s.buf_obs[rows], pre)
+    assert not torch.equal(pre, rl.obs)
     lq, la = s.update()
     assert np.isfinite(float(lq)) and np.isfinite(float(la))
     assert not torch.equal(w0, s.actor.latent[2].weight.detach())
@@ -416,6 +424,50 @@ def test_fused_sac_two_ranks_equal_one_rank(tmp_path):
            list(s.qt.parameters()) + [s.log_alpha]]
     assert len(one) == len(two)
     for x, y in zip(one, two):
+        assert torch.equal(x, y)
+
+
+def _captured_loop_params(comm, iters=6):
+    """The C5 iteration (fused policy sample, Descent step, replay insert, FusedSAC update)
+    captured as one HIP graph and replayed `iters` times; the networks afterwards."""
+    from bluesky_gym import _native as nat, config, core
+    dev = torch.device("cuda", 0)
+    b = core.DeviceBatch(config.descent_config(), 512, autoreset=nat.AUTORESET_SAME_STEP,
+                         compute_cd=False, seed=5)
+    b.reset()
+    s = sac_torch.FusedSAC(b.obs_dim, b.act_dim, dev, seed=2, lr=1e-3, comm=comm)
+    rl = sac_torch.RLLoop(b, s, learn=True, fused_policy=True)
+    rl.obs.copy_(b.obs)
+    for _ in range(4):
+        rl.step()
+    rl.capture()
+    for _ in range(iters):
+        rl.replay()
+    torch.cuda.synchronize()
+    return [p.detach().clone() for p in list(s.actor.parameters()) + list(s.q.parameters()) +
+            list(s.qt.parameters()) + [s.log_alpha]]
+
+
+def test_fused_sac_rccl_reduce_captured_bit_equal_to_unreduced():
+    """the N-rank learner's gradient all-reduce (bsg_comm_all_reduce,
+    ncclAllReduce avg on the update's stream) inside the captured C5 iteration.  With a
+    one-rank RCCL communicator the mean is the identity, so the replayed iterations must leave
+    the networks bit-equal to the same iterations without the reduce -- and the reduce calls
+    were recorded (two per update: the critics', the actor's with log_alpha)."""
+    from bluesky_gym.parallel import RcclGather
+    dev = torch.device("cuda", 0)
+    comm = RcclGather(dev)
+    try:
+        assert comm.info()["nranks"] == 1
+        red = _captured_loop_params(comm)
+        n = comm.info()["reduces"]
+    finally:
+        comm.close()
+    ref = _captured_loop_params(None)
+    # warm-up steps and the capture itself issue the calls; replays re-run the captured ones
+    assert n >= 2 * 5
+    assert len(red) == len(ref)
+    for x, y in zip(red, ref):
         assert torch.equal(x, y)
 
 

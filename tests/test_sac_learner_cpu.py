@@ -88,3 +88,44 @@ def test_gloo_world2_gradient_allreduce_equals_union_batch():
     for g0, g1, p in zip(res[0][0], res[1][0], s.q1.parameters()):
         np.testing.assert_array_equal(g0, g1)
         np.testing.assert_allclose(g0, p.grad.numpy(), rtol=1e-5, atol=1e-6)
+
+
+def _dp_seed_worker(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        # bench.py's construction: the rank is the sampling seed
+        s = sac_torch.SAC(4, 1, "cpu", buffer=64, batch=32, group=dist.group.WORLD, seed=rank)
+        g = torch.Generator().manual_seed(100 + rank)
+        for _ in range(4):
+            x = torch.randn(16, 4, generator=g)
+            s.insert(x, torch.rand(16, 1, generator=g) * 2 - 1, torch.randn(16, generator=g),
+                     torch.randn(16, 4, generator=g), torch.zeros(16))
+        for _ in range(3):
+            lq, la = s.update()
+            assert torch.isfinite(lq) and torch.isfinite(la)
+        nets = (list(s.actor.parameters()) + list(s.q.parameters()) + list(s.qt.parameters())
+                + [s.log_alpha])
+        q.put((rank, [p.detach().numpy().copy() for p in nets]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_different_seeds_same_parameters():
+    """each rank seeds SAC with its own rank (its replay draws and noise), yet
+    the ranks are one data-parallel learner -- rank 0's networks are broadcast at
+    construction and the mean gradient keeps them equal, update after update."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_dp_seed_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=180) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for a, b in zip(res[0], res[1]):
+        np.testing.assert_array_equal(a, b)

@@ -111,11 +111,11 @@ extern "C" int32_t sac_adam_step_polyak(const sac_adam_table* T, const float* st
 namespace {
 
 __global__ __launch_bounds__(256) void replay_insert_kernel(
-    float* __restrict__ buf, long long cap, int O, int A, const float* __restrict__ obs,
+    float* __restrict__ buf, long long cap, int O, int A, const float* obs,
     const double* __restrict__ act, const float* __restrict__ rew, const uint8_t* __restrict__ term,
     const uint8_t* __restrict__ trunc, const float* __restrict__ next_obs,
     const float* __restrict__ final_obs, int E, long long* pos, long long* size, unsigned* ticket,
-    float* __restrict__ obs_out) {
+    float* obs_out) {
   const int W = 2 * O + A + 2;
   const long long p0 = __atomic_load_n(pos, __ATOMIC_RELAXED);
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -123,9 +123,10 @@ __global__ __launch_bounds__(256) void replay_insert_kernel(
     const int e = (int)(i / W), c = (int)(i - (long long)e * W);
     float v;
     if (c < O) {
+      // obs_out (the loop's observation buffer) may be obs itself, so neither pointer is
+      // __restrict__: the compiler may not move this load after the store below (ADVICE
+      // r05).  This thread alone reads and writes element (e, c).
       v = obs[(size_t)e * O + c];
-      // obs_out (the loop's observation buffer, possibly obs itself: this thread alone reads
-      // that element, before it writes it): the post-step observation the next action samples
       if (obs_out) obs_out[(size_t)e * O + c] = next_obs[(size_t)e * O + c];
     } else if (c < O + A) {
       v = (float)act[(size_t)e * A + (c - O)];

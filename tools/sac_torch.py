@@ -327,7 +327,13 @@ class QView(nn.Module):
 
 class SAC:
     def __init__(self, obs_dim, act_dim, device, *, lr=3e-4, batch=256, buffer=1_000_000,
-                 gamma=0.99, tau=0.005, group=None, seed=0):
+                 gamma=0.99, tau=0.005, group=None, seed=0, comm=None):
+        """group: the data-parallel process group (None: one rank).  comm: an object with
+        all_reduce(t, avg) -- bluesky_gym.parallel.RcclGather, libbsg's RCCL communicator --
+        that reduces the gradients on the current stream (graph-capturable; also at one rank,
+        where it is the identity); without it several ranks reduce through torch.distributed
+        (eager).  seed: this rank's sampling seed (replay draws, noise); the parameters are
+        those of rank 0, broadcast over `group` (every rank starts from the same networks)."""
         torch.manual_seed(seed)
         self.dev = torch.device(device)
         self.actor = Actor(obs_dim, act_dim).to(self.dev)
@@ -359,8 +365,19 @@ class SAC:
             self.opt_al = torch.optim.Adam([self.log_alpha], **opt)
         self.gamma, self.tau = gamma, tau
         self.group = group
+        self.comm = comm
         world = torch.distributed.get_world_size(group) if group is not None else 1
+        if comm is not None and group is None:
+            world = int(getattr(comm, "world", 1))
         self.world = world
+        if group is not None and world > 1:
+            # data-parallel SAC: one set of networks.  Each rank seeded its own (seed = its
+            # sampling seed), so rank 0's are broadcast before any step
+            src = torch.distributed.get_global_rank(group, 0)
+            with torch.no_grad():
+                for t in (list(self.actor.parameters()) + list(self.q.parameters()) +
+                          list(self.qt.parameters()) + [self.log_alpha]):
+                    torch.distributed.broadcast(t.data, src=src, group=group)
         self.batch = max(1, batch // world)
         self.cap = buffer // world
         d = self.dev
@@ -458,13 +475,20 @@ class SAC:
         return self._y
 
     # -------------------------------------------------------------- SAC update
+    def _reduce_flat(self, flat):
+        """flat <- the mean over the ranks (in place)"""
+        if self.comm is not None:
+            self.comm.all_reduce(flat, avg=True)
+        elif self.world > 1:
+            torch.distributed.all_reduce(flat, group=self.group)
+            flat /= self.world
+
     def _allreduce(self, params):
-        if self.world == 1:
+        if self.world == 1 and self.comm is None:
             return
         grads = [p.grad for p in params if p.grad is not None]
         flat = torch.cat([g.reshape(-1) for g in grads])
-        torch.distributed.all_reduce(flat, group=self.group)
-        flat /= self.world
+        self._reduce_flat(flat)
         off = 0
         for g in grads:
             n = g.numel()
@@ -566,8 +590,8 @@ class FusedSAC(SAC):
         self._pol_eps = None
         if not self.hip_adam or self.dev.type != "cuda":
             raise ValueError("FusedSAC: the HIP Adam path (SAC_ADAM=hip) on a HIP device")
-        # (several ranks: the gradients are all-reduced before each Adam launch, SAC._allreduce;
-        # that path runs eagerly -- RLLoop.capture is for one rank)
+        # (several ranks: the gradients are all-reduced before each Adam launch, _reduce_flat:
+        # with an RCCL comm on the update's stream, so RLLoop.capture records it too)
         if FusedSAC._lib is None:
             if not os.path.exists(FUSED_LIB):
                 raise RuntimeError(f"{FUSED_LIB} missing: run __graft_entry__.build()")
@@ -604,8 +628,20 @@ class FusedSAC(SAC):
         self._dlogp, self._lossq, self._lossa = z(B), z(B), z(B)
         self._dg1, self._dg0 = z(2, B, H), z(2, B, H)
         self._dh1, self._dh0, self._dmu, self._dlsr = z(B, H), z(B, H), z(B, A), z(B, A)
-        for p in list(self.actor.parameters()) + list(self.q.parameters()) + [self.log_alpha]:
-            p.grad = torch.zeros_like(p)
+        # the gradients as views of two flat buffers -- the critics', and the actor's with the
+        # entropy coefficient's (the groups each Adam launch steps): the data-parallel
+        # reduction is one all-reduce per group, on the update's stream (graph-capturable with
+        # an RCCL comm)
+        def flat_grads(params):
+            n = sum(p.numel() for p in params)
+            flat = torch.zeros(n, dtype=torch.float32, device=d)
+            off = 0
+            for p in params:
+                p.grad = flat[off:off + p.numel()].view_as(p)
+                off += p.numel()
+            return flat
+        self._gq = flat_grads(list(self.q.parameters()))
+        self._ga = flat_grads(list(self.actor.parameters()) + [self.log_alpha])
 
     def attach_policy_noise(self, eps):
         """Philox noise: each update also fills `eps` (fp32, contiguous) with N(0, 1) draws for
@@ -707,8 +743,8 @@ class FusedSAC(SAC):
         self._mm(0, 1, self._dg1, q.w1, self._dg0, B, 2)
         f("sf_critic_bwd_in", self._dg0, self._g0, o, W, od, a, W, A, B, q.w0.grad, q.b0.grad,
           self._g1, self._dq, q.w2, q.w2.grad, q.b1.grad, q.b2.grad)
-        if self.world > 1:
-            self._allreduce(list(self.q.parameters()))
+        if self.world > 1 or self.comm is not None:
+            self._reduce_flat(self._gq)
         self.opt_q.step()                            # (the step count was advanced by the sample)
         # ---- actor loss through the updated critics on [o, ap] (critics frozen) ----------------
         ap, lp = act[B:], logp[B:]
@@ -731,8 +767,8 @@ class FusedSAC(SAC):
           self._dmu, self._dlsr, h1b, self._dh1, lp, float(self.target_entropy), A,
           lat.mu.weight.grad, lat.log_std.weight.grad, la_[2].bias.grad, lat.mu.bias.grad,
           lat.log_std.bias.grad, self.log_alpha.grad)
-        if self.world > 1:
-            self._allreduce(list(self.actor.parameters()) + [self.log_alpha])
+        if self.world > 1 or self.comm is not None:
+            self._reduce_flat(self._ga)
         self.opt_a.step()                            # actor + log_alpha in one launch
         if losses:
             return self._lossq.sum(), self._lossa.sum()
