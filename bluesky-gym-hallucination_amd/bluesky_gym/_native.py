@@ -94,8 +94,15 @@ EXPORTED_SYMBOLS = (
     "bsg_set_learner", "bsg_policy_sac", "bsg_lookahead_bytes", "bsg_set_lookahead",
     "bsg_comm_last_error", "bsg_comm_unique_id", "bsg_comm_create", "bsg_comm_destroy",
     "bsg_comm_all_gather", "bsg_comm_wait", "bsg_comm_get_info", "bsg_step_gather",
-    "bsg_comm_all_reduce",
+    "bsg_comm_all_reduce", "bsg_set_params",
 )
+# include/bsg.h BSG_MP_*: MergeEnv-v0's module constants (merge_env.py:13-46), in this order,
+# with the reference's values (bsg_create's defaults)
+MERGE_PARAMS = (("D_HEADING", 15.0), ("D_SPEED", 20.0), ("INTRUSION_DISTANCE", 4.0),
+                ("DISTANCE_MARGIN", 10.0), ("REACH_REWARD", 1.0), ("DRIFT_PENALTY", -0.1),
+                ("INTRUSION_PENALTY", -1.0), ("SPAWN_DISTANCE_MIN", 50.0),
+                ("SPAWN_DISTANCE_MAX", 200.0), ("INTRUDER_DISTANCE_MIN", 20.0),
+                ("INTRUDER_DISTANCE_MAX", 500.0))
 REDUCE_SUM, REDUCE_AVG = 0, 1   # include/bsg.h BSG_REDUCE_*
 COMM_ID_BYTES = 128          # include/bsg.h BSG_COMM_ID_BYTES
 COMM_SLOTS = 16              # BSG_COMM_SLOTS
@@ -187,6 +194,8 @@ def load_library(path: str | None = None):
                                         C.c_void_p]
     lib.bsg_comm_wait.restype = C.c_int32
     lib.bsg_comm_wait.argtypes = [C.c_void_p, C.c_int32, C.c_void_p]
+    lib.bsg_set_params.restype = C.c_int32
+    lib.bsg_set_params.argtypes = [C.c_void_p, C.c_void_p, C.c_int32]
     lib.bsg_comm_all_reduce.restype = C.c_int32
     lib.bsg_comm_all_reduce.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_int32, C.c_void_p]
     lib.bsg_comm_get_info.restype = C.c_int32

@@ -67,6 +67,8 @@ class EnvKindConfig:
     simdt: float
     max_episode_steps: int
     kind_option: int = 0
+    # MergeEnv-v0: its module constants (_native.MERGE_PARAMS order), () = the reference's
+    params: tuple = ()
 
     def to_c(self, num_envs, autoreset, compute_cd, seed, device, env_offset=0) -> nat.BsgConfig:
         c = nat.BsgConfig()
@@ -97,14 +99,26 @@ class EnvKindConfig:
 
 
 def merge_config(num_ac=20, num_ac_state=5, action_frequency=10, simdt=5.0,
-                 max_episode_steps=50, ac_spd=None):
-    """ac_spd: creation CAS [m/s] of every aircraft; None = merge_env.py:30's AC_SPD = 100.
-    Another value is a test hook (the logged revision of DESIGN.md §5), not the reference."""
+                 max_episode_steps=50, ac_spd=None, params=None):
+    """ac_spd: creation CAS [m/s] of every aircraft (merge_env.py:30 AC_SPD); None = 100.
+    params: {name: value} for any of merge_env.py:13-28's D_HEADING, D_SPEED,
+    INTRUSION_DISTANCE, DISTANCE_MARGIN, REACH_REWARD, DRIFT_PENALTY, INTRUSION_PENALTY,
+    SPAWN_DISTANCE_MIN/MAX, INTRUDER_DISTANCE_MIN/MAX (the others keep the reference's
+    values); handed to the kernel by bsg_set_params."""
     opt = 0 if ac_spd is None or int(ac_spd) == 100 else int(ac_spd)
     if ac_spd is not None and float(ac_spd) != int(ac_spd):
         raise ValueError("ac_spd must be a whole number of m/s")
+    vals = ()
+    if params:
+        names = [n for n, _ in nat.MERGE_PARAMS]
+        bad = set(params) - set(names)
+        if bad:
+            raise ValueError(f"merge_config: unknown params {sorted(bad)}; known {names}")
+        full = [float(params.get(n, v)) for n, v in nat.MERGE_PARAMS]
+        if full != [v for _, v in nat.MERGE_PARAMS]:
+            vals = tuple(full)
     return EnvKindConfig(nat.ENV_MERGE, num_ac, num_ac_state, action_frequency, simdt,
-                         max_episode_steps, opt)
+                         max_episode_steps, opt, vals)
 
 
 def vertical_config(num_intruders=5, action_frequency=30, simdt=1.0, max_episode_steps=300):

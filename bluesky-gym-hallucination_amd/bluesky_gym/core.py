@@ -59,6 +59,9 @@ class DeviceBatch:
         ctx = C.c_void_p()
         nat.check(self.lib.bsg_create(C.byref(ccfg), C.byref(ctx)), "bsg_create")
         self._ctx = ctx
+        if getattr(cfg, "params", ()):
+            pv = (C.c_double * len(cfg.params))(*cfg.params)
+            nat.check(self.lib.bsg_set_params(ctx, pv, len(cfg.params)), "bsg_set_params")
         self._alloc()
         self._bind()
         self.lookahead = False

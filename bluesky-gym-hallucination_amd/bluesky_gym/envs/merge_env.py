@@ -1,12 +1,18 @@
 """MergeEnv-v0 -- drop-in for bluesky_gym/envs/merge_env.py (class MergeEnv, :48).
 
-Module constants mirror merge_env.py:13-46; patching them (e.g. ``NUM_AC = 32``) before
-constructing an env changes the env exactly as it would the reference.
+Module constants mirror merge_env.py:13-46; patching them before constructing an env
+changes the env as it would the reference.  Live: NUM_AC, NUM_AC_STATE, ACTION_FREQUENCY,
+AC_SPD (a whole number of m/s), D_HEADING, D_SPEED, INTRUSION_DISTANCE, DISTANCE_MARGIN,
+REACH_REWARD, DRIFT_PENALTY, INTRUSION_PENALTY, SPAWN_DISTANCE_MIN/MAX and
+INTRUDER_DISTANCE_MIN/MAX (the kernel's through bsg_set_params, the spawn draws through
+spawn.merge_spawn).  Not live: NM2KM / MpS2Kt (unit constants), NUM_WAYPOINTS (unused by the
+reference), RWY_* / FIX_* (the route is the kernel's configuration, config.RWY_LAT/FIX_LAT).
 """
 from __future__ import annotations
 
 import numpy as np
 
+from .. import _native as nat
 from .. import config as cfgmod
 from .. import spawn as spawnmod
 from ._single import SingleEnvBase, nan_if_zero
@@ -41,14 +47,18 @@ class MergeEnv(SingleEnvBase):
                  compute_cd=False):
         n = NUM_AC if num_ac is None else num_ac
         k = NUM_AC_STATE if num_ac_state is None else num_ac_state
-        self._init_batch(cfgmod.merge_config(n, k, ACTION_FREQUENCY, 5.0, 0), render_mode,
-                         device, compute_cd)
+        params = {name: globals()[name] for name, _ in nat.MERGE_PARAMS}
+        self._init_batch(cfgmod.merge_config(n, k, ACTION_FREQUENCY, 5.0, 0, ac_spd=AC_SPD,
+                                             params=params), render_mode, device, compute_cd)
         self.nac = n
         self.wpt_lat, self.wpt_lon = FIX_LAT, FIX_LON
         self.rwy_lat, self.rwy_lon = RWY_LAT, RWY_LON
 
     def _spawn(self):
-        return spawnmod.merge_spawn(self.nac)          # global `random`, reference order
+        # global `random`, reference order, this module's (patchable) constants
+        return spawnmod.merge_spawn(self.nac, d_heading=D_HEADING,
+                                    spawn_range=(SPAWN_DISTANCE_MIN, SPAWN_DISTANCE_MAX),
+                                    intruder_range=(INTRUDER_DISTANCE_MIN, INTRUDER_DISTANCE_MAX))
 
     def _info(self):
         e = self.batch.envs

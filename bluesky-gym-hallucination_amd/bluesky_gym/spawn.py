@@ -40,13 +40,17 @@ def _vcas2tas(cas, h):
     return np.where(cas < 0, -1 * tas, tas)
 
 
-def merge_spawn(num_ac, rng=None):
+def merge_spawn(num_ac, rng=None, d_heading=None, spawn_range=None, intruder_range=None):
+    """d_heading / spawn_range / intruder_range: merge_env.py's D_HEADING,
+    SPAWN_DISTANCE_MIN/MAX, INTRUDER_DISTANCE_MIN/MAX (None: the reference's values)."""
     rng = _random if rng is None else rng
-    out = [rng.uniform(-D_HEADING, D_HEADING),
-           rng.uniform(SPAWN_DISTANCE_MIN, SPAWN_DISTANCE_MAX)]
+    dh = D_HEADING if d_heading is None else d_heading
+    s0, s1 = (SPAWN_DISTANCE_MIN, SPAWN_DISTANCE_MAX) if spawn_range is None else spawn_range
+    i0, i1 = (INTRUDER_DISTANCE_MIN, INTRUDER_DISTANCE_MAX) if intruder_range is None else intruder_range
+    out = [rng.uniform(-dh, dh), rng.uniform(s0, s1)]
     for _ in range(num_ac - 1):
-        out.append(rng.uniform(-D_HEADING, D_HEADING))
-        out.append(rng.uniform(INTRUDER_DISTANCE_MIN, INTRUDER_DISTANCE_MAX))
+        out.append(rng.uniform(-dh, dh))
+        out.append(rng.uniform(i0, i1))
     return np.array(out, np.float64)
 
 

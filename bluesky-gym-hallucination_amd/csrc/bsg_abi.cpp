@@ -55,6 +55,8 @@ struct bsg_ctx {
   int spawn_k_state = 0;
   double spawn_k[8] = {};
   double* spawn_k_dev = nullptr;
+  // the env module's constants (bsg_set_params; Merge: merge_env.py:13-46)
+  double kp[BSG_MERGE_NPARAMS] = {15.0, 20.0, 4.0, 10.0, 1.0, -0.1, -1.0, 50.0, 200.0, 20.0, 500.0};
 };
 
 namespace {
@@ -130,6 +132,7 @@ bsg::KParams make_params(const bsg_ctx* c, int mode) {
   p.no_fastpath = c->no_fastpath;
   p.spawn_k_ok = c->spawn_k_state == 1 ? 1 : 0;
   for (int k = 0; k < 8; ++k) p.spawn_k[k] = c->spawn_k[k];
+  for (int k = 0; k < BSG_MERGE_NPARAMS; ++k) p.kp[k] = c->kp[k];
   return p;
 }
 
@@ -430,6 +433,26 @@ int32_t bsg_create(const bsg_config* cfg, bsg_ctx** out) {
   if (const char* pad = std::getenv("BSG_LDS_PAD_BYTES")) c->lds_pad = (unsigned)std::atoi(pad);
   if (const char* nf = std::getenv("BSG_NO_FASTPATH")) c->no_fastpath = std::atoi(nf) != 0;
   *out = c;
+  return BSG_OK;
+}
+
+int32_t bsg_set_params(bsg_ctx* c, const double* v, int32_t n) {
+  if (!c || !v) return fail(BSG_E_INVALID_ARG, "bsg_set_params: null argument");
+  if (c->cfg.env_kind != BSG_ENV_MERGE)
+    return fail(BSG_E_UNSUPPORTED, "bsg_set_params: MergeEnv only");
+  if (n != BSG_MERGE_NPARAMS)
+    return fail(BSG_E_INVALID_ARG, "bsg_set_params: %d values, MergeEnv takes %d", (int)n,
+                (int)BSG_MERGE_NPARAMS);
+  if (c->launch_count > 0)
+    return fail(BSG_E_STATE, "bsg_set_params: the ctx has launched already");
+  for (int k = 0; k < n; ++k)
+    if (!std::isfinite(v[k])) return fail(BSG_E_INVALID_ARG, "bsg_set_params: value %d not finite", k);
+  if (!(v[BSG_MP_D_HEADING] >= 0.0) || !(v[BSG_MP_SPAWN_DISTANCE_MIN] >= 0.0) ||
+      !(v[BSG_MP_SPAWN_DISTANCE_MIN] <= v[BSG_MP_SPAWN_DISTANCE_MAX]) ||
+      !(v[BSG_MP_INTRUDER_DISTANCE_MIN] >= 0.0) ||
+      !(v[BSG_MP_INTRUDER_DISTANCE_MIN] <= v[BSG_MP_INTRUDER_DISTANCE_MAX]))
+    return fail(BSG_E_INVALID_ARG, "bsg_set_params: D_HEADING < 0 or a distance range out of order");
+  for (int k = 0; k < n; ++k) c->kp[k] = v[k];
   return BSG_OK;
 }
 

@@ -98,6 +98,8 @@ struct KParams {
   // not available (cre and the memo as before).
   double spawn_k[8];
   int spawn_k_ok;
+  // the env module's constants (bsg_set_params, include/bsg.h BSG_MP_*; Merge)
+  double kp[BSG_MERGE_NPARAMS];
 };
 
 hipError_t launch_step(const KParams& p, hipStream_t stream);

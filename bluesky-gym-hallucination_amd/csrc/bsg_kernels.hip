@@ -1056,9 +1056,10 @@ __device__ __forceinline__ void spawn_merge_pos(const KParams& p, int e, int j, 
   } else {
     U4 r = philox4x32_10((uint32_t)(e + p.cfg.env_offset), episode, (uint32_t)j, TAG_MERGE, p.seed);
     double ua = u01_53(r.x, r.y), ub = u01_53(r.z, r.w);
-    const double a = -15.0, b = 15.0;                       // +-D_HEADING (merge_env.py:27)
+    const double a = -p.kp[BSG_MP_D_HEADING], b = p.kp[BSG_MP_D_HEADING];   // merge_env.py:27
     brg = a + (b - a) * ua;
-    const double dmin = j == 0 ? 50.0 : 20.0, dmax = j == 0 ? 200.0 : 500.0;   // :21-25
+    const double dmin = j == 0 ? p.kp[BSG_MP_SPAWN_DISTANCE_MIN] : p.kp[BSG_MP_INTRUDER_DISTANCE_MIN];
+    const double dmax = j == 0 ? p.kp[BSG_MP_SPAWN_DISTANCE_MAX] : p.kp[BSG_MP_INTRUDER_DISTANCE_MAX];
     dist = dmin + (dmax - dmin) * ub;
   }
   get_point_at_distance(p.cfg.wpt_lat[0], p.cfg.wpt_lon[0], dist, brg, lat, lon);
@@ -1346,7 +1347,8 @@ struct OwnPre { double wlat, wlon, wdist, drift, sd, cd; };
 
 template <int KIND, class LT>
 __device__ __forceinline__ bool lane_obs(const LT& L, int base, int lane, double o[7],
-                                         double* sortkey, OwnPre* own = nullptr) {
+                                         double* sortkey, OwnPre* own = nullptr,
+                                         double intr_nm = 4.0) {
   const double lat0 = L.lat[base], lon0 = L.lon[base], hdg0 = L.hdg[base];
   const bool is_own = own != nullptr && lane == base;
   const double latj = is_own ? own->wlat : L.lat[lane], lonj = is_own ? own->wlon : L.lon[lane];
@@ -1378,7 +1380,7 @@ __device__ __forceinline__ bool lane_obs(const LT& L, int base, int lane, double
     sincos_t(track, &st, &ct);
     o[0] = x_r; o[1] = y_r; o[2] = vx_r; o[3] = vy_r; o[4] = ct; o[5] = st; o[6] = dmat;
     *sortkey = dmat;
-    return dist < 4;                                       // _check_intrusion :280-281
+    return dist < intr_nm;                  // _check_intrusion :280-281 (INTRUSION_DISTANCE)
   } else if constexpr (KIND == BSG_ENV_SECTOR_CR) {
     // sector_cr_env.py:245-278: positions in the flat NM frame about CENTER, in metres
     const double cc = cos_t(SC_CLAT * kD2R);
@@ -2268,7 +2270,7 @@ __device__ __forceinline__ void propagate(const KParams& p, int e, int j, size_t
   const AC s0 = s;                  // as loaded: the cross-step memo's keys (memo_load)
   if (j == 0) {
     if constexpr (KIND == BSG_ENV_MERGE) {
-      hdg_spd_action<WIND>(p, s, act[0], act[1], 15.0, 20.0);
+      hdg_spd_action<WIND>(p, s, act[0], act[1], p.kp[BSG_MP_D_HEADING], p.kp[BSG_MP_D_SPEED]);
     } else if constexpr (KIND == BSG_ENV_STATIC_OBSTACLE) {
       hdg_spd_action<WIND>(p, s, act[0], act[1], 45.0, 20.0 / 3.0);
     } else if constexpr (KIND == BSG_ENV_SECTOR_CR) {
@@ -3013,9 +3015,10 @@ __global__ __launch_bounds__(64 * CDW) BSG_WPE void step_kernel(KParams p) {
     const int w = ev.wpt_reach == 0 ? 0 : 1;
     own.wlat = p.cfg.wpt_lat[w];
     own.wlon = p.cfg.wpt_lon[w];
-    if (on) intr = lane_obs<KIND>(L, base, lane, o, &sortkey, &own);
+    if (on) intr = lane_obs<KIND>(L, base, lane, o, &sortkey, &own, p.kp[BSG_MP_INTRUSION_DISTANCE]);
   } else {
-    if (kLaneObs && on && j > 0) intr = lane_obs<KIND>(L, base, lane, o, &sortkey);
+    if (kLaneObs && on && j > 0)
+      intr = lane_obs<KIND>(L, base, lane, o, &sortkey, nullptr, p.kp[BSG_MP_INTRUSION_DISTANCE]);
   }
   if constexpr (kRanked) {
     if (wv == 0) L.d[lane] = sortkey;
@@ -3101,10 +3104,12 @@ __global__ __launch_bounds__(64 * CDW) BSG_WPE void step_kernel(KParams p) {
         // _check_waypoint :257-268 ; _check_drift :270-273 ; _check_intrusion :275-284
         const int wr = ev.wpt_reach;
         int reach = 0;
-        if (wdist < 10 && wr != 1) { ev.wpt_reach = 1; ev.faf_reached = 1; reach = 1; }
-        else if (wdist < 2 * 10 && wr == 1) { ev.faf_reached = 2; d = 1; }
+        const double margin = p.kp[BSG_MP_DISTANCE_MARGIN];
+        if (wdist < margin && wr != 1) { ev.wpt_reach = 1; ev.faf_reached = 1; reach = 1; }
+        else if (wdist < 2 * margin && wr == 1) { ev.faf_reached = 2; d = 1; }
         const double dd = fabs(drift * kD2R);
-        r = ((double)reach + dd * -0.1) + (double)(nintr * -1);
+        r = ((double)reach * p.kp[BSG_MP_REACH_REWARD] + dd * p.kp[BSG_MP_DRIFT_PENALTY]) +
+            (double)nintr * p.kp[BSG_MP_INTRUSION_PENALTY];
         ev.drift_sum += dd;
       } else if constexpr (kPlan) {
         // _get_reward :135-146 / _check_waypoint :215-227: +1 per newly reached waypoint

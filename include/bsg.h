@@ -258,6 +258,27 @@ int32_t bsg_step(bsg_ctx* ctx, const double* actions, const double* spawn, void*
  * call bsg_bind again (gs/trk become required; obs rows may widen). */
 int32_t bsg_set_wind(bsg_ctx* ctx, const bsg_wind* wind);
 
+/* The env module's constants (MergeEnv-v0: merge_env.py:13-46), so that a caller that patches
+ * them (the drop-in bluesky_gym.envs.merge_env reads its module globals at construction)
+ * changes the device env as it would the reference: values[BSG_MERGE_NPARAMS] in the order
+ * below (the reference's units: degrees, m/s, NM, km as merge_env.py compares them).  Each
+ * defaults to the reference's value at bsg_create.  AC_SPD is bsg_config.kind_option.
+ * Merge only; call before the first bsg_reset / bsg_step of the ctx (BSG_E_STATE after). */
+enum { BSG_MP_D_HEADING = 0,          /* merge_env.py:27: +-deg of the HDG action and of the
+                                          spawn bearings (:115, :150) */
+       BSG_MP_D_SPEED,                /* :28: m/s of the SPD action */
+       BSG_MP_INTRUSION_DISTANCE,     /* :19: NM, _check_intrusion */
+       BSG_MP_DISTANCE_MARGIN,        /* :13: _check_waypoint (compared with the NM distance) */
+       BSG_MP_REACH_REWARD,           /* :14 */
+       BSG_MP_DRIFT_PENALTY,          /* :16 */
+       BSG_MP_INTRUSION_PENALTY,      /* :17 */
+       BSG_MP_SPAWN_DISTANCE_MIN,     /* :21-22: the ownship's spawn distance to the FAF */
+       BSG_MP_SPAWN_DISTANCE_MAX,
+       BSG_MP_INTRUDER_DISTANCE_MIN,  /* :24-25: the intruders' */
+       BSG_MP_INTRUDER_DISTANCE_MAX,
+       BSG_MERGE_NPARAMS };
+int32_t bsg_set_params(bsg_ctx* ctx, const double* values, int32_t count);
+
 /* Observation row length of this ctx (bsg_obs_dim + 2 with an augmenting wind field). */
 int32_t bsg_ctx_obs_dim(const bsg_ctx* ctx);
 

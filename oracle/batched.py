@@ -270,13 +270,28 @@ class MergeOracle(_Base):
 
     def __init__(self, num_envs, num_ac=20, num_ac_state=5, action_frequency=10, simdt=5.0,
                  max_episode_steps=50, autoreset=AUTORESET_NEXT_STEP, seed=0,
-                 compute_cd=True, ac_spd=MERGE_AC_SPD):
+                 compute_cd=True, ac_spd=MERGE_AC_SPD, params=None):
         """ac_spd: creation CAS of every aircraft (merge_env.py:30 AC_SPD = 100; another value
-        restates the logged revision of DESIGN.md §5, tests/test_ref_logs.py)."""
+        restates the logged revision of DESIGN.md §5, tests/test_ref_logs.py).  params:
+        {name: value} overriding merge_env.py:13-28's module constants by their names
+        (D_HEADING, D_SPEED, INTRUSION_DISTANCE, DISTANCE_MARGIN, REACH_REWARD, DRIFT_PENALTY,
+        INTRUSION_PENALTY, SPAWN_DISTANCE_MIN/MAX, INTRUDER_DISTANCE_MIN/MAX), as a caller
+        patching the reference module would."""
         super().__init__(num_envs, num_ac, action_frequency, simdt, max_episode_steps,
                          autoreset, seed)
         assert num_ac - 1 >= num_ac_state
         self.ac_spd = float(ac_spd)
+        self.k = dict(D_HEADING=MERGE_D_HEADING, D_SPEED=MERGE_D_SPEED,
+                      INTRUSION_DISTANCE=MERGE_INTRUSION_DISTANCE,
+                      DISTANCE_MARGIN=MERGE_DISTANCE_MARGIN, REACH_REWARD=MERGE_REACH_REWARD,
+                      DRIFT_PENALTY=MERGE_DRIFT_PENALTY, INTRUSION_PENALTY=MERGE_INTRUSION_PENALTY,
+                      SPAWN_DISTANCE_MIN=MERGE_SPAWN_DISTANCE_MIN,
+                      SPAWN_DISTANCE_MAX=MERGE_SPAWN_DISTANCE_MAX,
+                      INTRUDER_DISTANCE_MIN=MERGE_INTRUDER_DISTANCE_MIN,
+                      INTRUDER_DISTANCE_MAX=MERGE_INTRUDER_DISTANCE_MAX)
+        unknown = set(params or {}) - set(self.k)
+        assert not unknown, f"unknown Merge constants {sorted(unknown)}"
+        self.k.update(params or {})
         self.K = int(num_ac_state)
         self.compute_cd = compute_cd
         self.wpt_reach = np.zeros(self.E, np.int32)
@@ -296,10 +311,11 @@ class MergeOracle(_Base):
                                               j, philox.TAG_MERGE, self.seed)
         ua = philox.u01_53(x0, x1)
         ub = philox.u01_53(x2, x3)
-        a, b = -MERGE_D_HEADING, MERGE_D_HEADING
+        k = self.k
+        a, b = -k["D_HEADING"], k["D_HEADING"]
         brg = a + (b - a) * ua
-        dmin = np.where(j == 0, MERGE_SPAWN_DISTANCE_MIN, MERGE_INTRUDER_DISTANCE_MIN).astype(np.float64)
-        dmax = np.where(j == 0, MERGE_SPAWN_DISTANCE_MAX, MERGE_INTRUDER_DISTANCE_MAX).astype(np.float64)
+        dmin = np.where(j == 0, k["SPAWN_DISTANCE_MIN"], k["INTRUDER_DISTANCE_MIN"]).astype(np.float64)
+        dmax = np.where(j == 0, k["SPAWN_DISTANCE_MAX"], k["INTRUDER_DISTANCE_MAX"]).astype(np.float64)
         dist = dmin + (dmax - dmin) * ub
         out = np.empty((len(env_ids), 2 * self.N))
         out[:, 0::2] = brg
@@ -326,8 +342,8 @@ class MergeOracle(_Base):
     def _apply_action(self, actions):
         """merge_env.py:286-293 + BlueSky HDG / SPD stack commands."""
         st = self.st
-        dh = actions[:, 0] * MERGE_D_HEADING
-        dv = actions[:, 1] * MERGE_D_SPEED
+        dh = actions[:, 0] * self.k["D_HEADING"]
+        dv = actions[:, 1] * self.k["D_SPEED"]
         heading_new = bsx.bound_angle_positive_negative_180(st.hdg[:, 0] + dh)
         speed_new = (st.cas[:, 0] + dv) * MPS2KT
         st.ap_trk[:, 0] = bsx.selhdg_track(st, (slice(None), 0), heading_new, self.wind)
@@ -385,19 +401,20 @@ class MergeOracle(_Base):
         # _check_waypoint (merge_env.py:257-268)
         wr = self.wpt_reach.copy()
         faf = self.faf_reached.copy()
-        c1 = (wpt_dist < MERGE_DISTANCE_MARGIN) & (wr != 1)
-        c2 = ~c1 & (wpt_dist < 2 * MERGE_DISTANCE_MARGIN) & (wr == 1)
-        reach_reward = np.where(c1, MERGE_REACH_REWARD, 0)
+        k = self.k
+        c1 = (wpt_dist < k["DISTANCE_MARGIN"]) & (wr != 1)
+        c2 = ~c1 & (wpt_dist < 2 * k["DISTANCE_MARGIN"]) & (wr == 1)
+        reach_reward = np.where(c1, k["REACH_REWARD"], 0)
         new_wr = np.where(c1, 1, wr)
         new_faf = np.where(c1, 1, np.where(c2, 2, faf))
         done = c2
         # _check_drift (:270-273)
         d = np.abs(np.deg2rad(drift))
-        drift_reward = d * MERGE_DRIFT_PENALTY
+        drift_reward = d * k["DRIFT_PENALTY"]
         # _check_intrusion (:275-284), intruders by index
-        intr = dist < MERGE_INTRUSION_DISTANCE
+        intr = dist < k["INTRUSION_DISTANCE"]
         nintr = intr.sum(axis=1)
-        intrusion_reward = nintr * MERGE_INTRUSION_PENALTY
+        intrusion_reward = nintr * k["INTRUSION_PENALTY"]
         reward = reach_reward + drift_reward + intrusion_reward
         intr_mask = np.zeros(self.E, np.uint64)
         for i in range(self.N - 1):

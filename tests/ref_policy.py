@@ -253,12 +253,18 @@ KNOWN_RED.update({
     ("merge_sat_100", "average_drift"): _MERGE_DRIFT,
 })
 # Regression bounds on the known-red z of the reference's own creation speed: the
-# whitelist above must not hide a further drift of the default config.  z against either log,
-# oracle (2,048 envs) and device (4,096 envs) rollouts at MMO 0.80: intrusions +3.5..+3.8,
-# reward -3.4..-3.6, drift -4.1..-4.3; the bounds leave ~2 SE of sampling room each side.
-MERGE_SAT_Z_BOUNDS = {("merge_sat_100", "total_intrusions"): (1.5, 6.0),
-                      ("merge_sat_100", "total_reward"): (-6.0, -1.5),
-                      ("merge_sat_100", "average_drift"): (-6.5, -2.0)}
+# whitelist above must not hide a further drift of the default config.  Derived from the runs
+# they guard (tools/merge_sat_z.py, profiles/r06/merge_sat_z_{oracle,
+# device}.json): z against either log over 6 oracle seeds (2,048 envs, tests/test_ref_logs.py's
+# size; its seed 11 reads intrusions +3.76 / +3.54) and 8 device seeds (4,096 envs, tests/
+# test_gpu_ref_logs.py's size; its seed 7 reads +5.50 / +5.28):
+#   intrusions +3.22 .. +5.77 (seed-to-seed sd 0.70 oracle, 0.55 device)
+#   reward     -5.65 .. -3.11 (sd 0.71 / 0.55)
+#   drift      -4.58 .. -2.92 (sd 0.44 / 0.32)
+# Bounds: the measured range widened by two seed-to-seed sd (the larger of the two) each side.
+MERGE_SAT_Z_BOUNDS = {("merge_sat_100", "total_intrusions"): (1.8, 7.2),
+                      ("merge_sat_100", "total_reward"): (-7.1, -1.7),
+                      ("merge_sat_100", "average_drift"): (-5.5, -2.0)}
 
 
 def merge_logs():

@@ -189,6 +189,67 @@ def test_merge_batch_autoreset_parity(bg, autoreset):
             close(b.final_obs.cpu().numpy()[d], r["final_obs"][d], f"final_obs t={t}")
 
 
+PATCHED = {"D_HEADING": 30.0, "INTRUSION_DISTANCE": 9.0, "DISTANCE_MARGIN": 25.0,
+           "DRIFT_PENALTY": -0.25, "INTRUDER_DISTANCE_MAX": 150.0}
+
+
+@pytest.mark.parametrize("lookahead", [True, False])
+def test_merge_patched_constants_parity(bg, lookahead):
+    """VERDICT r05 next #4 (missing #4): merge_env.py's module constants reach the kernel
+    (bsg_set_params).  Five of them patched -- the HDG action and spawn bearing range, the
+    intrusion radius, the waypoint margin, the drift penalty, the intruders' spawn range (so
+    intrusions are frequent) -- on the device and, by the same names, on the oracle: every
+    output bit-exact / within the bar over 110 steps with NEXT_STEP autoresets, with the
+    lookahead (its spawn cache and the lookahead waves' spawns) and without."""
+    core, config, nat = bg
+    E, N, T = 256, 32, 110
+    b = core.DeviceBatch(config.merge_config(num_ac=N, params=PATCHED), E, compute_cd=True,
+                         seed=321, lookahead=lookahead)
+    o = ob.MergeOracle(E, num_ac=N, seed=321, compute_cd=True, params=PATCHED)
+    close(b.reset().cpu().numpy(), o.reset()["obs"], "reset obs")
+    rng = np.random.default_rng(8)
+    for t in range(T):
+        a = rng.uniform(-1, 1, (E, 2))
+        b.step(torch.from_numpy(a))
+        r = o.step(a)
+        _compare_step(b, r, N, "merge", t)
+    # the patch matters: the unpatched oracle differs
+    o2 = ob.MergeOracle(E, num_ac=N, seed=321, compute_cd=True)
+    assert not np.array_equal(o2.reset()["obs"], o.reset()["obs"])
+
+
+def test_merge_env_module_constants_are_live(bg):
+    """The drop-in MergeEnv reads merge_env.py's constants at construction, as the reference
+    module does: patched D_SPEED / INTRUSION_DISTANCE / SPAWN_DISTANCE_MIN change the env,
+    and it matches the oracle restated with the same patch on the same Python-random spawn."""
+    import random
+    from bluesky_gym.envs import merge_env as me
+    from bluesky_gym import spawn as spawnmod
+    patch = {"D_SPEED": 35.0, "INTRUSION_DISTANCE": 12.0, "SPAWN_DISTANCE_MIN": 80.0}
+    saved = {k: getattr(me, k) for k in patch}
+    try:
+        for k, v in patch.items():
+            setattr(me, k, v)
+        env = me.MergeEnv(num_ac=16)
+        random.seed(5)
+        env.reset()
+        random.seed(5)
+        sp = spawnmod.merge_spawn(16, spawn_range=(80.0, 200.0))
+        o = ob.MergeOracle(1, num_ac=16, autoreset=ob.AUTORESET_NONE, params=patch)
+        o.reset(spawn=sp[None, :])
+        rng = np.random.default_rng(4)
+        for t in range(30):
+            a = rng.uniform(-1, 1, 2)
+            obs, rew, term, trunc, info = env.step(a)
+            r = o.step(a[None, :])
+            close(env.batch.obs.cpu().numpy(), r["obs"], f"obs t={t}")
+            close([rew], r["reward"], f"reward t={t}")
+            assert info["total_intrusions"] == int(o.info()["total_intrusions"][0])
+    finally:
+        for k, v in saved.items():
+            setattr(me, k, v)
+
+
 @pytest.mark.parametrize("N", [6, 32])
 def test_vertical_batch_autoreset_parity(bg, N):
     core, config, nat = bg
