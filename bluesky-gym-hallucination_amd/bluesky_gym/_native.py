@@ -94,8 +94,10 @@ EXPORTED_SYMBOLS = (
     "bsg_set_learner", "bsg_policy_sac", "bsg_lookahead_bytes", "bsg_set_lookahead",
     "bsg_comm_last_error", "bsg_comm_unique_id", "bsg_comm_create", "bsg_comm_destroy",
     "bsg_comm_all_gather", "bsg_comm_wait", "bsg_comm_get_info", "bsg_step_gather",
-    "bsg_comm_all_reduce", "bsg_set_params",
+    "bsg_comm_all_reduce", "bsg_set_params", "bsg_trajectory_bytes", "bsg_set_trajectory",
+    "bsg_trajectory_info",
 )
+TRAJ_SYNC = 1                # include/bsg.h BSG_TRAJ_SYNC
 # include/bsg.h BSG_MP_*: MergeEnv-v0's module constants (merge_env.py:13-46), in this order,
 # with the reference's values (bsg_create's defaults)
 MERGE_PARAMS = (("D_HEADING", 15.0), ("D_SPEED", 20.0), ("INTRUSION_DISTANCE", 4.0),
@@ -176,6 +178,12 @@ def load_library(path: str | None = None):
     lib.bsg_ctx_obs_dim.argtypes = [C.c_void_p]
     lib.bsg_lookahead_bytes.restype = C.c_int64
     lib.bsg_lookahead_bytes.argtypes = [C.c_void_p]
+    lib.bsg_trajectory_bytes.restype = C.c_int64
+    lib.bsg_trajectory_bytes.argtypes = [C.c_void_p]
+    lib.bsg_set_trajectory.restype = C.c_int32
+    lib.bsg_set_trajectory.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_int32]
+    lib.bsg_trajectory_info.restype = C.c_int32
+    lib.bsg_trajectory_info.argtypes = [C.c_void_p, C.c_void_p]
     lib.bsg_set_lookahead.restype = C.c_int32
     lib.bsg_set_lookahead.argtypes = [C.c_void_p, C.c_void_p, C.c_int64]
     lib.bsg_policy_sac.restype = C.c_int32

@@ -4,6 +4,8 @@ the HIP kernels (csrc/bsg_kernels.hip).  There is no CPU fallback.
 """
 from __future__ import annotations
 
+import os
+
 import ctypes as C
 
 import torch
@@ -25,9 +27,13 @@ class DeviceBatch:
     # auto lookahead up to this many envs per GPU: below it the launch leaves SIMDs idle
     # and the intruders' substeps are the critical path (C4 shards); DESIGN.md §3
     LOOKAHEAD_MAX_ENVS = 2048
+    # auto trajectory store (MergeEnv) up to this many envs per GPU: its producer waves share
+    # the SIMDs the step launch leaves idle (C4's 8- and 4-GPU shards); DESIGN.md §6
+    TRAJECTORY_MAX_ENVS = 1024
+
     def __init__(self, cfg: EnvKindConfig, num_envs: int, *, autoreset=nat.AUTORESET_NEXT_STEP,
                  compute_cd=True, seed=0, device=None, learner=False, env_offset=0,
-                 memo_cache=True, lookahead=None):
+                 memo_cache=True, lookahead=None, trajectory=None):
         """lookahead: propagate the intruders (Merge, Vertical) one RL step ahead in extra workgroups
         (bsg_set_lookahead; bit-identical results).  None = on where the library supports
         it and the batch is small enough to leave SIMDs idle (LOOKAHEAD_MAX_ENVS); True /
@@ -77,6 +83,25 @@ class DeviceBatch:
         elif lookahead:
             raise nat.BsgError("lookahead: MergeEnv / VerticalCREnv with NEXT_STEP (or no) "
                                "autoreset only")
+        # trajectory store (bsg_set_trajectory): MergeEnv's future episodes flown ahead on a
+        # low-priority stream, copied by the lookahead (bit-identical).  None = on for the
+        # lookahead's Merge batches up to TRAJECTORY_MAX_ENVS; True / False force it; "sync"
+        # runs the producers on the launch stream (tests)
+        self.trajectory = False
+        self._tj_buf = None
+        tbytes = int(self.lib.bsg_trajectory_bytes(self._ctx)) if self.lookahead else 0
+        # (BSG_TRAJECTORY=0: the automatic choice off -- A/B runs, tools/)
+        want_tj = (trajectory if trajectory is not None
+                   else self.E <= self.TRAJECTORY_MAX_ENVS and os.environ.get("BSG_TRAJECTORY", "1") != "0")
+        if want_tj and tbytes > 0:
+            self._tj_buf = torch.empty((tbytes + 7) // 8, dtype=torch.float64, device=self.device)
+            flags = nat.TRAJ_SYNC if trajectory == "sync" else 0
+            nat.check(self.lib.bsg_set_trajectory(self._ctx, C.c_void_p(self._tj_buf.data_ptr()),
+                                                  tbytes, flags), "bsg_set_trajectory")
+            self.trajectory = True
+        elif trajectory:
+            raise nat.BsgError("trajectory: MergeEnv with the lookahead, NEXT_STEP autoreset and a "
+                               "TimeLimit of 1..64 steps only")
 
     # ------------------------------------------------------------------ buffers
     def _alloc(self):
@@ -252,6 +277,16 @@ class DeviceBatch:
                     faf_reach=self.envs["faf_reached"],
                     drift_sum=self.envs["drift_sum"], step_count=self.envs["step_count"],
                     final_altitude=self.envs["final_altitude"])
+
+    def trajectory_info(self) -> dict:
+        """bsg_trajectory_info and the lookahead's copies from the store per env (the store's
+        diagnostic counters, tests/test_gpu_trajectory.py)."""
+        out = (C.c_int64 * 4)()
+        nat.check(self.lib.bsg_trajectory_info(self._ctx, out), "bsg_trajectory_info")
+        copies = (self._tj_buf[:self.E].view(torch.int64).cpu() if self._tj_buf is not None
+                  else torch.zeros(self.E, dtype=torch.int64))
+        return {"bound": int(out[0]), "producer_launches": int(out[1]), "published": int(out[2]),
+                "generation": int(out[3]), "copies": copies}
 
     def close(self):
         if getattr(self, "_ctx", None) is not None and self._ctx.value:

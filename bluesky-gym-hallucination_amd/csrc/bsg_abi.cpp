@@ -57,6 +57,22 @@ struct bsg_ctx {
   double* spawn_k_dev = nullptr;
   // the env module's constants (bsg_set_params; Merge: merge_env.py:13-46)
   double kp[BSG_MERGE_NPARAMS] = {15.0, 20.0, 4.0, 10.0, 1.0, -0.1, -1.0, 50.0, 200.0, 20.0, 500.0};
+  bool launched = false;            // a reset / step has been enqueued
+  // trajectory store (bsg_set_trajectory; bsg_internal.h tj_doubles): the producers run on
+  // their own stream of the least priority, one launch in flight at a time; a producer launch
+  // is "published" (traj_pub = its sequence number) once the host has seen its completion
+  // event, and every later step launch is ordered after that event on its stream
+  double* traj = nullptr;
+  bool traj_sync = false;           // test hook: producers on the caller's stream, in order
+  uint32_t traj_gen = 1;            // 1..0xFFE; bumped when the stored episodes may be stale
+  uint32_t prod_seq = 0;            // last producer sequence number issued (1..0xFFFFE)
+  uint64_t traj_pub = 0;
+  bool prod_inflight = false;
+  uint32_t prod_inflight_seq = 0;
+  int steps_since_prod = 0;
+  int64_t prod_launches = 0;
+  hipStream_t prod_st = nullptr;
+  hipEvent_t ev_step = nullptr, ev_prod = nullptr;
 };
 
 namespace {
@@ -133,6 +149,9 @@ bsg::KParams make_params(const bsg_ctx* c, int mode) {
   p.spawn_k_ok = c->spawn_k_state == 1 ? 1 : 0;
   for (int k = 0; k < 8; ++k) p.spawn_k[k] = c->spawn_k[k];
   for (int k = 0; k < BSG_MERGE_NPARAMS; ++k) p.kp[k] = c->kp[k];
+  p.traj_gen = c->traj_gen;
+  p.traj_pub = c->traj_pub;
+  p.traj_S = c->cfg.max_episode_steps;
   return p;
 }
 
@@ -256,6 +275,87 @@ int trim_pending(bsg_ctx* c) {
   return BSG_OK;
 }
 
+// ---- trajectory store scheduling ------------------------------------------------------
+constexpr int kProdEvery = 4;       // step launches between producer launches (at least)
+
+// wait for an in-flight producer (its buffers are about to change or go away) and fold it in
+int traj_quiesce(bsg_ctx* c) {
+  if (!c->prod_inflight) return BSG_OK;
+  hipError_t e = hipEventSynchronize(c->ev_prod);
+  if (e != hipSuccess) return hip_fail(e, "hipEventSynchronize(producer)");
+  c->prod_inflight = false;
+  c->traj_pub = c->prod_inflight_seq;
+  return BSG_OK;
+}
+
+void traj_new_gen(bsg_ctx* c) {
+  c->traj_gen = (c->traj_gen % 0xFFEu) + 1u;
+}
+
+// Before a launch: publish a producer launch that has completed (and order this stream after
+// it), and retire the stored episodes when this launch spawns from host rows (the store holds
+// Philox episodes: a host-row episode under the same counter is another episode)
+int traj_before(bsg_ctx* c, hipStream_t st, const double* spawn) {
+  if (c->prod_inflight && hipEventQuery(c->ev_prod) == hipSuccess) {
+    c->prod_inflight = false;
+    c->traj_pub = c->prod_inflight_seq;
+    hipError_t e = hipStreamWaitEvent(st, c->ev_prod, 0);
+    if (e != hipSuccess) return hip_fail(e, "hipStreamWaitEvent(producer)");
+  }
+  if (spawn) traj_new_gen(c);
+  return BSG_OK;
+}
+
+// After a launch: a reset with device spawns flies the episodes it just created and the next
+// ones on this stream (ordered: usable from the next launch on); a step launch starts the
+// next producer launch on the producer stream when none is in flight
+int traj_after(bsg_ctx* c, const bsg::KParams& p0, hipStream_t st, int mode, const double* spawn) {
+  bsg::KParams q = p0;
+  q.actions = nullptr;
+  q.spawn = nullptr;
+  hipError_t e;
+  if (mode == bsg::MODE_RESET) {
+    if (spawn) return BSG_OK;
+    // (the producer memo regions are per episode-ahead d: no two producer launches at once)
+    if (int r = traj_quiesce(c)) return r;
+    q.prod_d0 = 0;
+    q.prod_d1 = 2;
+    q.prod_seq = 0;
+    if ((e = bsg::launch_produce(q, st)) != hipSuccess) return hip_fail(e, "produce launch (reset)");
+    ++c->prod_launches;
+    c->steps_since_prod = kProdEvery;
+    return BSG_OK;
+  }
+  if (mode != bsg::MODE_STEP || c->prod_inflight || ++c->steps_since_prod < kProdEvery) return BSG_OK;
+  c->steps_since_prod = 0;
+  q.env_mask = nullptr;
+  q.prod_d0 = 1;
+  q.prod_d1 = bsg::TJ_D;
+  if (c->traj_sync) {
+    q.prod_seq = 0;
+    if ((e = bsg::launch_produce(q, st)) != hipSuccess) return hip_fail(e, "produce launch");
+    ++c->prod_launches;
+    return BSG_OK;
+  }
+  if (c->prod_seq >= 0xFFFFEu) {            // the header's 20-bit sequence wraps: new generation
+    if (int r = traj_quiesce(c)) return r;
+    c->prod_seq = 0;
+    c->traj_pub = 0;
+    traj_new_gen(c);
+    q.traj_gen = c->traj_gen;
+  }
+  q.prod_seq = ++c->prod_seq;
+  if ((e = hipEventRecord(c->ev_step, st)) != hipSuccess) return hip_fail(e, "hipEventRecord(step)");
+  if ((e = hipStreamWaitEvent(c->prod_st, c->ev_step, 0)) != hipSuccess)
+    return hip_fail(e, "hipStreamWaitEvent(producer stream)");
+  if ((e = bsg::launch_produce(q, c->prod_st)) != hipSuccess) return hip_fail(e, "produce launch");
+  if ((e = hipEventRecord(c->ev_prod, c->prod_st)) != hipSuccess) return hip_fail(e, "hipEventRecord(producer)");
+  c->prod_inflight = true;
+  c->prod_inflight_seq = q.prod_seq;
+  ++c->prod_launches;
+  return BSG_OK;
+}
+
 int launch(bsg_ctx* c, int mode, const double* actions, const double* spawn,
            const uint8_t* env_mask, void* stream) {
   hipError_t e = hipSetDevice(c->cfg.device);
@@ -269,10 +369,19 @@ int launch(bsg_ctx* c, int mode, const double* actions, const double* spawn,
   }
   if (int r = la_prepare(c, st)) return r;
   if (int r = spawn_k_prepare(c, st)) return r;
+  // trajectory store: active with the lookahead itself (no wind, no graph capture)
+  const bool tj = c->traj && la_active(c);
+  if (tj) {
+    if (int r = traj_before(c, st, spawn)) return r;
+  } else if (c->traj) {
+    if (int r = traj_quiesce(c)) return r;
+  }
   bsg::KParams p = make_params(c, mode);
   p.actions = actions;
   p.spawn = spawn;
   p.env_mask = env_mask;
+  p.traj = tj ? c->traj : nullptr;
+  c->launched = true;
 #if defined(BSG_LA_LEGACY) && BSG_LA_LEGACY
   c->la_prime = false;                // negative-control debug builds: round 3 had no priming pass
 #endif
@@ -322,6 +431,7 @@ int launch(bsg_ctx* c, int mode, const double* actions, const double* spawn,
     if (mode == bsg::MODE_STEP) c->la_par ^= 1;   // this step wrote the other slot
     ++c->la_seq;                                   // and the other snapshot
   }
+  if (tj) return traj_after(c, p, st, mode, spawn);
   return BSG_OK;
 }
 
@@ -443,7 +553,7 @@ int32_t bsg_set_params(bsg_ctx* c, const double* v, int32_t n) {
   if (n != BSG_MERGE_NPARAMS)
     return fail(BSG_E_INVALID_ARG, "bsg_set_params: %d values, MergeEnv takes %d", (int)n,
                 (int)BSG_MERGE_NPARAMS);
-  if (c->launch_count > 0)
+  if (c->launched)
     return fail(BSG_E_STATE, "bsg_set_params: the ctx has launched already");
   for (int k = 0; k < n; ++k)
     if (!std::isfinite(v[k])) return fail(BSG_E_INVALID_ARG, "bsg_set_params: value %d not finite", k);
@@ -458,6 +568,11 @@ int32_t bsg_set_params(bsg_ctx* c, const double* v, int32_t n) {
 
 int32_t bsg_destroy(bsg_ctx* c) {
   if (!c) return BSG_OK;
+  (void)traj_quiesce(c);
+  if (c->prod_st) (void)hipStreamSynchronize(c->prod_st);
+  if (c->ev_step) (void)hipEventDestroy(c->ev_step);
+  if (c->ev_prod) (void)hipEventDestroy(c->ev_prod);
+  if (c->prod_st) (void)hipStreamDestroy(c->prod_st);
   for (auto& pr : c->pending) {
     (void)hipEventDestroy(pr.first);
     (void)hipEventDestroy(pr.second);
@@ -492,9 +607,11 @@ int32_t bsg_bind(bsg_ctx* c, const bsg_buffers* b) {
   if (c->cfg.compute_cd && c->cfg.num_ac > 1 &&
       (!b->conf_mask || !b->los_mask || !b->tcpamax || !b->min_sep))
     return fail(BSG_E_INVALID_ARG, "bsg_bind: compute_cd needs conf_mask/los_mask/tcpamax/min_sep");
+  if (int r = traj_quiesce(c)) return r;       // (it reads the episode words of the old buffers)
   c->bufs = *b;
   c->bound = true;
   c->la_dirty = true;               // new buffers: the lookahead restarts from them
+  traj_new_gen(c);
   return BSG_OK;
 }
 
@@ -518,8 +635,73 @@ int32_t bsg_set_lookahead(bsg_ctx* c, void* scratch, int64_t bytes) {
     if (reinterpret_cast<uintptr_t>(scratch) & 7)
       return fail(BSG_E_INVALID_ARG, "bsg_set_lookahead: scratch must be 8-byte aligned");
   }
+  if (int r = traj_quiesce(c)) return r;
   c->la = static_cast<double*>(scratch);
   c->la_dirty = true;               // also re-arms after the caller wrote state directly
+  traj_new_gen(c);
+  return BSG_OK;
+}
+
+int64_t bsg_trajectory_bytes(const bsg_ctx* c) {
+  if (!c) return fail(BSG_E_INVALID_ARG, "bsg_trajectory_bytes: null ctx");
+#if (defined(BSG_LA_WAIT) && BSG_LA_WAIT) || (defined(BSG_ONLY_LA) && BSG_ONLY_LA)
+  return 0;                          // (the lookahead's debug builds test the lookahead alone)
+#else
+  if (c->cfg.env_kind != BSG_ENV_MERGE || c->cfg.autoreset_mode != BSG_AUTORESET_NEXT_STEP ||
+      c->cfg.max_episode_steps < 1 || c->cfg.max_episode_steps > bsg::TJ_SMAX)
+    return 0;
+  return (int64_t)(8 * bsg::tj_doubles((size_t)c->cfg.num_envs, (size_t)c->cfg.num_ac,
+                                       (size_t)c->cfg.max_episode_steps));
+#endif
+}
+
+int32_t bsg_set_trajectory(bsg_ctx* c, void* scratch, int64_t bytes, int32_t flags) {
+  if (!c) return fail(BSG_E_INVALID_ARG, "bsg_set_trajectory: null ctx");
+  if (int r = traj_quiesce(c)) return r;
+  if (!scratch) {
+    c->traj = nullptr;
+    return BSG_OK;
+  }
+  const int64_t need = bsg_trajectory_bytes(c);
+  if (need <= 0)
+    return fail(BSG_E_UNSUPPORTED, "bsg_set_trajectory: MergeEnv with NEXT_STEP autoreset and a "
+                "TimeLimit of 1..%d steps only", bsg::TJ_SMAX);
+  if (!c->la) return fail(BSG_E_STATE, "bsg_set_trajectory: bind the lookahead scratch first");
+  if (bytes < need)
+    return fail(BSG_E_INVALID_ARG, "bsg_set_trajectory: scratch too small (need %lld bytes)",
+                (long long)need);
+  if (reinterpret_cast<uintptr_t>(scratch) & 7)
+    return fail(BSG_E_INVALID_ARG, "bsg_set_trajectory: scratch must be 8-byte aligned");
+  if (flags & ~BSG_TRAJ_SYNC) return fail(BSG_E_INVALID_ARG, "bsg_set_trajectory: unknown flags");
+  hipError_t e = hipSetDevice(c->cfg.device);
+  if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
+  if (!c->prod_st) {
+    int least = 0, greatest = 0;
+    e = hipDeviceGetStreamPriorityRange(&least, &greatest);
+    if (e == hipSuccess) e = hipStreamCreateWithPriority(&c->prod_st, hipStreamNonBlocking, least);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_step, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_prod, hipEventDisableTiming);
+    if (e != hipSuccess) return hip_fail(e, "bsg_set_trajectory: stream / events");
+  }
+  // headers of no generation (0xFF..), counters zero; entries are written before use
+  const size_t head = 8 * (size_t)c->cfg.num_envs * (1 + bsg::TJ_P);
+  e = hipMemset(scratch, 0xFF, head);
+  if (e == hipSuccess) e = hipMemset(scratch, 0, 8 * (size_t)c->cfg.num_envs);
+  if (e == hipSuccess) e = hipDeviceSynchronize();
+  if (e != hipSuccess) return hip_fail(e, "bsg_set_trajectory: hipMemset");
+  c->traj = static_cast<double*>(scratch);
+  c->traj_sync = (flags & BSG_TRAJ_SYNC) != 0;
+  traj_new_gen(c);
+  c->steps_since_prod = kProdEvery;
+  return BSG_OK;
+}
+
+int32_t bsg_trajectory_info(const bsg_ctx* c, int64_t* out /* [4] */) {
+  if (!c || !out) return fail(BSG_E_INVALID_ARG, "bsg_trajectory_info: null argument");
+  out[0] = c->traj ? 1 : 0;
+  out[1] = c->prod_launches;
+  out[2] = (int64_t)c->traj_pub;
+  out[3] = (int64_t)c->traj_gen;
   return BSG_OK;
 }
 

@@ -61,6 +61,25 @@ __host__ __device__ constexpr size_t la_sc_offset(size_t E, size_t N) {
   return (2 * LA_F + LA_MC) * E * N + (8 + LA_WAIT_E) * E;
 }
 
+// Trajectory store (bsg_set_trajectory; MergeEnv with the lookahead, NEXT_STEP autoreset, a
+// TimeLimit of S <= TJ_SMAX steps).  A Merge intruder's whole episode is a function of (seed,
+// env, Philox episode counter) alone (merge_env.py:148-158, RESO OFF), so produce_kernel flies
+// future episodes ahead on a low-priority stream -- every post-step state of steps 1..S and
+// the intruder pairs' StateBased rows -- and the step kernel's lookahead waves copy the next
+// step's entry into the lookahead slot instead of running ten substeps on the launch's
+// critical path.  Layout, in doubles: [E] u64 copy counters (diagnostics), [E][TJ_P] u64
+// headers (tj_pack: generation | producer sequence | episode counter, written after the
+// episode's last entry), entries [TJ_P][S][TJ_F][EN] (the lookahead slot's LA_F fields and
+// the env's minimum separation over the intruder pairs at the ownship's index), then the
+// producers' memo [TJ_D + 1][LA_MC][EN].  Slot = episode counter % TJ_P.
+constexpr int TJ_P = 4;
+constexpr int TJ_F = LA_F + 1;
+constexpr int TJ_D = 3;            // a producer launch covers the episodes 1..TJ_D ahead
+constexpr int TJ_SMAX = 64;
+__host__ __device__ constexpr size_t tj_doubles(size_t E, size_t N, size_t S) {
+  return E + TJ_P * E + TJ_P * S * TJ_F * E * N + (TJ_D + 1) * LA_MC * E * N;
+}
+
 // Passed by value to every launch (kernarg segment).
 struct KParams {
   bsg_config cfg;
@@ -100,9 +119,21 @@ struct KParams {
   int spawn_k_ok;
   // the env module's constants (bsg_set_params, include/bsg.h BSG_MP_*; Merge)
   double kp[BSG_MERGE_NPARAMS];
+  // trajectory store (bsg_set_trajectory; tj_doubles): nullptr = off
+  double* traj;
+  uint64_t traj_pub;         // producer launches known complete when this launch was enqueued
+  uint32_t traj_gen;         // generation: headers of other generations are stale
+  int traj_S;                // steps per stored episode (the TimeLimit)
+  int prod_d0, prod_d1;      // produce_kernel: episodes ahead of the running one it covers
+  uint32_t prod_seq;         // produce_kernel: its sequence number (0: ordered on the stream)
+  int is_prod;               // produce_kernel: its waves run at the lowest priority
 };
 
 hipError_t launch_step(const KParams& p, hipStream_t stream);
+
+// produce_kernel (Merge translation unit): the episodes prod_d0..prod_d1 ahead of each env's
+// running one into the trajectory store, on `stream`
+hipError_t launch_produce(const KParams& p, hipStream_t stream);
 
 // Merge's creation-state constants (KParams::spawn_k) into out[0..7] (device; out[4] = 1.0
 // when valid; out[5..7] the creation altitude's atmosphere), one thread, on `stream` (bsg_kernels.hip, the Merge translation unit)

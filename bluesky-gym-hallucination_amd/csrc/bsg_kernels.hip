@@ -2454,7 +2454,8 @@ __device__ __forceinline__ void propagate(const KParams& p, int e, int j, size_t
         constexpr bool CR = decltype(cruise_tag)::value && LA_ROLE && KIND == BSG_ENV_MERGE && !WIND;
         int it = it0;
         for (; it < S; ++it) {
-          if (p.la) __builtin_amdgcn_s_setprio(3);
+          if (p.is_prod) __builtin_amdgcn_s_setprio(0);   // (produce_kernel: below the step's waves)
+          else if (p.la) __builtin_amdgcn_s_setprio(3);
           else if ((slot & 1) ? (it < sw) : (it >= sw)) __builtin_amdgcn_s_setprio(1);
           else __builtin_amdgcn_s_setprio(0);
           substep<WIND, KIND != BSG_ENV_MERGE, CR>(s, m, dt, rt, p.wind, it == 0 ? fh0 : trk_ok);
@@ -2593,6 +2594,36 @@ __device__ __forceinline__ void la_wait_for_main(const KParams& p, size_t EN, in
 }
 #endif
 
+// ---- trajectory store (bsg_internal.h tj_doubles; produce_kernel below) -----------------
+__device__ __forceinline__ uint64_t* tj_count(const KParams& p) {
+  return reinterpret_cast<uint64_t*>(p.traj);
+}
+__device__ __forceinline__ uint64_t* tj_hdr(const KParams& p) {
+  return reinterpret_cast<uint64_t*>(p.traj) + p.E;
+}
+// the entry of post-step index k (1..S) of the episode in `slot`: TJ_F fields x EN
+__device__ __forceinline__ double* tj_entry(const KParams& p, int slot, int k) {
+  const size_t EN = (size_t)p.E * p.N;
+  return p.traj + (size_t)p.E * (1 + TJ_P) + ((size_t)slot * p.traj_S + (size_t)(k - 1)) * TJ_F * EN;
+}
+__device__ __forceinline__ double* tj_memo(const KParams& p, int d) {
+  const size_t EN = (size_t)p.E * p.N;
+  return p.traj + (size_t)p.E * (1 + TJ_P) + (size_t)TJ_P * p.traj_S * TJ_F * EN +
+         (size_t)d * LA_MC * EN;
+}
+// header: generation (12 bits, 0xFFF = none: the scratch's 0xFF fill) | producer sequence
+// (20 bits; 0 = produced in the stream's own order) | Philox episode counter (32 bits)
+__device__ __forceinline__ uint64_t tj_pack(uint32_t gen, uint32_t seq, uint32_t counter) {
+  return ((uint64_t)(gen & 0xFFFu) << 52) | ((uint64_t)(seq & 0xFFFFFu) << 32) | (uint64_t)counter;
+}
+// an episode this launch may copy: this generation, this counter, and written by a producer
+// launch the host saw complete before enqueueing this one (or ordered before it on the stream)
+__device__ __forceinline__ bool tj_ready(const KParams& p, uint64_t h, uint32_t counter) {
+  const uint32_t seq = (uint32_t)(h >> 32) & 0xFFFFFu;
+  return (uint32_t)(h >> 52) == (p.traj_gen & 0xFFFu) && (uint32_t)h == counter &&
+         (seq == 0 || (uint64_t)seq <= p.traj_pub);
+}
+
 // One lookahead wave: the intruders of the same 64/GS envs as main workgroup
 // (blockIdx - la_grid0).  It reads only words no main wave of its launch writes: the
 // env-scalar snapshot (la_snap), the slot and tag row the main waves read too (slots are
@@ -2607,8 +2638,12 @@ __device__ __forceinline__ void la_wait_for_main(const KParams& p, size_t EN, in
 // next launch reads), so in a run the tags always match.
 template <int KIND, int GS, bool WIND, int CDW, class LT>
 __device__ __forceinline__ void lookahead_role(const KParams& p, LT& L, unsigned short* cd_lists) {
-  if (threadIdx.x >= 64) return;              // (la_cd: Vertical, one wave per workgroup)
-  const int lane = threadIdx.x;
+  // Waves 1.. of a CDW > 1 workgroup (Merge's C4 shards) take no aircraft; with la_cd they
+  // stay for the CD block's barriers (a wave that has left would not be waited for on every
+  // implementation), else they leave now
+  const bool hw = threadIdx.x >= 64;
+  if (hw && !(KIND == BSG_ENV_MERGE && p.la_cd)) return;
+  const int lane = threadIdx.x & 63;
   const int g = lane / GS, j = lane % GS;
   const int e = ((int)blockIdx.x - p.la_grid0) * (64 / GS) + g;
   const int N = p.N;
@@ -2624,7 +2659,7 @@ __device__ __forceinline__ void lookahead_role(const KParams& p, LT& L, unsigned
   la_wait_for_main(p, EN, e);
 #endif
   // this lane propagates intruder (e, j) (and, with la_cd, takes part in its env's pairs)
-  bool run = e < p.E && j > 0 && j < N;
+  bool run = !hw && e < p.E && j > 0 && j < N;
   AC s = {};
   if (run) {
     // every read of the common case is issued here, before any decision needs it, so the
@@ -2677,6 +2712,44 @@ __device__ __forceinline__ void lookahead_role(const KParams& p, LT& L, unsigned
         sct = sc_tags(p)[e];
       }
     }
+    // The trajectory store (a step launch, Merge): the state the next launch's main waves
+    // need is entry k of episode c -- a resetting env's first step (c = the counter this
+    // launch spawns with), else the step after this one -- when a producer has flown that
+    // episode (tj_ready).  Its copy replaces the ten substeps (and the intruder pairs' CD):
+    // the same function of the same counter, so the same bits (tests/test_gpu_trajectory.py).
+    if (p.traj && p.mode == MODE_STEP && known) {
+      const uint32_t c = rst ? episode : episode - 1u;
+      const int k = rst ? 1 : step + 2;
+      if (k <= p.traj_S) {
+        const uint64_t h = tj_hdr(p)[(size_t)e * TJ_P + c % TJ_P];
+        if (tj_ready(p, h, c)) {
+          const uint64_t* en = reinterpret_cast<const uint64_t*>(tj_entry(p, (int)(c % TJ_P), k));
+          uint64_t* sl = reinterpret_cast<uint64_t*>(p.la + (size_t)wslot * LA_F * EN);
+          const int nf = p.la_cd ? LA_F : LA_STATE;
+          uint64_t v[LA_F];
+#pragma unroll
+          for (int f = 0; f < LA_F; ++f) v[f] = f < nf ? en[(size_t)f * EN + a] : 0ull;
+          const uint64_t gm = (p.la_cd && j == 1) ? en[(size_t)LA_F * EN + (size_t)e * N] : 0ull;
+#pragma unroll
+          for (int f = 0; f < LA_F; ++f)
+            if (f < nf) sl[(size_t)f * EN + a] = v[f];
+          if (j == 1) {
+            if (p.la_cd)
+              reinterpret_cast<uint64_t*>(p.la + (2 * LA_F + MC_FIELDS) * EN)
+                  [2 * (size_t)p.E + (size_t)wslot * p.E + e] = gm;
+            tags[(size_t)wslot * p.E + e] = rst ? la_tag(episode + 1u, 0, p.la_gen)
+                                                : la_tag(episode, step + 1, p.la_gen);
+            tj_count(p)[e] += 1ull;
+          }
+          run = false;
+          known = false;                       // (nothing else below for this lane)
+        }
+      }
+    }
+    // NEXT_STEP: an env whose step now reaches the TimeLimit is reset by the next launch,
+    // which steps nothing of it -- its slot would never be read
+    const bool last = p.traj && p.mode == MODE_STEP && known && !rst &&
+                      p.cfg.max_episode_steps > 0 && step + 1 >= p.cfg.max_episode_steps;
     bool resetting;
     if (p.mode == MODE_RESET) resetting = p.env_mask ? (p.env_mask[e] != 0) : true;
     else if (p.mode == MODE_PRIME) resetting = false;
@@ -2685,10 +2758,10 @@ __device__ __forceinline__ void lookahead_role(const KParams& p, LT& L, unsigned
     // MODE_RESET: the masked envs; MODE_STEP: every env, from a spawn or a valid slot
     bool valid;
     if (p.mode == MODE_PRIME) valid = !rst;
-    else if (!known) valid = false;
+    else if (!known || last) valid = false;
     else if (resetting) valid = true;
     else valid = p.mode == MODE_STEP && tag_in == la_tag(episode, step, p.la_gen);
-    const bool touch = p.mode == MODE_STEP || (p.mode == MODE_RESET ? resetting : valid);
+    const bool touch = (p.mode == MODE_STEP && run) || (p.mode == MODE_RESET ? resetting : valid);
 #if defined(BSG_LA_LEGACY) && BSG_LA_LEGACY
     // round 3's priming: on a tag mismatch, this launch's step from the live state
     const bool legacy_prime = p.mode == MODE_STEP && known && !resetting && !valid;
@@ -2750,19 +2823,21 @@ __device__ __forceinline__ void lookahead_role(const KParams& p, LT& L, unsigned
     } else if (touch && j == 1) {
       tags[(size_t)wslot * p.E + e] = ~0ull;   // no generation produces this tag
     }
-    run = valid;
+    run = run && valid;
   }
-  if (KIND != BSG_ENV_VERTICAL_CR || !p.la_cd) return;
+  if ((KIND != BSG_ENV_VERTICAL_CR && KIND != BSG_ENV_MERGE) || !p.la_cd) return;
   // The intruder pairs' StateBased rows of the state just stored (the next launch's), for
   // the main waves that take this slot (cd_pairs CD_OWN adds the ownship's pairs)
   if (run) stage(L, lane, s);
-  if (j == 1) L.cdsel[g] = run ? CD_INTR : CD_NONE;     // every group has a lane j == 1
-  L.cm[lane] = 0ull;
-  L.lm[lane] = 0ull;
-  L.tmax[lane] = 0ull;                                   // bits of +0.0
-  if (j == 0) L.gmin[g] = bits(__builtin_inf());
+  if (!hw) {
+    if (j == 1) L.cdsel[g] = run ? CD_INTR : CD_NONE;   // every group has a lane j == 1
+    L.cm[lane] = 0ull;
+    L.lm[lane] = 0ull;
+    L.tmax[lane] = 0ull;                                 // bits of +0.0
+    if (j == 0) L.gmin[g] = bits(__builtin_inf());
+  }
   __syncthreads();
-  const bool cd_on = L.cdsel[g] == CD_INTR && j < N;
+  const bool cd_on = !hw && L.cdsel[g] == CD_INTR && j < N;
   constexpr int kList = 64 * (GS > 1 ? GS - 1 : 1);
   cd_pairs<GS, 1>(L, cd_lists, lane, 0, j, g * GS, N, cd_on, CD_INTR);
   if (run) {
@@ -2799,7 +2874,8 @@ __global__ __launch_bounds__(64 * CDW) BSG_WPE void step_kernel(KParams p) {
   constexpr bool kLA = (KIND == BSG_ENV_MERGE || KIND == BSG_ENV_VERTICAL_CR) && !WIND && LAK;
   // (la_cd is Vertical's only: compiled out of the other kinds, whose registers it would
   // otherwise hold across the substep loop)
-  constexpr bool kLaCd = KIND == BSG_ENV_VERTICAL_CR && !WIND && LAK;
+  // (Merge: with the trajectory store, whose entries carry the intruder pairs' rows)
+  constexpr bool kLaCd = (KIND == BSG_ENV_VERTICAL_CR || KIND == BSG_ENV_MERGE) && !WIND && LAK;
   __shared__ Lds<WIND> L;
   constexpr int kList = 64 * (GS > 1 ? GS - 1 : 1);
   __shared__ unsigned short cd_lists[CDW * kList];   // per-wave CD work lists (cd_pairs)
@@ -2811,6 +2887,11 @@ __global__ __launch_bounds__(64 * CDW) BSG_WPE void step_kernel(KParams p) {
 #endif
       return;                                  // the whole workgroup: no barrier below
     }
+  }
+  // with the trajectory store the producers' waves share SIMDs with these: the step's own
+  // waves issue first
+  if constexpr (kLA) {
+    if (p.traj) __builtin_amdgcn_s_setprio(2);
   }
   const int lane = threadIdx.x & 63;
   const int wv = CDW > 1 ? (int)(threadIdx.x >> 6) : 0;   // CD helper waves: wv > 0
@@ -3307,7 +3388,10 @@ static hipError_t launch_kind_w(const KParams& p0, hipStream_t st) {
   // Vertical: the lookahead waves also take the intruder pairs' CD (they end well before the
   // main waves there, whose phase 2 runs ~4 rounds of ~230 candidate pairs); Merge: not (its
   // lookahead waves are the critical path, profiles/r03/fastown/README.md)
-  p.la_cd = (KIND == BSG_ENV_VERTICAL_CR && p.la && p.cfg.compute_cd) ? 1 : 0;
+  // ... and Merge's, once the trajectory store feeds them (its entries carry the rows; the
+  // lookahead waves that still fly an episode compute them as Vertical's do)
+  p.la_cd = ((KIND == BSG_ENV_VERTICAL_CR || (KIND == BSG_ENV_MERGE && p.traj)) && p.la &&
+             p.cfg.compute_cd) ? 1 : 0;
   const int grid = (p.la && p.mode != MODE_PRIME) ? 2 * grid0 : grid0;
 #define BSG_CASE(G) \
   case G: hipLaunchKernelGGL((step_kernel<KIND, G, WIND>), dim3(grid), dim3(64), p.lds_pad, st, p); break;
@@ -3379,6 +3463,107 @@ static hipError_t launch_kind(const KParams& p, hipStream_t st) {
 }
 
 #if !defined(BSG_KIND_TU) || BSG_KIND_TU == 0
+// ---- produce_kernel: future episodes' intruders into the trajectory store -----------------
+// One wave per (group of 64/GS envs, episode ahead d).  For each env the Philox counter of the
+// episode d ahead of its running one (episode - 1 + d; the episode word is read once, racing
+// the step launches on the other stream: any value it reads is a counter the env has reached
+// or will reach, bsg_internal.h tj_doubles): unless this generation already holds it, the
+// wave creates its intruders (spawn_merge, memo_spawned) and flies the whole episode --
+// propagate<..., LA_ROLE> step after step with the memo fetched between steps, exactly the
+// lookahead wave's sequence over the launches of that episode -- storing every post-step
+// state and, with CD on, the intruder pairs' StateBased rows of it (the lookahead's la_cd
+// block), then the header.  Entries of a slot are only ever overwritten for a counter >= 4
+// ahead, which no env still runs.  d = 0 (bsg_reset with device spawns, on the stream, the
+// envs env_mask selects): the episode just created.  The waves run at priority 0 (is_prod).
+template <int GS>
+__global__ __launch_bounds__(64) void produce_kernel(KParams p) {
+  __shared__ Lds<false> L;
+  __shared__ unsigned short cd_lists[64 * (GS > 1 ? GS - 1 : 1)];
+  __builtin_amdgcn_s_setprio(0);
+  const int lane = threadIdx.x;
+  const int g = lane / GS, j = lane % GS;
+  const int nd = p.prod_d1 - p.prod_d0 + 1;
+  const int grp = (int)blockIdx.x / nd;
+  const int d = p.prod_d0 + (int)blockIdx.x % nd;
+  const int e = grp * (64 / GS) + g;
+  const int N = p.N;
+  const size_t EN = (size_t)p.E * N;
+  const size_t a = (size_t)e * N + j;
+  uint32_t c = 0;
+  bool need = false;
+  if (e < p.E && !(d == 0 && p.env_mask && p.env_mask[e] == 0)) {
+    const uint32_t X = *(volatile const uint32_t*)&p.b.episode[e];
+    c = X - 1u + (uint32_t)d;
+    const uint64_t h = tj_hdr(p)[(size_t)e * TJ_P + c % TJ_P];
+    need = !((uint32_t)(h >> 52) == (p.traj_gen & 0xFFFu) && (uint32_t)h == c);
+  }
+  if (__ballot(need) == 0) return;                 // (wave-uniform: one wave per workgroup)
+  const bool run = need && j > 0 && j < N;
+  double* memo = tj_memo(p, d);
+  const int slot = (int)(c % TJ_P);
+  AC s = {};
+  double mc[MC_FIELDS];
+  if (run) {
+    double aux[4] = {0.0, 0.0, 0.0, 0.0};
+    spawn<BSG_ENV_MERGE>(p, e, j, c, s, aux, false);
+    memo_spawned<BSG_ENV_MERGE>(p, memo, a, EN, mc);
+  }
+  const double act[2] = {0.0, 0.0};
+  const double oat[4] = {0.0, 0.0, 0.0, 0.0};
+  for (int k = 1; k <= p.traj_S; ++k) {
+    double* en = tj_entry(p, slot, k);
+    if (run) {
+      if (k > 1) memo_fetch(mc, memo, a, EN);
+      double sub_reward = 0.0;
+      bool sub_done = false;
+      EnvScalars ev = {};
+      propagate<BSG_ENV_MERGE, false, true>(p, e, j, a, s, ev, sub_reward, sub_done, act, mc, oat,
+                                            memo, k == 1);
+      la_store(en, a, EN, s);
+    }
+    if (p.cfg.compute_cd) {
+      if (run) stage(L, lane, s);
+      if (j == 1) L.cdsel[g] = need ? CD_INTR : CD_NONE;
+      L.cm[lane] = 0ull;
+      L.lm[lane] = 0ull;
+      L.tmax[lane] = 0ull;
+      if (j == 0) L.gmin[g] = bits(__builtin_inf());
+      __syncthreads();
+      const bool cd_on = L.cdsel[g] == CD_INTR && j < N;
+      cd_pairs<GS, 1>(L, cd_lists, lane, 0, j, g * GS, N, cd_on, CD_INTR);
+      if (run) {
+        en[(size_t)LA_STATE * EN + a] = __longlong_as_double((long long)L.cm[lane]);
+        en[(size_t)(LA_STATE + 1) * EN + a] = __longlong_as_double((long long)L.lm[lane]);
+        en[(size_t)(LA_STATE + 2) * EN + a] = __longlong_as_double((long long)L.tmax[lane]);
+      }
+      if (need && j == 0)
+        en[(size_t)LA_F * EN + (size_t)e * N] = __longlong_as_double((long long)L.gmin[g]);
+    }
+  }
+  if (need && j == 1) tj_hdr(p)[(size_t)e * TJ_P + slot] = tj_pack(p.traj_gen, p.prod_seq, c);
+}
+
+hipError_t launch_produce(const KParams& p0, hipStream_t st) {
+  if (p0.cfg.env_kind != BSG_ENV_MERGE || !p0.traj || p0.prod_d1 < p0.prod_d0) return hipErrorInvalidValue;
+  int gs = 1;
+  while (gs < p0.N) gs <<= 1;
+  const int groups = (p0.E + 64 / gs - 1) / (64 / gs);
+  const int grid = groups * (p0.prod_d1 - p0.prod_d0 + 1);
+  KParams p = p0;
+  p.is_prod = 1;
+  p.la = nullptr;
+  p.spawn = nullptr;
+  p.wind.np = 0;
+#define BSG_CASE_P(G) \
+  case G: hipLaunchKernelGGL((produce_kernel<G>), dim3(grid), dim3(64), 0, st, p); break;
+  switch (gs) {
+    BSG_CASE_P(2) BSG_CASE_P(4) BSG_CASE_P(8) BSG_CASE_P(16) BSG_CASE_P(32) BSG_CASE_P(64)
+    default: return hipErrorInvalidValue;
+  }
+#undef BSG_CASE_P
+  return hipGetLastError();
+}
+
 // KParams::spawn_k for Merge: Traffic.cre's tas / cas at the creation speed and altitude, and
 // the speed memo the first substep of such an aircraft leaves (substep's spd_miss path and
 // general limits at vatmos(alt)); the 'level' form when the stored cas is the one

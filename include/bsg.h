@@ -241,6 +241,25 @@ int32_t bsg_set_learner(bsg_ctx* ctx, float* learner_rows);
 int64_t bsg_lookahead_bytes(const bsg_ctx* ctx);
 int32_t bsg_set_lookahead(bsg_ctx* ctx, void* scratch, int64_t bytes);
 
+/* Trajectory store (MergeEnv-v0 with the lookahead bound, NEXT_STEP autoreset, a TimeLimit of
+ * 1..64 steps; device spawns).  A Merge intruder's whole episode depends only on (seed, env,
+ * Philox episode counter) -- it spawns at merge_env.py:148-158 and flies LNAV with RESO OFF --
+ * so the library flies future episodes ahead, every post-step state of every step and the
+ * intruder pairs' conflict rows, on a stream of its own at the least priority, and the step
+ * launch's lookahead copies the next step's entry instead of propagating ten substeps on its
+ * critical path.  Same function of the same inputs: every output is bit-identical to the
+ * inline path.  A reset with device spawns flies the new episodes on the caller's stream; a
+ * launch with host spawn rows, a re-bind or a re-armed lookahead retires the stored episodes.
+ * The caller owns the scratch (bsg_trajectory_bytes; 0 = unsupported configuration) and
+ * keeps it until bsg_set_trajectory(ctx, NULL, 0, 0) or bsg_destroy, which wait for the
+ * producer.  flags: BSG_TRAJ_SYNC (tests) runs the producers on the caller's stream. */
+#define BSG_TRAJ_SYNC 1
+int64_t bsg_trajectory_bytes(const bsg_ctx* ctx);
+int32_t bsg_set_trajectory(bsg_ctx* ctx, void* scratch, int64_t bytes, int32_t flags);
+/* out[0] store bound, out[1] producer launches issued, out[2] last sequence published,
+ * out[3] generation */
+int32_t bsg_trajectory_info(const bsg_ctx* ctx, int64_t* out);
+
 /* Replaces: Env.reset() (merge_env.py:103-130 + _gen_aircraft :148-158;
  * vertical_cr_env.py:258-281 + _generate_conflicts :183-200; descent_env.py:162-182).
  * env_mask: device u8 [E] (NULL = all envs).  spawn: device f64 [E, spawn_width]
