@@ -64,6 +64,7 @@ struct bsg_ctx {
   // event, and every later step launch is ordered after that event on its stream
   double* traj = nullptr;
   bool traj_sync = false;           // test hook: producers on the caller's stream, in order
+  bool traj_noasync = false;        // BSG_TRAJ_NOASYNC=1 (A/B runs): reset-time production only
   uint32_t traj_gen = 1;            // 1..0xFFE; bumped when the stored episodes may be stale
   uint32_t prod_seq = 0;            // last producer sequence number issued (1..0xFFFFE)
   uint64_t traj_pub = 0;
@@ -326,7 +327,9 @@ int traj_after(bsg_ctx* c, const bsg::KParams& p0, hipStream_t st, int mode, con
     c->steps_since_prod = kProdEvery;
     return BSG_OK;
   }
-  if (mode != bsg::MODE_STEP || c->prod_inflight || ++c->steps_since_prod < kProdEvery) return BSG_OK;
+  if (mode != bsg::MODE_STEP || c->prod_inflight || c->traj_noasync ||
+      ++c->steps_since_prod < kProdEvery)
+    return BSG_OK;
   c->steps_since_prod = 0;
   q.env_mask = nullptr;
   q.prod_d0 = 1;
@@ -691,6 +694,7 @@ int32_t bsg_set_trajectory(bsg_ctx* c, void* scratch, int64_t bytes, int32_t fla
   if (e != hipSuccess) return hip_fail(e, "bsg_set_trajectory: hipMemset");
   c->traj = static_cast<double*>(scratch);
   c->traj_sync = (flags & BSG_TRAJ_SYNC) != 0;
+  if (const char* na = std::getenv("BSG_TRAJ_NOASYNC")) c->traj_noasync = std::atoi(na) != 0;
   traj_new_gen(c);
   c->steps_since_prod = kProdEvery;
   return BSG_OK;

@@ -3551,6 +3551,7 @@ hipError_t launch_produce(const KParams& p0, hipStream_t st) {
   const int grid = groups * (p0.prod_d1 - p0.prod_d0 + 1);
   KParams p = p0;
   p.is_prod = 1;
+  p.stamps = nullptr;        // (diagnostic builds: the stamp rows are the step grid's, not ours)
   p.la = nullptr;
   p.spawn = nullptr;
   p.wind.np = 0;
