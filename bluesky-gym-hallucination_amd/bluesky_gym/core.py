@@ -101,7 +101,7 @@ class DeviceBatch:
             self.trajectory = True
         elif trajectory:
             raise nat.BsgError("trajectory: MergeEnv with the lookahead, NEXT_STEP autoreset and a "
-                               "TimeLimit of 1..64 steps only")
+                               "TimeLimit of 1..63 steps only")
 
     # ------------------------------------------------------------------ buffers
     def _alloc(self):

@@ -277,7 +277,7 @@ int trim_pending(bsg_ctx* c) {
 }
 
 // ---- trajectory store scheduling ------------------------------------------------------
-constexpr int kProdEvery = 4;       // step launches between producer launches (at least)
+constexpr int kProdEvery = 1;       // step launches between producer launches (at least)
 
 // wait for an in-flight producer (its buffers are about to change or go away) and fold it in
 int traj_quiesce(bsg_ctx* c) {
@@ -321,6 +321,7 @@ int traj_after(bsg_ctx* c, const bsg::KParams& p0, hipStream_t st, int mode, con
     if (int r = traj_quiesce(c)) return r;
     q.prod_d0 = 0;
     q.prod_d1 = 2;
+    q.prod_q = bsg::TJ_SMAX;          // whole episodes
     q.prod_seq = 0;
     if ((e = bsg::launch_produce(q, st)) != hipSuccess) return hip_fail(e, "produce launch (reset)");
     ++c->prod_launches;
@@ -334,13 +335,14 @@ int traj_after(bsg_ctx* c, const bsg::KParams& p0, hipStream_t st, int mode, con
   q.env_mask = nullptr;
   q.prod_d0 = 1;
   q.prod_d1 = bsg::TJ_D;
+  q.prod_q = bsg::TJ_Q;
   if (c->traj_sync) {
     q.prod_seq = 0;
     if ((e = bsg::launch_produce(q, st)) != hipSuccess) return hip_fail(e, "produce launch");
     ++c->prod_launches;
     return BSG_OK;
   }
-  if (c->prod_seq >= 0xFFFFEu) {            // the header's 20-bit sequence wraps: new generation
+  if (c->prod_seq >= 0x3FFEu) {             // the header's 14-bit sequence wraps: new generation
     if (int r = traj_quiesce(c)) return r;
     c->prod_seq = 0;
     c->traj_pub = 0;
@@ -687,7 +689,7 @@ int32_t bsg_set_trajectory(bsg_ctx* c, void* scratch, int64_t bytes, int32_t fla
     if (e != hipSuccess) return hip_fail(e, "bsg_set_trajectory: stream / events");
   }
   // headers of no generation (0xFF..), counters zero; entries are written before use
-  const size_t head = 8 * (size_t)c->cfg.num_envs * (1 + bsg::TJ_P);
+  const size_t head = 8 * (size_t)c->cfg.num_envs * (1 + 2 * bsg::TJ_P);
   e = hipMemset(scratch, 0xFF, head);
   if (e == hipSuccess) e = hipMemset(scratch, 0, 8 * (size_t)c->cfg.num_envs);
   if (e == hipSuccess) e = hipDeviceSynchronize();

@@ -2604,24 +2604,29 @@ __device__ __forceinline__ uint64_t* tj_hdr(const KParams& p) {
 // the entry of post-step index k (1..S) of the episode in `slot`: TJ_F fields x EN
 __device__ __forceinline__ double* tj_entry(const KParams& p, int slot, int k) {
   const size_t EN = (size_t)p.E * p.N;
-  return p.traj + (size_t)p.E * (1 + TJ_P) + ((size_t)slot * p.traj_S + (size_t)(k - 1)) * TJ_F * EN;
+  return p.traj + (size_t)p.E * (1 + 2 * TJ_P) + ((size_t)slot * p.traj_S + (size_t)(k - 1)) * TJ_F * EN;
 }
 __device__ __forceinline__ double* tj_memo(const KParams& p, int d) {
   const size_t EN = (size_t)p.E * p.N;
-  return p.traj + (size_t)p.E * (1 + TJ_P) + (size_t)TJ_P * p.traj_S * TJ_F * EN +
+  return p.traj + (size_t)p.E * (1 + 2 * TJ_P) + (size_t)TJ_P * p.traj_S * TJ_F * EN +
          (size_t)d * LA_MC * EN;
 }
 // header: generation (12 bits, 0xFFF = none: the scratch's 0xFF fill) | producer sequence
-// (20 bits; 0 = produced in the stream's own order) | Philox episode counter (32 bits)
-__device__ __forceinline__ uint64_t tj_pack(uint32_t gen, uint32_t seq, uint32_t counter) {
-  return ((uint64_t)(gen & 0xFFFu) << 52) | ((uint64_t)(seq & 0xFFFFFu) << 32) | (uint64_t)counter;
+// (14 bits; 0 = produced in the stream's own order) | steps stored (6 bits) | Philox episode
+// counter (32 bits)
+__device__ __forceinline__ uint64_t tj_pack(uint32_t gen, uint32_t seq, int prog, uint32_t counter) {
+  return ((uint64_t)(gen & 0xFFFu) << 52) | ((uint64_t)(seq & 0x3FFFu) << 38) |
+         ((uint64_t)(prog & 63) << 32) | (uint64_t)counter;
 }
-// an episode this launch may copy: this generation, this counter, and written by a producer
-// launch the host saw complete before enqueueing this one (or ordered before it on the stream)
-__device__ __forceinline__ bool tj_ready(const KParams& p, uint64_t h, uint32_t counter) {
-  const uint32_t seq = (uint32_t)(h >> 32) & 0xFFFFFu;
-  return (uint32_t)(h >> 52) == (p.traj_gen & 0xFFFu) && (uint32_t)h == counter &&
-         (seq == 0 || (uint64_t)seq <= p.traj_pub);
+__device__ __forceinline__ int tj_prog(uint64_t h) { return (int)((h >> 32) & 63u); }
+// steps of episode `counter` this launch may copy from one header version: this generation and
+// counter, written by a producer launch the host saw complete before enqueueing this one (or
+// ordered before it on the stream); 0 = none
+__device__ __forceinline__ int tj_ready(const KParams& p, uint64_t h, uint32_t counter) {
+  const uint32_t seq = (uint32_t)(h >> 38) & 0x3FFFu;
+  const bool ok = (uint32_t)(h >> 52) == (p.traj_gen & 0xFFFu) && (uint32_t)h == counter &&
+                  (seq == 0 || (uint64_t)seq <= p.traj_pub);
+  return ok ? tj_prog(h) : 0;
 }
 
 // One lookahead wave: the intruders of the same 64/GS envs as main workgroup
@@ -2721,8 +2726,9 @@ __device__ __forceinline__ void lookahead_role(const KParams& p, LT& L, unsigned
       const uint32_t c = rst ? episode : episode - 1u;
       const int k = rst ? 1 : step + 2;
       if (k <= p.traj_S) {
-        const uint64_t h = tj_hdr(p)[(size_t)e * TJ_P + c % TJ_P];
-        if (tj_ready(p, h, c)) {
+        const uint64_t* hv = tj_hdr(p) + ((size_t)e * TJ_P + c % TJ_P) * 2;
+        const uint64_t h0 = hv[0], h1 = hv[1];
+        if (k <= max(tj_ready(p, h0, c), tj_ready(p, h1, c))) {
           const uint64_t* en = reinterpret_cast<const uint64_t*>(tj_entry(p, (int)(c % TJ_P), k));
           uint64_t* sl = reinterpret_cast<uint64_t*>(p.la + (size_t)wslot * LA_F * EN);
           const int nf = p.la_cd ? LA_F : LA_STATE;
@@ -3491,11 +3497,20 @@ __global__ __launch_bounds__(64) void produce_kernel(KParams p) {
   const size_t a = (size_t)e * N + j;
   uint32_t c = 0;
   bool need = false;
+  int k0 = 1, k1 = 0, wv = 0;                     // steps k0..k1 into header version wv
   if (e < p.E && !(d == 0 && p.env_mask && p.env_mask[e] == 0)) {
     const uint32_t X = *(volatile const uint32_t*)&p.b.episode[e];
     c = X - 1u + (uint32_t)d;
-    const uint64_t h = tj_hdr(p)[(size_t)e * TJ_P + c % TJ_P];
-    need = !((uint32_t)(h >> 52) == (p.traj_gen & 0xFFFu) && (uint32_t)h == c);
+    // (producer launches run one at a time: both versions are final here)
+    const uint64_t* hv = tj_hdr(p) + ((size_t)e * TJ_P + c % TJ_P) * 2;
+    const bool m0 = (uint32_t)(hv[0] >> 52) == (p.traj_gen & 0xFFFu) && (uint32_t)hv[0] == c;
+    const bool m1 = (uint32_t)(hv[1] >> 52) == (p.traj_gen & 0xFFFu) && (uint32_t)hv[1] == c;
+    const int g0 = m0 ? tj_prog(hv[0]) : 0, g1 = m1 ? tj_prog(hv[1]) : 0;
+    const int have = g0 > g1 ? g0 : g1;
+    wv = g0 > g1 ? 1 : 0;                          // rewrite the version that is not the best
+    k0 = have + 1;
+    k1 = min(p.traj_S, have + p.prod_q);
+    need = k0 <= k1;
   }
   if (__ballot(need) == 0) return;                 // (wave-uniform: one wave per workgroup)
   const bool run = need && j > 0 && j < N;
@@ -3506,14 +3521,33 @@ __global__ __launch_bounds__(64) void produce_kernel(KParams p) {
   if (run) {
     double aux[4] = {0.0, 0.0, 0.0, 0.0};
     spawn<BSG_ENV_MERGE>(p, e, j, c, s, aux, false);
-    memo_spawned<BSG_ENV_MERGE>(p, memo, a, EN, mc);
+    if (k0 == 1) {
+      memo_spawned<BSG_ENV_MERGE>(p, memo, a, EN, mc);
+    } else {
+      // resume from the last stored step: its state over the creation's (selspd / selalt /
+      // selvs never change for an intruder), the memo emptied (a cache: the same bits)
+      la_load(tj_entry(p, slot, k0 - 1), a, EN, s);
+      memo_invalidate(memo, a, EN);
+#pragma unroll
+      for (int f = 0; f < MC_FIELDS; ++f) mc[f] = key_as_double(kNoKey);
+    }
   }
   const double act[2] = {0.0, 0.0};
   const double oat[4] = {0.0, 0.0, 0.0, 0.0};
-  for (int k = 1; k <= p.traj_S; ++k) {
+  // (the loop bound is wave-uniform: the CD block's barriers; lanes outside [k0, k1] idle)
+  int klo = k0, khi = k1;
+  if (!need) { klo = 1 << 20; khi = -1; }
+  int wlo = klo, whi = khi;
+#pragma unroll 1
+  for (int off = 32; off > 0; off >>= 1) {
+    wlo = min(wlo, __shfl_xor(wlo, off, 64));
+    whi = max(whi, __shfl_xor(whi, off, 64));
+  }
+  for (int k = wlo; k <= whi; ++k) {
+    const bool in = need && k >= k0 && k <= k1;
     double* en = tj_entry(p, slot, k);
-    if (run) {
-      if (k > 1) memo_fetch(mc, memo, a, EN);
+    if (run && in) {
+      if (k > k0) memo_fetch(mc, memo, a, EN);
       double sub_reward = 0.0;
       bool sub_done = false;
       EnvScalars ev = {};
@@ -3522,8 +3556,8 @@ __global__ __launch_bounds__(64) void produce_kernel(KParams p) {
       la_store(en, a, EN, s);
     }
     if (p.cfg.compute_cd) {
-      if (run) stage(L, lane, s);
-      if (j == 1) L.cdsel[g] = need ? CD_INTR : CD_NONE;
+      if (run && in) stage(L, lane, s);
+      if (j == 1) L.cdsel[g] = in ? CD_INTR : CD_NONE;
       L.cm[lane] = 0ull;
       L.lm[lane] = 0ull;
       L.tmax[lane] = 0ull;
@@ -3531,16 +3565,17 @@ __global__ __launch_bounds__(64) void produce_kernel(KParams p) {
       __syncthreads();
       const bool cd_on = L.cdsel[g] == CD_INTR && j < N;
       cd_pairs<GS, 1>(L, cd_lists, lane, 0, j, g * GS, N, cd_on, CD_INTR);
-      if (run) {
+      if (run && in) {
         en[(size_t)LA_STATE * EN + a] = __longlong_as_double((long long)L.cm[lane]);
         en[(size_t)(LA_STATE + 1) * EN + a] = __longlong_as_double((long long)L.lm[lane]);
         en[(size_t)(LA_STATE + 2) * EN + a] = __longlong_as_double((long long)L.tmax[lane]);
       }
-      if (need && j == 0)
+      if (in && j == 0)
         en[(size_t)LA_F * EN + (size_t)e * N] = __longlong_as_double((long long)L.gmin[g]);
     }
   }
-  if (need && j == 1) tj_hdr(p)[(size_t)e * TJ_P + slot] = tj_pack(p.traj_gen, p.prod_seq, c);
+  if (need && j == 1)
+    tj_hdr(p)[((size_t)e * TJ_P + slot) * 2 + wv] = tj_pack(p.traj_gen, p.prod_seq, k1, c);
 }
 
 hipError_t launch_produce(const KParams& p0, hipStream_t st) {

@@ -242,10 +242,11 @@ int64_t bsg_lookahead_bytes(const bsg_ctx* ctx);
 int32_t bsg_set_lookahead(bsg_ctx* ctx, void* scratch, int64_t bytes);
 
 /* Trajectory store (MergeEnv-v0 with the lookahead bound, NEXT_STEP autoreset, a TimeLimit of
- * 1..64 steps; device spawns).  A Merge intruder's whole episode depends only on (seed, env,
+ * 1..63 steps; device spawns).  A Merge intruder's whole episode depends only on (seed, env,
  * Philox episode counter) -- it spawns at merge_env.py:148-158 and flies LNAV with RESO OFF --
  * so the library flies future episodes ahead, every post-step state of every step and the
- * intruder pairs' conflict rows, on a stream of its own at the least priority, and the step
+ * intruder pairs' conflict rows, on a stream of its own at the least priority (a few steps of
+ * each episode per producer launch, one launch after the other), and the step
  * launch's lookahead copies the next step's entry instead of propagating ten substeps on its
  * critical path.  Same function of the same inputs: every output is bit-identical to the
  * inline path.  A reset with device spawns flies the new episodes on the caller's stream; a
