@@ -376,10 +376,10 @@ int launch(bsg_ctx* c, int mode, const double* actions, const double* spawn,
   if (int r = spawn_k_prepare(c, st)) return r;
   // trajectory store: active with the lookahead itself (no wind, no graph capture)
   const bool tj = c->traj && la_active(c);
+  // (an in-flight producer writes only the store; a launch without it leaves it running --
+  // synchronising here would be illegal inside a stream capture)
   if (tj) {
     if (int r = traj_before(c, st, spawn)) return r;
-  } else if (c->traj) {
-    if (int r = traj_quiesce(c)) return r;
   }
   bsg::KParams p = make_params(c, mode);
   p.actions = actions;
