@@ -65,6 +65,7 @@ struct bsg_ctx {
   double* traj = nullptr;
   bool traj_sync = false;           // test hook: producers on the caller's stream, in order
   bool traj_noasync = false;        // BSG_TRAJ_NOASYNC=1 (A/B runs): reset-time production only
+  int traj_wprio = 1;               // BSG_TRAJ_WPRIO=1: producer waves at s_setprio 1 (else 0)
   uint32_t traj_gen = 1;            // 1..0xFFE; bumped when the stored episodes may be stale
   uint32_t prod_seq = 0;            // last producer sequence number issued (1..0xFFFFE)
   uint64_t traj_pub = 0;
@@ -336,6 +337,7 @@ int traj_after(bsg_ctx* c, const bsg::KParams& p0, hipStream_t st, int mode, con
   q.prod_d0 = 1;
   q.prod_d1 = bsg::TJ_D;
   q.prod_q = bsg::TJ_Q;
+  q.is_prod = c->traj_wprio == 1 ? 2 : 1;
   if (c->traj_sync) {
     q.prod_seq = 0;
     if ((e = bsg::launch_produce(q, st)) != hipSuccess) return hip_fail(e, "produce launch");
@@ -683,7 +685,10 @@ int32_t bsg_set_trajectory(bsg_ctx* c, void* scratch, int64_t bytes, int32_t fla
   if (!c->prod_st) {
     int least = 0, greatest = 0;
     e = hipDeviceGetStreamPriorityRange(&least, &greatest);
-    if (e == hipSuccess) e = hipStreamCreateWithPriority(&c->prod_st, hipStreamNonBlocking, least);
+    // BSG_TRAJ_QPRIO=normal (A/B runs): the producer stream at the default priority
+    const char* qp = std::getenv("BSG_TRAJ_QPRIO");
+    const int prio = (qp && std::strcmp(qp, "normal") == 0) ? 0 : least;
+    if (e == hipSuccess) e = hipStreamCreateWithPriority(&c->prod_st, hipStreamNonBlocking, prio);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_step, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_prod, hipEventDisableTiming);
     if (e != hipSuccess) return hip_fail(e, "bsg_set_trajectory: stream / events");
@@ -697,6 +702,7 @@ int32_t bsg_set_trajectory(bsg_ctx* c, void* scratch, int64_t bytes, int32_t fla
   c->traj = static_cast<double*>(scratch);
   c->traj_sync = (flags & BSG_TRAJ_SYNC) != 0;
   if (const char* na = std::getenv("BSG_TRAJ_NOASYNC")) c->traj_noasync = std::atoi(na) != 0;
+  if (const char* wp = std::getenv("BSG_TRAJ_WPRIO")) c->traj_wprio = std::atoi(wp);
   traj_new_gen(c);
   c->steps_since_prod = kProdEvery;
   return BSG_OK;

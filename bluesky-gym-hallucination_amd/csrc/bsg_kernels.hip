@@ -2454,7 +2454,8 @@ __device__ __forceinline__ void propagate(const KParams& p, int e, int j, size_t
         constexpr bool CR = decltype(cruise_tag)::value && LA_ROLE && KIND == BSG_ENV_MERGE && !WIND;
         int it = it0;
         for (; it < S; ++it) {
-          if (p.is_prod) __builtin_amdgcn_s_setprio(0);   // (produce_kernel: below the step's waves)
+          if (p.is_prod == 2) __builtin_amdgcn_s_setprio(1);   // (produce_kernel: below the
+          else if (p.is_prod) __builtin_amdgcn_s_setprio(0);   //  step's own waves)
           else if (p.la) __builtin_amdgcn_s_setprio(3);
           else if ((slot & 1) ? (it < sw) : (it >= sw)) __builtin_amdgcn_s_setprio(1);
           else __builtin_amdgcn_s_setprio(0);
@@ -3485,7 +3486,8 @@ template <int GS>
 __global__ __launch_bounds__(64) void produce_kernel(KParams p) {
   __shared__ Lds<false> L;
   __shared__ unsigned short cd_lists[64 * (GS > 1 ? GS - 1 : 1)];
-  __builtin_amdgcn_s_setprio(0);
+  if (p.is_prod == 2) __builtin_amdgcn_s_setprio(1);
+  else __builtin_amdgcn_s_setprio(0);
   const int lane = threadIdx.x;
   const int g = lane / GS, j = lane % GS;
   const int nd = p.prod_d1 - p.prod_d0 + 1;
@@ -3585,7 +3587,7 @@ hipError_t launch_produce(const KParams& p0, hipStream_t st) {
   const int groups = (p0.E + 64 / gs - 1) / (64 / gs);
   const int grid = groups * (p0.prod_d1 - p0.prod_d0 + 1);
   KParams p = p0;
-  p.is_prod = 1;
+  p.is_prod = p0.is_prod > 0 ? p0.is_prod : 1;
   p.stamps = nullptr;        // (diagnostic builds: the stamp rows are the step grid's, not ours)
   p.la = nullptr;
   p.spawn = nullptr;
