@@ -59,22 +59,22 @@ struct bsg_ctx {
   double kp[BSG_MERGE_NPARAMS] = {15.0, 20.0, 4.0, 10.0, 1.0, -0.1, -1.0, 50.0, 200.0, 20.0, 500.0};
   bool launched = false;            // a reset / step has been enqueued
   // trajectory store (bsg_set_trajectory; bsg_internal.h tj_doubles): the producers run on
-  // their own stream of the least priority, one launch in flight at a time; a producer launch
-  // is "published" (traj_pub = its sequence number) once the host has seen its completion
-  // event, and every later step launch is ordered after that event on its stream
+  // their own stream of the least priority, at most kProdMax launches enqueued (they run one
+  // after the other); each publishes itself on the device when its last wave ends
+  // (produce_kernel), so the step launches enqueued ahead of it see it as soon as it is done
   double* traj = nullptr;
   bool traj_sync = false;           // test hook: producers on the caller's stream, in order
   bool traj_noasync = false;        // BSG_TRAJ_NOASYNC=1 (A/B runs): reset-time production only
   int traj_wprio = 1;               // BSG_TRAJ_WPRIO=1: producer waves at s_setprio 1 (else 0)
   uint32_t traj_gen = 1;            // 1..0xFFE; bumped when the stored episodes may be stale
-  uint32_t prod_seq = 0;            // last producer sequence number issued (1..0xFFFFE)
-  uint64_t traj_pub = 0;
-  bool prod_inflight = false;
-  uint32_t prod_inflight_seq = 0;
+  uint32_t prod_seq = 0;            // last producer sequence number issued (1..0x3FFE)
+  int prod_out = 0;                 // producer launches enqueued and not seen complete
+  int prod_head = 0;                // oldest of them in ev_prod[] (a ring)
   int steps_since_prod = 0;
   int64_t prod_launches = 0;
   hipStream_t prod_st = nullptr;
-  hipEvent_t ev_step = nullptr, ev_prod = nullptr;
+  hipEvent_t ev_step = nullptr;
+  hipEvent_t ev_prod[4] = {};
 };
 
 namespace {
@@ -152,7 +152,6 @@ bsg::KParams make_params(const bsg_ctx* c, int mode) {
   for (int k = 0; k < 8; ++k) p.spawn_k[k] = c->spawn_k[k];
   for (int k = 0; k < BSG_MERGE_NPARAMS; ++k) p.kp[k] = c->kp[k];
   p.traj_gen = c->traj_gen;
-  p.traj_pub = c->traj_pub;
   p.traj_S = c->cfg.max_episode_steps;
   return p;
 }
@@ -279,31 +278,35 @@ int trim_pending(bsg_ctx* c) {
 
 // ---- trajectory store scheduling ------------------------------------------------------
 constexpr int kProdEvery = 1;       // step launches between producer launches (at least)
+constexpr int kProdMax = 2;         // producer launches enqueued at once (<= 4)
 
-// wait for an in-flight producer (its buffers are about to change or go away) and fold it in
+// wait for the enqueued producers (their buffers are about to change or go away)
 int traj_quiesce(bsg_ctx* c) {
-  if (!c->prod_inflight) return BSG_OK;
-  hipError_t e = hipEventSynchronize(c->ev_prod);
-  if (e != hipSuccess) return hip_fail(e, "hipEventSynchronize(producer)");
-  c->prod_inflight = false;
-  c->traj_pub = c->prod_inflight_seq;
+  if (!c->prod_out) return BSG_OK;
+  hipError_t e = hipStreamSynchronize(c->prod_st);
+  if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize(producer)");
+  c->prod_out = 0;
   return BSG_OK;
+}
+
+// retire the producer launches that have completed (flow control only: publication is the
+// producers' own, on the device)
+void traj_poll(bsg_ctx* c) {
+  while (c->prod_out > 0 && hipEventQuery(c->ev_prod[c->prod_head]) == hipSuccess) {
+    c->prod_head = (c->prod_head + 1) % 4;
+    --c->prod_out;
+  }
 }
 
 void traj_new_gen(bsg_ctx* c) {
   c->traj_gen = (c->traj_gen % 0xFFEu) + 1u;
 }
 
-// Before a launch: publish a producer launch that has completed (and order this stream after
-// it), and retire the stored episodes when this launch spawns from host rows (the store holds
-// Philox episodes: a host-row episode under the same counter is another episode)
+// Before a launch: retire the stored episodes when this launch spawns from host rows (the
+// store holds Philox episodes: a host-row episode under the same counter is another one)
 int traj_before(bsg_ctx* c, hipStream_t st, const double* spawn) {
-  if (c->prod_inflight && hipEventQuery(c->ev_prod) == hipSuccess) {
-    c->prod_inflight = false;
-    c->traj_pub = c->prod_inflight_seq;
-    hipError_t e = hipStreamWaitEvent(st, c->ev_prod, 0);
-    if (e != hipSuccess) return hip_fail(e, "hipStreamWaitEvent(producer)");
-  }
+  (void)st;
+  traj_poll(c);
   if (spawn) traj_new_gen(c);
   return BSG_OK;
 }
@@ -329,7 +332,7 @@ int traj_after(bsg_ctx* c, const bsg::KParams& p0, hipStream_t st, int mode, con
     c->steps_since_prod = kProdEvery;
     return BSG_OK;
   }
-  if (mode != bsg::MODE_STEP || c->prod_inflight || c->traj_noasync ||
+  if (mode != bsg::MODE_STEP || c->prod_out >= kProdMax || c->traj_noasync ||
       ++c->steps_since_prod < kProdEvery)
     return BSG_OK;
   c->steps_since_prod = 0;
@@ -347,18 +350,21 @@ int traj_after(bsg_ctx* c, const bsg::KParams& p0, hipStream_t st, int mode, con
   if (c->prod_seq >= 0x3FFEu) {             // the header's 14-bit sequence wraps: new generation
     if (int r = traj_quiesce(c)) return r;
     c->prod_seq = 0;
-    c->traj_pub = 0;
     traj_new_gen(c);
     q.traj_gen = c->traj_gen;
+    // the publication word back to 0, ordered before every later launch of both streams
+    if ((e = hipMemsetAsync(c->traj + c->cfg.num_envs, 0, 16, st)) != hipSuccess)
+      return hip_fail(e, "hipMemsetAsync(publication)");
   }
   q.prod_seq = ++c->prod_seq;
   if ((e = hipEventRecord(c->ev_step, st)) != hipSuccess) return hip_fail(e, "hipEventRecord(step)");
   if ((e = hipStreamWaitEvent(c->prod_st, c->ev_step, 0)) != hipSuccess)
     return hip_fail(e, "hipStreamWaitEvent(producer stream)");
   if ((e = bsg::launch_produce(q, c->prod_st)) != hipSuccess) return hip_fail(e, "produce launch");
-  if ((e = hipEventRecord(c->ev_prod, c->prod_st)) != hipSuccess) return hip_fail(e, "hipEventRecord(producer)");
-  c->prod_inflight = true;
-  c->prod_inflight_seq = q.prod_seq;
+  const int slot = (c->prod_head + c->prod_out) % 4;
+  if ((e = hipEventRecord(c->ev_prod[slot], c->prod_st)) != hipSuccess)
+    return hip_fail(e, "hipEventRecord(producer)");
+  ++c->prod_out;
   ++c->prod_launches;
   return BSG_OK;
 }
@@ -578,7 +584,8 @@ int32_t bsg_destroy(bsg_ctx* c) {
   (void)traj_quiesce(c);
   if (c->prod_st) (void)hipStreamSynchronize(c->prod_st);
   if (c->ev_step) (void)hipEventDestroy(c->ev_step);
-  if (c->ev_prod) (void)hipEventDestroy(c->ev_prod);
+  for (auto ev : c->ev_prod)
+    if (ev) (void)hipEventDestroy(ev);
   if (c->prod_st) (void)hipStreamDestroy(c->prod_st);
   for (auto& pr : c->pending) {
     (void)hipEventDestroy(pr.first);
@@ -690,13 +697,14 @@ int32_t bsg_set_trajectory(bsg_ctx* c, void* scratch, int64_t bytes, int32_t fla
     const int prio = (qp && std::strcmp(qp, "normal") == 0) ? 0 : least;
     if (e == hipSuccess) e = hipStreamCreateWithPriority(&c->prod_st, hipStreamNonBlocking, prio);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_step, hipEventDisableTiming);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_prod, hipEventDisableTiming);
+    for (int k = 0; k < 4 && e == hipSuccess; ++k)
+      e = hipEventCreateWithFlags(&c->ev_prod[k], hipEventDisableTiming);
     if (e != hipSuccess) return hip_fail(e, "bsg_set_trajectory: stream / events");
   }
   // headers of no generation (0xFF..), counters zero; entries are written before use
-  const size_t head = 8 * (size_t)c->cfg.num_envs * (1 + 2 * bsg::TJ_P);
+  const size_t head = 8 * ((size_t)c->cfg.num_envs * (1 + 2 * bsg::TJ_P) + 2);
   e = hipMemset(scratch, 0xFF, head);
-  if (e == hipSuccess) e = hipMemset(scratch, 0, 8 * (size_t)c->cfg.num_envs);
+  if (e == hipSuccess) e = hipMemset(scratch, 0, 8 * ((size_t)c->cfg.num_envs + 2));
   if (e == hipSuccess) e = hipDeviceSynchronize();
   if (e != hipSuccess) return hip_fail(e, "bsg_set_trajectory: hipMemset");
   c->traj = static_cast<double*>(scratch);
@@ -712,7 +720,7 @@ int32_t bsg_trajectory_info(const bsg_ctx* c, int64_t* out /* [4] */) {
   if (!c || !out) return fail(BSG_E_INVALID_ARG, "bsg_trajectory_info: null argument");
   out[0] = c->traj ? 1 : 0;
   out[1] = c->prod_launches;
-  out[2] = (int64_t)c->traj_pub;
+  out[2] = (int64_t)c->prod_seq;
   out[3] = (int64_t)c->traj_gen;
   return BSG_OK;
 }

@@ -69,7 +69,9 @@ __host__ __device__ constexpr size_t la_sc_offset(size_t E, size_t N) {
 // step's entry into the lookahead slot instead of running ten substeps on the launch's
 // critical path.  A producer launch flies up to TJ_Q more steps of each episode it covers
 // (resuming from the last stored entry), so launches are short and follow each other.
-// Layout, in doubles: [E] u64 copy counters (diagnostics), [E][TJ_P][2] u64 headers (two
+// Layout, in doubles: [E] u64 copy counters (diagnostics), [2] u64 the last producer
+// launch published (its sequence number, stored by its last wave with release semantics) and
+// that launch's wave counter, [E][TJ_P][2] u64 headers (two
 // versions per slot, tj_pack: generation | producer sequence | steps stored | episode
 // counter; a producer rewrites the version that is not the slot's best, so the best stays
 // readable while it runs), entries [TJ_P][S][TJ_F][EN] (the lookahead slot's LA_F fields and
@@ -81,7 +83,7 @@ constexpr int TJ_D = 3;            // a producer launch covers the episodes 1..T
 constexpr int TJ_SMAX = 63;        // (6 bits of the header)
 constexpr int TJ_Q = 6;            // steps per episode per producer launch
 __host__ __device__ constexpr size_t tj_doubles(size_t E, size_t N, size_t S) {
-  return E + 2 * TJ_P * E + TJ_P * S * TJ_F * E * N + (TJ_D + 1) * LA_MC * E * N;
+  return E + 2 + 2 * TJ_P * E + TJ_P * S * TJ_F * E * N + (TJ_D + 1) * LA_MC * E * N;
 }
 
 // Passed by value to every launch (kernarg segment).
@@ -125,7 +127,6 @@ struct KParams {
   double kp[BSG_MERGE_NPARAMS];
   // trajectory store (bsg_set_trajectory; tj_doubles): nullptr = off
   double* traj;
-  uint64_t traj_pub;         // producer launches known complete when this launch was enqueued
   uint32_t traj_gen;         // generation: headers of other generations are stale
   int traj_S;                // steps per stored episode (the TimeLimit)
   int prod_d0, prod_d1;      // produce_kernel: episodes ahead of the running one it covers

@@ -2599,17 +2599,24 @@ __device__ __forceinline__ void la_wait_for_main(const KParams& p, size_t EN, in
 __device__ __forceinline__ uint64_t* tj_count(const KParams& p) {
   return reinterpret_cast<uint64_t*>(p.traj);
 }
-__device__ __forceinline__ uint64_t* tj_hdr(const KParams& p) {
+// the last producer launch whose every wave has finished (release / acquire, agent scope)
+__device__ __forceinline__ uint64_t* tj_pub(const KParams& p) {
   return reinterpret_cast<uint64_t*>(p.traj) + p.E;
+}
+__device__ __forceinline__ uint32_t* tj_done(const KParams& p) {
+  return reinterpret_cast<uint32_t*>(reinterpret_cast<uint64_t*>(p.traj) + p.E + 1);
+}
+__device__ __forceinline__ uint64_t* tj_hdr(const KParams& p) {
+  return reinterpret_cast<uint64_t*>(p.traj) + p.E + 2;
 }
 // the entry of post-step index k (1..S) of the episode in `slot`: TJ_F fields x EN
 __device__ __forceinline__ double* tj_entry(const KParams& p, int slot, int k) {
   const size_t EN = (size_t)p.E * p.N;
-  return p.traj + (size_t)p.E * (1 + 2 * TJ_P) + ((size_t)slot * p.traj_S + (size_t)(k - 1)) * TJ_F * EN;
+  return p.traj + (size_t)p.E * (1 + 2 * TJ_P) + 2 + ((size_t)slot * p.traj_S + (size_t)(k - 1)) * TJ_F * EN;
 }
 __device__ __forceinline__ double* tj_memo(const KParams& p, int d) {
   const size_t EN = (size_t)p.E * p.N;
-  return p.traj + (size_t)p.E * (1 + 2 * TJ_P) + (size_t)TJ_P * p.traj_S * TJ_F * EN +
+  return p.traj + (size_t)p.E * (1 + 2 * TJ_P) + 2 + (size_t)TJ_P * p.traj_S * TJ_F * EN +
          (size_t)d * LA_MC * EN;
 }
 // header: generation (12 bits, 0xFFF = none: the scratch's 0xFF fill) | producer sequence
@@ -2621,12 +2628,12 @@ __device__ __forceinline__ uint64_t tj_pack(uint32_t gen, uint32_t seq, int prog
 }
 __device__ __forceinline__ int tj_prog(uint64_t h) { return (int)((h >> 32) & 63u); }
 // steps of episode `counter` this launch may copy from one header version: this generation and
-// counter, written by a producer launch the host saw complete before enqueueing this one (or
-// ordered before it on the stream); 0 = none
-__device__ __forceinline__ int tj_ready(const KParams& p, uint64_t h, uint32_t counter) {
+// counter, written by a producer launch published before (pub: tj_pub read with acquire) or
+// ordered before this launch on its stream (sequence 0); 0 = none
+__device__ __forceinline__ int tj_ready(const KParams& p, uint64_t h, uint32_t counter, uint64_t pub) {
   const uint32_t seq = (uint32_t)(h >> 38) & 0x3FFFu;
   const bool ok = (uint32_t)(h >> 52) == (p.traj_gen & 0xFFFu) && (uint32_t)h == counter &&
-                  (seq == 0 || (uint64_t)seq <= p.traj_pub);
+                  (seq == 0 || (uint64_t)seq <= pub);
   return ok ? tj_prog(h) : 0;
 }
 
@@ -2724,12 +2731,15 @@ __device__ __forceinline__ void lookahead_role(const KParams& p, LT& L, unsigned
     // episode (tj_ready).  Its copy replaces the ten substeps (and the intruder pairs' CD):
     // the same function of the same counter, so the same bits (tests/test_gpu_trajectory.py).
     if (p.traj && p.mode == MODE_STEP && known) {
+      // (the producers run concurrently on their own stream: the publication word with
+      // acquire semantics first, then the headers and entries it covers)
+      const uint64_t pub = __hip_atomic_load(tj_pub(p), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
       const uint32_t c = rst ? episode : episode - 1u;
       const int k = rst ? 1 : step + 2;
       if (k <= p.traj_S) {
         const uint64_t* hv = tj_hdr(p) + ((size_t)e * TJ_P + c % TJ_P) * 2;
         const uint64_t h0 = hv[0], h1 = hv[1];
-        if (k <= max(tj_ready(p, h0, c), tj_ready(p, h1, c))) {
+        if (k <= max(tj_ready(p, h0, c, pub), tj_ready(p, h1, c, pub))) {
           const uint64_t* en = reinterpret_cast<const uint64_t*>(tj_entry(p, (int)(c % TJ_P), k));
           uint64_t* sl = reinterpret_cast<uint64_t*>(p.la + (size_t)wslot * LA_F * EN);
           const int nf = p.la_cd ? LA_F : LA_STATE;
@@ -3514,7 +3524,7 @@ __global__ __launch_bounds__(64) void produce_kernel(KParams p) {
     k1 = min(p.traj_S, have + p.prod_q);
     need = k0 <= k1;
   }
-  if (__ballot(need) == 0) return;                 // (wave-uniform: one wave per workgroup)
+  if (__ballot(need) != 0) {                      // (wave-uniform: one wave per workgroup)
   const bool run = need && j > 0 && j < N;
   double* memo = tj_memo(p, d);
   const int slot = (int)(c % TJ_P);
@@ -3578,6 +3588,22 @@ __global__ __launch_bounds__(64) void produce_kernel(KParams p) {
   }
   if (need && j == 1)
     tj_hdr(p)[((size_t)e * TJ_P + slot) * 2 + wv] = tj_pack(p.traj_gen, p.prod_seq, k1, c);
+  }
+  // Publication (an asynchronous launch: sequence > 0): every wave releases its stores and
+  // counts itself out; the last one publishes the launch's sequence number, which the step
+  // launches' lookahead waves read with acquire before the headers (producer launches run
+  // one after the other on their stream, so one counter serves them all)
+  if (p.prod_seq != 0) {
+    __threadfence();
+    if (lane == 0) {
+      const uint32_t old = __hip_atomic_fetch_add(tj_done(p), 1u, __ATOMIC_ACQ_REL,
+                                                  __HIP_MEMORY_SCOPE_AGENT);
+      if (old == gridDim.x - 1) {
+        __hip_atomic_store(tj_done(p), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(tj_pub(p), (uint64_t)p.prod_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
 }
 
 hipError_t launch_produce(const KParams& p0, hipStream_t st) {

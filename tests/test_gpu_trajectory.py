@@ -68,11 +68,11 @@ def test_trajectory_sync_bit_identical():
 
 
 def test_trajectory_async_bit_identical():
-    """The product path: producers on their own least-priority stream, published once the
-    host has seen them complete; the reference TimeLimit (50) over three episodes."""
+    """The product path: producers on their own least-priority stream, each publishing itself
+    on the device when its last wave ends; the reference TimeLimit (50) over three episodes."""
     E, N = 512, 32
     info = _run(E, N, 160, True, maxep=50)
-    assert info["producer_launches"] > 2 and info["published"] >= 1
+    assert info["producer_launches"] > 2 and info["producer_seq"] >= 1
     assert int(info["copies"].sum()) > E * 60, int(info["copies"].sum())
 
 
@@ -98,3 +98,27 @@ def test_trajectory_small_groups(N):
     """Env groups of 8 / 4 envs per wave (GS 8, 16): the producers' and the copy's indexing."""
     info = _run(200, N, 40, "sync", maxep=9)
     assert int(info["copies"].sum()) > 200 * 20
+
+
+def test_trajectory_async_host_ahead():
+    """The bench's regime: the host enqueues steps far ahead of the GPU (no synchronisation
+    in the loop), so the lookahead waves meet producers that finish while the step launches
+    enqueued before them run.  Every step's outputs and state are snapshotted on the device
+    and compared after the loop."""
+    E, N, T = 512, 32, 220
+    ref, b = _batch(E, N, False, False, maxep=50), _batch(E, N, True, True, maxep=50)
+    g = torch.Generator(device="cuda").manual_seed(9)
+    acts = torch.rand((T, E, 2), dtype=torch.float64, device="cuda", generator=g) * 2 - 1
+    ref.reset()
+    b.reset()
+    sa, sb = [], []
+    for t in range(T):
+        ref.step(acts[t])
+        b.step(acts[t])
+        sa.append(_snap(ref))
+        sb.append(_snap(b))
+    torch.cuda.synchronize()
+    for t in range(T):
+        _same(sa[t], sb[t], t)
+    info = b.trajectory_info()
+    assert int(info["copies"].sum()) > E * 120, int(info["copies"].sum())
