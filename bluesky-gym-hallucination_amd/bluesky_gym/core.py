@@ -285,7 +285,7 @@ class DeviceBatch:
         nat.check(self.lib.bsg_trajectory_info(self._ctx, out), "bsg_trajectory_info")
         copies = (self._tj_buf[:self.E].view(torch.int64).cpu() if self._tj_buf is not None
                   else torch.zeros(self.E, dtype=torch.int64))
-        return {"bound": int(out[0]), "producer_launches": int(out[1]), "producer_seq": int(out[2]),
+        return {"bound": int(out[0]), "producer_launches": int(out[1]), "producer_outstanding": int(out[2]),
                 "generation": int(out[3]), "copies": copies}
 
     def close(self):

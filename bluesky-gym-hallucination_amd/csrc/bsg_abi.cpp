@@ -67,7 +67,6 @@ struct bsg_ctx {
   bool traj_noasync = false;        // BSG_TRAJ_NOASYNC=1 (A/B runs): reset-time production only
   int traj_wprio = 1;               // BSG_TRAJ_WPRIO=1: producer waves at s_setprio 1 (else 0)
   uint32_t traj_gen = 1;            // 1..0xFFE; bumped when the stored episodes may be stale
-  uint32_t prod_seq = 0;            // last producer sequence number issued (1..0x3FFE)
   int prod_out = 0;                 // producer launches enqueued and not seen complete
   int prod_head = 0;                // oldest of them in ev_prod[] (a ring)
   int steps_since_prod = 0;
@@ -326,7 +325,7 @@ int traj_after(bsg_ctx* c, const bsg::KParams& p0, hipStream_t st, int mode, con
     q.prod_d0 = 0;
     q.prod_d1 = 2;
     q.prod_q = bsg::TJ_SMAX;          // whole episodes
-    q.prod_seq = 0;
+    q.prod_async = 0;
     if ((e = bsg::launch_produce(q, st)) != hipSuccess) return hip_fail(e, "produce launch (reset)");
     ++c->prod_launches;
     c->steps_since_prod = kProdEvery;
@@ -337,26 +336,17 @@ int traj_after(bsg_ctx* c, const bsg::KParams& p0, hipStream_t st, int mode, con
     return BSG_OK;
   c->steps_since_prod = 0;
   q.env_mask = nullptr;
-  q.prod_d0 = 1;
+  q.prod_d0 = 0;                    // (the running episode: continued only)
   q.prod_d1 = bsg::TJ_D;
-  q.prod_q = bsg::TJ_Q;
+  q.prod_q = bsg::TJ_SMAX;
   q.is_prod = c->traj_wprio == 1 ? 2 : 1;
+  q.prod_async = 1;                 // (the running episode continued only, also in sync mode)
   if (c->traj_sync) {
-    q.prod_seq = 0;
     if ((e = bsg::launch_produce(q, st)) != hipSuccess) return hip_fail(e, "produce launch");
     ++c->prod_launches;
     return BSG_OK;
   }
-  if (c->prod_seq >= 0x3FFEu) {             // the header's 14-bit sequence wraps: new generation
-    if (int r = traj_quiesce(c)) return r;
-    c->prod_seq = 0;
-    traj_new_gen(c);
-    q.traj_gen = c->traj_gen;
-    // the publication word back to 0, ordered before every later launch of both streams
-    if ((e = hipMemsetAsync(c->traj + c->cfg.num_envs, 0, 16, st)) != hipSuccess)
-      return hip_fail(e, "hipMemsetAsync(publication)");
-  }
-  q.prod_seq = ++c->prod_seq;
+  q.prod_async = 1;
   if ((e = hipEventRecord(c->ev_step, st)) != hipSuccess) return hip_fail(e, "hipEventRecord(step)");
   if ((e = hipStreamWaitEvent(c->prod_st, c->ev_step, 0)) != hipSuccess)
     return hip_fail(e, "hipStreamWaitEvent(producer stream)");
@@ -702,9 +692,9 @@ int32_t bsg_set_trajectory(bsg_ctx* c, void* scratch, int64_t bytes, int32_t fla
     if (e != hipSuccess) return hip_fail(e, "bsg_set_trajectory: stream / events");
   }
   // headers of no generation (0xFF..), counters zero; entries are written before use
-  const size_t head = 8 * ((size_t)c->cfg.num_envs * (1 + 2 * bsg::TJ_P) + 2);
+  const size_t head = 8 * (size_t)c->cfg.num_envs * (1 + bsg::TJ_P);
   e = hipMemset(scratch, 0xFF, head);
-  if (e == hipSuccess) e = hipMemset(scratch, 0, 8 * ((size_t)c->cfg.num_envs + 2));
+  if (e == hipSuccess) e = hipMemset(scratch, 0, 8 * (size_t)c->cfg.num_envs);
   if (e == hipSuccess) e = hipDeviceSynchronize();
   if (e != hipSuccess) return hip_fail(e, "bsg_set_trajectory: hipMemset");
   c->traj = static_cast<double*>(scratch);
@@ -720,7 +710,7 @@ int32_t bsg_trajectory_info(const bsg_ctx* c, int64_t* out /* [4] */) {
   if (!c || !out) return fail(BSG_E_INVALID_ARG, "bsg_trajectory_info: null argument");
   out[0] = c->traj ? 1 : 0;
   out[1] = c->prod_launches;
-  out[2] = (int64_t)c->prod_seq;
+  out[2] = (int64_t)c->prod_out;
   out[3] = (int64_t)c->traj_gen;
   return BSG_OK;
 }

@@ -67,23 +67,20 @@ __host__ __device__ constexpr size_t la_sc_offset(size_t E, size_t N) {
 // future episodes ahead on a low-priority stream -- every post-step state of steps 1..S and
 // the intruder pairs' StateBased rows -- and the step kernel's lookahead waves copy the next
 // step's entry into the lookahead slot instead of running ten substeps on the launch's
-// critical path.  A producer launch flies up to TJ_Q more steps of each episode it covers
-// (resuming from the last stored entry), so launches are short and follow each other.
-// Layout, in doubles: [E] u64 copy counters (diagnostics), [2] u64 the last producer
-// launch published (its sequence number, stored by its last wave with release semantics) and
-// that launch's wave counter, [E][TJ_P][2] u64 headers (two
-// versions per slot, tj_pack: generation | producer sequence | steps stored | episode
-// counter; a producer rewrites the version that is not the slot's best, so the best stays
-// readable while it runs), entries [TJ_P][S][TJ_F][EN] (the lookahead slot's LA_F fields and
-// the env's minimum separation over the intruder pairs at the ownship's index), then the
-// producers' memo [TJ_D + 1][LA_MC][EN].  Slot = episode counter % TJ_P.
+// critical path.  A producer wave releases each step as it stores it (the header counts the
+// steps held), so an episode is usable step by step while it is being flown; a later launch
+// resumes an episode from its last stored step.
+// Layout, in doubles: [E] u64 copy counters (diagnostics), [E][TJ_P] u64 headers (tj_pack:
+// generation | steps held | episode counter), entries [TJ_P][S][TJ_F][EN] (the lookahead
+// slot's LA_F fields and the env's minimum separation over the intruder pairs at the
+// ownship's index), then the producers' memo [TJ_D + 1][LA_MC][EN].  Slot = episode counter
+// % TJ_P.
 constexpr int TJ_P = 4;
 constexpr int TJ_F = LA_F + 1;
 constexpr int TJ_D = 3;            // a producer launch covers the episodes 1..TJ_D ahead
 constexpr int TJ_SMAX = 63;        // (6 bits of the header)
-constexpr int TJ_Q = 6;            // steps per episode per producer launch
 __host__ __device__ constexpr size_t tj_doubles(size_t E, size_t N, size_t S) {
-  return E + 2 + 2 * TJ_P * E + TJ_P * S * TJ_F * E * N + (TJ_D + 1) * LA_MC * E * N;
+  return E + TJ_P * E + TJ_P * S * TJ_F * E * N + (TJ_D + 1) * LA_MC * E * N;
 }
 
 // Passed by value to every launch (kernarg segment).
@@ -131,7 +128,9 @@ struct KParams {
   int traj_S;                // steps per stored episode (the TimeLimit)
   int prod_d0, prod_d1;      // produce_kernel: episodes ahead of the running one it covers
   int prod_q;                // produce_kernel: steps per episode this launch flies (at most)
-  uint32_t prod_seq;         // produce_kernel: its sequence number (0: ordered on the stream)
+  int prod_async;            // produce_kernel: a step's producer launch, which continues the
+                             // running episode only (0: a reset's, which flies it from its
+                             // creation)
   int is_prod;               // produce_kernel: its waves run at the lowest priority
 };
 

@@ -2599,42 +2599,33 @@ __device__ __forceinline__ void la_wait_for_main(const KParams& p, size_t EN, in
 __device__ __forceinline__ uint64_t* tj_count(const KParams& p) {
   return reinterpret_cast<uint64_t*>(p.traj);
 }
-// the last producer launch whose every wave has finished (release / acquire, agent scope)
-__device__ __forceinline__ uint64_t* tj_pub(const KParams& p) {
-  return reinterpret_cast<uint64_t*>(p.traj) + p.E;
-}
-__device__ __forceinline__ uint32_t* tj_done(const KParams& p) {
-  return reinterpret_cast<uint32_t*>(reinterpret_cast<uint64_t*>(p.traj) + p.E + 1);
-}
 __device__ __forceinline__ uint64_t* tj_hdr(const KParams& p) {
-  return reinterpret_cast<uint64_t*>(p.traj) + p.E + 2;
+  return reinterpret_cast<uint64_t*>(p.traj) + p.E;
 }
 // the entry of post-step index k (1..S) of the episode in `slot`: TJ_F fields x EN
 __device__ __forceinline__ double* tj_entry(const KParams& p, int slot, int k) {
   const size_t EN = (size_t)p.E * p.N;
-  return p.traj + (size_t)p.E * (1 + 2 * TJ_P) + 2 + ((size_t)slot * p.traj_S + (size_t)(k - 1)) * TJ_F * EN;
+  return p.traj + (size_t)p.E * (1 + TJ_P) + ((size_t)slot * p.traj_S + (size_t)(k - 1)) * TJ_F * EN;
 }
 __device__ __forceinline__ double* tj_memo(const KParams& p, int d) {
   const size_t EN = (size_t)p.E * p.N;
-  return p.traj + (size_t)p.E * (1 + 2 * TJ_P) + 2 + (size_t)TJ_P * p.traj_S * TJ_F * EN +
+  return p.traj + (size_t)p.E * (1 + TJ_P) + (size_t)TJ_P * p.traj_S * TJ_F * EN +
          (size_t)d * LA_MC * EN;
 }
-// header: generation (12 bits, 0xFFF = none: the scratch's 0xFF fill) | producer sequence
-// (14 bits; 0 = produced in the stream's own order) | steps stored (6 bits) | Philox episode
-// counter (32 bits)
-__device__ __forceinline__ uint64_t tj_pack(uint32_t gen, uint32_t seq, int prog, uint32_t counter) {
-  return ((uint64_t)(gen & 0xFFFu) << 52) | ((uint64_t)(seq & 0x3FFFu) << 38) |
-         ((uint64_t)(prog & 63) << 32) | (uint64_t)counter;
+// header: generation (12 bits, 0xFFF = none: the scratch's 0xFF fill) | steps stored (6 bits)
+// | Philox episode counter (32 bits).  The producers write it after the entries it covers,
+// behind a release fence, and the lookahead reads it and those entries with agent-coherent
+// loads (tj_ld): the producers run concurrently on their own stream, and no L2 of another
+// XCD may hand back an older line.
+__device__ __forceinline__ uint64_t tj_pack(uint32_t gen, int prog, uint32_t counter) {
+  return ((uint64_t)(gen & 0xFFFu) << 52) | ((uint64_t)(prog & 63) << 32) | (uint64_t)counter;
 }
 __device__ __forceinline__ int tj_prog(uint64_t h) { return (int)((h >> 32) & 63u); }
-// steps of episode `counter` this launch may copy from one header version: this generation and
-// counter, written by a producer launch published before (pub: tj_pub read with acquire) or
-// ordered before this launch on its stream (sequence 0); 0 = none
-__device__ __forceinline__ int tj_ready(const KParams& p, uint64_t h, uint32_t counter, uint64_t pub) {
-  const uint32_t seq = (uint32_t)(h >> 38) & 0x3FFFu;
-  const bool ok = (uint32_t)(h >> 52) == (p.traj_gen & 0xFFFu) && (uint32_t)h == counter &&
-                  (seq == 0 || (uint64_t)seq <= pub);
-  return ok ? tj_prog(h) : 0;
+__device__ __forceinline__ bool tj_match(const KParams& p, uint64_t h, uint32_t counter) {
+  return (uint32_t)(h >> 52) == (p.traj_gen & 0xFFFu) && (uint32_t)h == counter;
+}
+__device__ __forceinline__ uint64_t tj_ld(const uint64_t* q) {
+  return __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // One lookahead wave: the intruders of the same 64/GS envs as main workgroup
@@ -2731,22 +2722,18 @@ __device__ __forceinline__ void lookahead_role(const KParams& p, LT& L, unsigned
     // episode (tj_ready).  Its copy replaces the ten substeps (and the intruder pairs' CD):
     // the same function of the same counter, so the same bits (tests/test_gpu_trajectory.py).
     if (p.traj && p.mode == MODE_STEP && known) {
-      // (the producers run concurrently on their own stream: the publication word with
-      // acquire semantics first, then the headers and entries it covers)
-      const uint64_t pub = __hip_atomic_load(tj_pub(p), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
       const uint32_t c = rst ? episode : episode - 1u;
       const int k = rst ? 1 : step + 2;
       if (k <= p.traj_S) {
-        const uint64_t* hv = tj_hdr(p) + ((size_t)e * TJ_P + c % TJ_P) * 2;
-        const uint64_t h0 = hv[0], h1 = hv[1];
-        if (k <= max(tj_ready(p, h0, c, pub), tj_ready(p, h1, c, pub))) {
+        const uint64_t h = tj_ld(tj_hdr(p) + (size_t)e * TJ_P + c % TJ_P);
+        if (tj_match(p, h, c) && k <= tj_prog(h)) {
           const uint64_t* en = reinterpret_cast<const uint64_t*>(tj_entry(p, (int)(c % TJ_P), k));
           uint64_t* sl = reinterpret_cast<uint64_t*>(p.la + (size_t)wslot * LA_F * EN);
           const int nf = p.la_cd ? LA_F : LA_STATE;
           uint64_t v[LA_F];
 #pragma unroll
-          for (int f = 0; f < LA_F; ++f) v[f] = f < nf ? en[(size_t)f * EN + a] : 0ull;
-          const uint64_t gm = (p.la_cd && j == 1) ? en[(size_t)LA_F * EN + (size_t)e * N] : 0ull;
+          for (int f = 0; f < LA_F; ++f) v[f] = f < nf ? tj_ld(en + (size_t)f * EN + a) : 0ull;
+          const uint64_t gm = (p.la_cd && j == 1) ? tj_ld(en + (size_t)LA_F * EN + (size_t)e * N) : 0ull;
 #pragma unroll
           for (int f = 0; f < LA_F; ++f)
             if (f < nf) sl[(size_t)f * EN + a] = v[f];
@@ -3481,17 +3468,21 @@ static hipError_t launch_kind(const KParams& p, hipStream_t st) {
 
 #if !defined(BSG_KIND_TU) || BSG_KIND_TU == 0
 // ---- produce_kernel: future episodes' intruders into the trajectory store -----------------
-// One wave per (group of 64/GS envs, episode ahead d).  For each env the Philox counter of the
-// episode d ahead of its running one (episode - 1 + d; the episode word is read once, racing
-// the step launches on the other stream: any value it reads is a counter the env has reached
-// or will reach, bsg_internal.h tj_doubles): unless this generation already holds it, the
-// wave creates its intruders (spawn_merge, memo_spawned) and flies the whole episode --
-// propagate<..., LA_ROLE> step after step with the memo fetched between steps, exactly the
+// One wave per (group of 64/GS envs, episode d ahead of each env's running one).  For each env
+// the Philox counter episode - 1 + d (the episode word is read once, racing the step launches
+// on the other stream: any value it reads is a counter the env has reached or will reach,
+// bsg_internal.h tj_doubles).  The wave flies the episode from the last step this generation
+// holds (a fresh one: spawn_merge + memo_spawned; else resumed from the stored state over the
+// creation's, the memo emptied -- a cache, so the same bits) to step min(S, held + prod_q),
+// propagate<..., LA_ROLE> step after step with the memo fetched between steps -- exactly the
 // lookahead wave's sequence over the launches of that episode -- storing every post-step
 // state and, with CD on, the intruder pairs' StateBased rows of it (the lookahead's la_cd
-// block), then the header.  Entries of a slot are only ever overwritten for a counter >= 4
-// ahead, which no env still runs.  d = 0 (bsg_reset with device spawns, on the stream, the
-// envs env_mask selects): the episode just created.  The waves run at priority 0 (is_prod).
+// block); after each step a release fence and the header (steps held).  The asynchronous
+// launches (prod_async) continue the running episode (d = 0) only where it is held already:
+// a running episode created from host rows must not be flown as a Philox one (such a
+// launch retires the generation, so no header of its counter matches).  Entries of a slot
+// are only ever overwritten for a counter >= 4 ahead, which no env still runs.  The waves run
+// below the step launch's (is_prod).
 template <int GS>
 __global__ __launch_bounds__(64) void produce_kernel(KParams p) {
   __shared__ Lds<false> L;
@@ -3509,22 +3500,18 @@ __global__ __launch_bounds__(64) void produce_kernel(KParams p) {
   const size_t a = (size_t)e * N + j;
   uint32_t c = 0;
   bool need = false;
-  int k0 = 1, k1 = 0, wv = 0;                     // steps k0..k1 into header version wv
+  int k0 = 1, k1 = 0;
   if (e < p.E && !(d == 0 && p.env_mask && p.env_mask[e] == 0)) {
     const uint32_t X = *(volatile const uint32_t*)&p.b.episode[e];
     c = X - 1u + (uint32_t)d;
-    // (producer launches run one at a time: both versions are final here)
-    const uint64_t* hv = tj_hdr(p) + ((size_t)e * TJ_P + c % TJ_P) * 2;
-    const bool m0 = (uint32_t)(hv[0] >> 52) == (p.traj_gen & 0xFFFu) && (uint32_t)hv[0] == c;
-    const bool m1 = (uint32_t)(hv[1] >> 52) == (p.traj_gen & 0xFFFu) && (uint32_t)hv[1] == c;
-    const int g0 = m0 ? tj_prog(hv[0]) : 0, g1 = m1 ? tj_prog(hv[1]) : 0;
-    const int have = g0 > g1 ? g0 : g1;
-    wv = g0 > g1 ? 1 : 0;                          // rewrite the version that is not the best
+    // (producer launches run one at a time: the header is final here)
+    const uint64_t h = tj_hdr(p)[(size_t)e * TJ_P + c % TJ_P];
+    const int have = tj_match(p, h, c) ? tj_prog(h) : 0;
     k0 = have + 1;
     k1 = min(p.traj_S, have + p.prod_q);
-    need = k0 <= k1;
+    need = k0 <= k1 && !(p.prod_async && d == 0 && have == 0);
   }
-  if (__ballot(need) != 0) {                      // (wave-uniform: one wave per workgroup)
+  if (__ballot(need) == 0) return;                 // (wave-uniform: one wave per workgroup)
   const bool run = need && j > 0 && j < N;
   double* memo = tj_memo(p, d);
   const int slot = (int)(c % TJ_P);
@@ -3536,8 +3523,6 @@ __global__ __launch_bounds__(64) void produce_kernel(KParams p) {
     if (k0 == 1) {
       memo_spawned<BSG_ENV_MERGE>(p, memo, a, EN, mc);
     } else {
-      // resume from the last stored step: its state over the creation's (selspd / selalt /
-      // selvs never change for an intruder), the memo emptied (a cache: the same bits)
       la_load(tj_entry(p, slot, k0 - 1), a, EN, s);
       memo_invalidate(memo, a, EN);
 #pragma unroll
@@ -3546,10 +3531,8 @@ __global__ __launch_bounds__(64) void produce_kernel(KParams p) {
   }
   const double act[2] = {0.0, 0.0};
   const double oat[4] = {0.0, 0.0, 0.0, 0.0};
-  // (the loop bound is wave-uniform: the CD block's barriers; lanes outside [k0, k1] idle)
-  int klo = k0, khi = k1;
-  if (!need) { klo = 1 << 20; khi = -1; }
-  int wlo = klo, whi = khi;
+  // wave-uniform step range (the CD block's barriers); lanes outside their [k0, k1] idle
+  int wlo = need ? k0 : (1 << 20), whi = need ? k1 : -1;
 #pragma unroll 1
   for (int off = 32; off > 0; off >>= 1) {
     wlo = min(wlo, __shfl_xor(wlo, off, 64));
@@ -3585,24 +3568,11 @@ __global__ __launch_bounds__(64) void produce_kernel(KParams p) {
       if (in && j == 0)
         en[(size_t)LA_F * EN + (size_t)e * N] = __longlong_as_double((long long)L.gmin[g]);
     }
-  }
-  if (need && j == 1)
-    tj_hdr(p)[((size_t)e * TJ_P + slot) * 2 + wv] = tj_pack(p.traj_gen, p.prod_seq, k1, c);
-  }
-  // Publication (an asynchronous launch: sequence > 0): every wave releases its stores and
-  // counts itself out; the last one publishes the launch's sequence number, which the step
-  // launches' lookahead waves read with acquire before the headers (producer launches run
-  // one after the other on their stream, so one counter serves them all)
-  if (p.prod_seq != 0) {
+    // step k of this env is stored: release it, then the header says so
     __threadfence();
-    if (lane == 0) {
-      const uint32_t old = __hip_atomic_fetch_add(tj_done(p), 1u, __ATOMIC_ACQ_REL,
-                                                  __HIP_MEMORY_SCOPE_AGENT);
-      if (old == gridDim.x - 1) {
-        __hip_atomic_store(tj_done(p), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(tj_pub(p), (uint64_t)p.prod_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
+    if (in && j == 1)
+      __hip_atomic_store(tj_hdr(p) + (size_t)e * TJ_P + slot, tj_pack(p.traj_gen, k, c),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 

@@ -257,7 +257,7 @@ int32_t bsg_set_lookahead(bsg_ctx* ctx, void* scratch, int64_t bytes);
 #define BSG_TRAJ_SYNC 1
 int64_t bsg_trajectory_bytes(const bsg_ctx* ctx);
 int32_t bsg_set_trajectory(bsg_ctx* ctx, void* scratch, int64_t bytes, int32_t flags);
-/* out[0] store bound, out[1] producer launches issued, out[2] last producer sequence issued,
+/* out[0] store bound, out[1] producer launches issued, out[2] producer launches enqueued and not seen complete,
  * out[3] generation */
 int32_t bsg_trajectory_info(const bsg_ctx* ctx, int64_t* out);
 

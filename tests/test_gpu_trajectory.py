@@ -72,7 +72,7 @@ def test_trajectory_async_bit_identical():
     on the device when its last wave ends; the reference TimeLimit (50) over three episodes."""
     E, N = 512, 32
     info = _run(E, N, 160, True, maxep=50)
-    assert info["producer_launches"] > 2 and info["producer_seq"] >= 1
+    assert info["producer_launches"] > 2
     assert int(info["copies"].sum()) > E * 60, int(info["copies"].sum())
 
 
