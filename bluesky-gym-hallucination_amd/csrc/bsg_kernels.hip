@@ -2627,6 +2627,24 @@ __device__ __forceinline__ bool tj_match(const KParams& p, uint64_t h, uint32_t 
 __device__ __forceinline__ uint64_t tj_ld(const uint64_t* q) {
   return __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// the producer's stores of entries and headers: agent-coherent as well (written through to
+// the agent's coherence point), so a step needs no L2 write-back to be released -- only its
+// stores complete (tj_drain) before its header is stored
+__device__ __forceinline__ void tj_st(double* q, double v) {
+  __hip_atomic_store(reinterpret_cast<uint64_t*>(q), (uint64_t)__double_as_longlong(v),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void tj_drain() {
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);        // (no compiler reordering across it)
+  __builtin_amdgcn_s_waitcnt(0);                  // every store of this wave performed
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+}
+__device__ __forceinline__ void tj_store_state(double* slot, size_t a, size_t EN, const AC& s) {
+  tj_st(slot + a, s.lat); tj_st(slot + EN + a, s.lon); tj_st(slot + 2 * EN + a, s.alt);
+  tj_st(slot + 3 * EN + a, s.hdg); tj_st(slot + 4 * EN + a, s.tas); tj_st(slot + 5 * EN + a, s.cas);
+  tj_st(slot + 6 * EN + a, s.vs); tj_st(slot + 7 * EN + a, s.ax); tj_st(slot + 8 * EN + a, s.ap_trk);
+  tj_st(slot + 9 * EN + a, __longlong_as_double((long long)s.nav));
+}
 
 // One lookahead wave: the intruders of the same 64/GS envs as main workgroup
 // (blockIdx - la_grid0).  It reads only words no main wave of its launch writes: the
@@ -3548,7 +3566,7 @@ __global__ __launch_bounds__(64) void produce_kernel(KParams p) {
       EnvScalars ev = {};
       propagate<BSG_ENV_MERGE, false, true>(p, e, j, a, s, ev, sub_reward, sub_done, act, mc, oat,
                                             memo, k == 1);
-      la_store(en, a, EN, s);
+      tj_store_state(en, a, EN, s);
     }
     if (p.cfg.compute_cd) {
       if (run && in) stage(L, lane, s);
@@ -3561,15 +3579,15 @@ __global__ __launch_bounds__(64) void produce_kernel(KParams p) {
       const bool cd_on = L.cdsel[g] == CD_INTR && j < N;
       cd_pairs<GS, 1>(L, cd_lists, lane, 0, j, g * GS, N, cd_on, CD_INTR);
       if (run && in) {
-        en[(size_t)LA_STATE * EN + a] = __longlong_as_double((long long)L.cm[lane]);
-        en[(size_t)(LA_STATE + 1) * EN + a] = __longlong_as_double((long long)L.lm[lane]);
-        en[(size_t)(LA_STATE + 2) * EN + a] = __longlong_as_double((long long)L.tmax[lane]);
+        tj_st(en + (size_t)LA_STATE * EN + a, __longlong_as_double((long long)L.cm[lane]));
+        tj_st(en + (size_t)(LA_STATE + 1) * EN + a, __longlong_as_double((long long)L.lm[lane]));
+        tj_st(en + (size_t)(LA_STATE + 2) * EN + a, __longlong_as_double((long long)L.tmax[lane]));
       }
       if (in && j == 0)
-        en[(size_t)LA_F * EN + (size_t)e * N] = __longlong_as_double((long long)L.gmin[g]);
+        tj_st(en + (size_t)LA_F * EN + (size_t)e * N, __longlong_as_double((long long)L.gmin[g]));
     }
-    // step k of this env is stored: release it, then the header says so
-    __threadfence();
+    // step k of this env is stored (every store of the wave performed), then the header says so
+    tj_drain();
     if (in && j == 1)
       __hip_atomic_store(tj_hdr(p) + (size_t)e * TJ_P + slot, tj_pack(p.traj_gen, k, c),
                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
