@@ -93,19 +93,40 @@ def cpu_baseline(seconds: float):
     per = [n / el for n, el in res]
     per1 = [n / el for n, el in res1]
     model = platform.processor() or "unknown"
+    cores = set()
     try:
         with open("/proc/cpuinfo") as f:
+            phys = core = None
             for line in f:
-                if line.startswith("model name"):
+                if line.startswith("model name") and model in ("unknown", platform.processor()):
                     model = line.split(":", 1)[1].strip()
-                    break
+                elif line.startswith("physical id"):
+                    phys = line.split(":", 1)[1].strip()
+                elif line.startswith("core id"):
+                    core = line.split(":", 1)[1].strip()
+                elif not line.strip():
+                    if core is not None:
+                        cores.add((phys, core))
+                    phys = core = None
+            if core is not None:
+                cores.add((phys, core))
     except OSError:
         pass
+    node_cores = len(cores) or (os.cpu_count() or P)
     return {"value": value, "unit": "env_steps/s", "cores": P, "kind": "port",
             "sample": f"oracle/batched.py MergeOracle, {P} processes x 128 envs x 32 aircraft, "
                       f"CD on, {seconds:.0f} s each ({min(per):.0f}-{max(per):.0f} env-steps/s "
                       f"per core), NumPy fp64 one thread per process on '{model}' "
                       f"({avail} CPUs available to this process, {os.cpu_count()} on the host)",
+            # the whole node's CPUs, beside the per-GPU share.  Not run on
+            # them (a GPU box's CPU share is 16 per GPU): the measured mean per-core rate times
+            # the host's physical cores -- an extrapolation, labelled as one
+            "node": {"value": value / P * node_cores, "unit": "env_steps/s", "cores": node_cores,
+                     "kind": "port", "measured": False,
+                     "sample": f"extrapolated: the {P} processes' mean {value / P:.0f} env-steps/s "
+                               f"per core x {node_cores} physical cores of '{model}' "
+                               f"({os.cpu_count()} logical CPUs); the 16-core share above is "
+                               f"the measured figure"},
             # one env per process, as the reference runs (SubprocVecEnv): the same oracle at E=1
             "per_env": {"value": sum(per1), "unit": "env_steps/s", "cores": P,
                         "sample": f"MergeOracle with 1 env x 32 aircraft per process, {P} processes, "

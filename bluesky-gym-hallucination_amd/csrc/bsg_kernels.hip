@@ -2518,6 +2518,9 @@ __device__ __forceinline__ void propagate(const KParams& p, int e, int j, size_t
 // the outputs are the inline path's bit for bit.
 static_assert(LA_MC == MC_FIELDS, "lookahead memo layout");
 
+// (bit 23 of a slot's tag, above any step count: the slot carries the intruder pairs' CD rows
+// -- Merge: copied from the trajectory store; la_tag never sets it)
+constexpr uint64_t kLaRows = 1ull << 23;
 __device__ __forceinline__ uint64_t la_tag(uint32_t episode, int step, uint32_t gen) {
   return ((uint64_t)(gen & 0x7fffu) << 48) | ((uint64_t)(episode & 0xffffffu) << 24) |
          (uint64_t)((uint32_t)step & 0xffffffu);
@@ -2660,11 +2663,10 @@ __device__ __forceinline__ void tj_store_state(double* slot, size_t a, size_t EN
 // next launch reads), so in a run the tags always match.
 template <int KIND, int GS, bool WIND, int CDW, class LT>
 __device__ __forceinline__ void lookahead_role(const KParams& p, LT& L, unsigned short* cd_lists) {
-  // Waves 1.. of a CDW > 1 workgroup (Merge's C4 shards) take no aircraft; with la_cd they
-  // stay for the CD block's barriers (a wave that has left would not be waited for on every
-  // implementation), else they leave now
+  // waves 1.. of a CDW > 1 workgroup (Merge's C4 shards) take no aircraft (and Merge's
+  // lookahead waves run no CD block: the rows come from the trajectory store's copies)
   const bool hw = threadIdx.x >= 64;
-  if (hw && !(KIND == BSG_ENV_MERGE && p.la_cd)) return;
+  if (hw) return;
   const int lane = threadIdx.x & 63;
   const int g = lane / GS, j = lane % GS;
   const int e = ((int)blockIdx.x - p.la_grid0) * (64 / GS) + g;
@@ -2759,8 +2761,9 @@ __device__ __forceinline__ void lookahead_role(const KParams& p, LT& L, unsigned
             if (p.la_cd)
               reinterpret_cast<uint64_t*>(p.la + (2 * LA_F + MC_FIELDS) * EN)
                   [2 * (size_t)p.E + (size_t)wslot * p.E + e] = gm;
-            tags[(size_t)wslot * p.E + e] = rst ? la_tag(episode + 1u, 0, p.la_gen)
-                                                : la_tag(episode, step + 1, p.la_gen);
+            tags[(size_t)wslot * p.E + e] = (rst ? la_tag(episode + 1u, 0, p.la_gen)
+                                                 : la_tag(episode, step + 1, p.la_gen)) |
+                                            (p.la_cd ? kLaRows : 0ull);
             tj_count(p)[e] += 1ull;
           }
           run = false;
@@ -2782,7 +2785,7 @@ __device__ __forceinline__ void lookahead_role(const KParams& p, LT& L, unsigned
     if (p.mode == MODE_PRIME) valid = !rst;
     else if (!known || last) valid = false;
     else if (resetting) valid = true;
-    else valid = p.mode == MODE_STEP && tag_in == la_tag(episode, step, p.la_gen);
+    else valid = p.mode == MODE_STEP && (tag_in & ~kLaRows) == la_tag(episode, step, p.la_gen);
     const bool touch = (p.mode == MODE_STEP && run) || (p.mode == MODE_RESET ? resetting : valid);
 #if defined(BSG_LA_LEGACY) && BSG_LA_LEGACY
     // round 3's priming: on a tag mismatch, this launch's step from the live state
@@ -2847,7 +2850,7 @@ __device__ __forceinline__ void lookahead_role(const KParams& p, LT& L, unsigned
     }
     run = run && valid;
   }
-  if ((KIND != BSG_ENV_VERTICAL_CR && KIND != BSG_ENV_MERGE) || !p.la_cd) return;
+  if (KIND != BSG_ENV_VERTICAL_CR || !p.la_cd) return;
   // The intruder pairs' StateBased rows of the state just stored (the next launch's), for
   // the main waves that take this slot (cd_pairs CD_OWN adds the ownship's pairs)
   if (run) stage(L, lane, s);
@@ -3063,7 +3066,7 @@ __global__ __launch_bounds__(64 * CDW) BSG_WPE void step_kernel(KParams p) {
         }
       }
       if (stepping && on) {
-        if (la_intr && la_tag_in == la_tag(ev.episode, ev.step_count, p.la_gen)) {
+        if (la_intr && (la_tag_in & ~kLaRows) == la_tag(ev.episode, ev.step_count, p.la_gen)) {
           s.lat = s_la.lat; s.lon = s_la.lon; s.alt = s_la.alt; s.hdg = s_la.hdg;
           s.tas = s_la.tas; s.cas = s_la.cas; s.vs = s_la.vs; s.ax = s_la.ax;
           s.ap_trk = s_la.ap_trk; s.nav = s_la.nav;
@@ -3095,7 +3098,10 @@ __global__ __launch_bounds__(64 * CDW) BSG_WPE void step_kernel(KParams p) {
     if constexpr (kLaCd) {
       // the CD of this env takes the lookahead's intruder rows when its intruders' state did
       if (wv == 0 && j == 1)
-        L.cdsel[g] = (stepping && la_intr && la_tag_in == la_tag(ev.episode, ev.step_count, p.la_gen))
+        // (Merge: only a slot the trajectory store filled carries the rows)
+        L.cdsel[g] = (stepping && la_intr &&
+                      (la_tag_in & ~kLaRows) == la_tag(ev.episode, ev.step_count, p.la_gen) &&
+                      (KIND != BSG_ENV_MERGE || (la_tag_in & kLaRows)))
                          ? CD_OWN : CD_ALL;
     }
   }
@@ -3410,8 +3416,8 @@ static hipError_t launch_kind_w(const KParams& p0, hipStream_t st) {
   // Vertical: the lookahead waves also take the intruder pairs' CD (they end well before the
   // main waves there, whose phase 2 runs ~4 rounds of ~230 candidate pairs); Merge: not (its
   // lookahead waves are the critical path, profiles/r03/fastown/README.md)
-  // ... and Merge's, once the trajectory store feeds them (its entries carry the rows; the
-  // lookahead waves that still fly an episode compute them as Vertical's do)
+  // ... and Merge's, once the trajectory store feeds them: its copies carry the rows and mark
+  // the slot (kLaRows); a slot a Merge lookahead wave flew has none and its env takes CD_ALL
   p.la_cd = ((KIND == BSG_ENV_VERTICAL_CR || (KIND == BSG_ENV_MERGE && p.traj)) && p.la &&
              p.cfg.compute_cd) ? 1 : 0;
   const int grid = (p.la && p.mode != MODE_PRIME) ? 2 * grid0 : grid0;
