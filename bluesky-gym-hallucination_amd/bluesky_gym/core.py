@@ -84,15 +84,16 @@ class DeviceBatch:
             raise nat.BsgError("lookahead: MergeEnv / VerticalCREnv with NEXT_STEP (or no) "
                                "autoreset only")
         # trajectory store (bsg_set_trajectory): MergeEnv's future episodes flown ahead on a
-        # low-priority stream, copied by the lookahead (bit-identical).  None = on for the
-        # lookahead's Merge batches up to TRAJECTORY_MAX_ENVS; True / False force it; "sync"
-        # runs the producers on the launch stream (tests)
+        # low-priority stream, copied by the lookahead (bit-identical).  Opt-in: True / "sync"
+        # (the producers on the launch stream, tests); None = BSG_TRAJECTORY=1 turns it on for
+        # the lookahead's Merge batches up to TRAJECTORY_MAX_ENVS.  Off by default: its
+        # concurrent producers slow the step launches they share SIMDs with by more than the
+        # copies save in steady state (profiles/r06/trajectory/)
         self.trajectory = False
         self._tj_buf = None
         tbytes = int(self.lib.bsg_trajectory_bytes(self._ctx)) if self.lookahead else 0
-        # (BSG_TRAJECTORY=0: the automatic choice off -- A/B runs, tools/)
         want_tj = (trajectory if trajectory is not None
-                   else self.E <= self.TRAJECTORY_MAX_ENVS and os.environ.get("BSG_TRAJECTORY", "1") != "0")
+                   else self.E <= self.TRAJECTORY_MAX_ENVS and os.environ.get("BSG_TRAJECTORY", "0") == "1")
         if want_tj and tbytes > 0:
             self._tj_buf = torch.empty((tbytes + 7) // 8, dtype=torch.float64, device=self.device)
             flags = nat.TRAJ_SYNC if trajectory == "sync" else 0

@@ -4,6 +4,7 @@
 // lives in bsg_kernels.hip.  No C++ exception crosses the ABI.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -66,6 +67,8 @@ struct bsg_ctx {
   bool traj_sync = false;           // test hook: producers on the caller's stream, in order
   bool traj_noasync = false;        // BSG_TRAJ_NOASYNC=1 (A/B runs): reset-time production only
   int traj_wprio = 1;               // BSG_TRAJ_WPRIO=1: producer waves at s_setprio 1 (else 0)
+  int traj_every = 1;               // BSG_TRAJ_EVERY: step launches between producer launches
+  int traj_sleep = 0;               // BSG_TRAJ_SLEEP: produce_kernel prod_sleep
   uint32_t traj_gen = 1;            // 1..0xFFE; bumped when the stored episodes may be stale
   int prod_out = 0;                 // producer launches enqueued and not seen complete
   int prod_head = 0;                // oldest of them in ev_prod[] (a ring)
@@ -276,7 +279,7 @@ int trim_pending(bsg_ctx* c) {
 }
 
 // ---- trajectory store scheduling ------------------------------------------------------
-constexpr int kProdEvery = 1;       // step launches between producer launches (at least)
+
 constexpr int kProdMax = 2;         // producer launches enqueued at once (<= 4)
 
 // wait for the enqueued producers (their buffers are about to change or go away)
@@ -328,11 +331,11 @@ int traj_after(bsg_ctx* c, const bsg::KParams& p0, hipStream_t st, int mode, con
     q.prod_async = 0;
     if ((e = bsg::launch_produce(q, st)) != hipSuccess) return hip_fail(e, "produce launch (reset)");
     ++c->prod_launches;
-    c->steps_since_prod = kProdEvery;
+    c->steps_since_prod = 1 << 20;
     return BSG_OK;
   }
   if (mode != bsg::MODE_STEP || c->prod_out >= kProdMax || c->traj_noasync ||
-      ++c->steps_since_prod < kProdEvery)
+      ++c->steps_since_prod < c->traj_every)
     return BSG_OK;
   c->steps_since_prod = 0;
   q.env_mask = nullptr;
@@ -340,6 +343,7 @@ int traj_after(bsg_ctx* c, const bsg::KParams& p0, hipStream_t st, int mode, con
   q.prod_d1 = bsg::TJ_D;
   q.prod_q = bsg::TJ_SMAX;
   q.is_prod = c->traj_wprio == 1 ? 2 : 1;
+  q.prod_sleep = c->traj_sleep;
   q.prod_async = 1;                 // (the running episode continued only, also in sync mode)
   if (c->traj_sync) {
     if ((e = bsg::launch_produce(q, st)) != hipSuccess) return hip_fail(e, "produce launch");
@@ -701,8 +705,10 @@ int32_t bsg_set_trajectory(bsg_ctx* c, void* scratch, int64_t bytes, int32_t fla
   c->traj_sync = (flags & BSG_TRAJ_SYNC) != 0;
   if (const char* na = std::getenv("BSG_TRAJ_NOASYNC")) c->traj_noasync = std::atoi(na) != 0;
   if (const char* wp = std::getenv("BSG_TRAJ_WPRIO")) c->traj_wprio = std::atoi(wp);
+  if (const char* ev = std::getenv("BSG_TRAJ_EVERY")) c->traj_every = std::max(1, std::atoi(ev));
+  if (const char* sl = std::getenv("BSG_TRAJ_SLEEP")) c->traj_sleep = std::max(0, std::atoi(sl));
   traj_new_gen(c);
-  c->steps_since_prod = kProdEvery;
+  c->steps_since_prod = 1 << 20;
   return BSG_OK;
 }
 

@@ -128,6 +128,8 @@ struct KParams {
   int traj_S;                // steps per stored episode (the TimeLimit)
   int prod_d0, prod_d1;      // produce_kernel: episodes ahead of the running one it covers
   int prod_q;                // produce_kernel: steps per episode this launch flies (at most)
+  int prod_sleep;            // produce_kernel: s_sleep(127) rounds after each step of an
+                             // episode >= 2 ahead (duty-cycle throttle; BSG_TRAJ_SLEEP)
   int prod_async;            // produce_kernel: a step's producer launch, which continues the
                              // running episode only (0: a reset's, which flies it from its
                              // creation)

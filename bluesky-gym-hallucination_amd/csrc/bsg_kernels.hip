@@ -3597,6 +3597,9 @@ __global__ __launch_bounds__(64) void produce_kernel(KParams p) {
     if (in && j == 1)
       __hip_atomic_store(tj_hdr(p) + (size_t)e * TJ_P + slot, tj_pack(p.traj_gen, k, c),
                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // an episode two or more ahead has time: leave the SIMD to the step launch's waves
+    if (d >= 2)
+      for (int z = 0; z < p.prod_sleep; ++z) __builtin_amdgcn_s_sleep(127);
   }
 }
 

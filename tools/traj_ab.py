@@ -19,7 +19,7 @@ def one(mode, E):
     import torch
     from bluesky_gym import config, core
     b = core.DeviceBatch(config.merge_config(num_ac=32), E, compute_cd=True, seed=1234,
-                         trajectory=(mode != "off"))
+                         trajectory=(mode != "off"))     # (explicit: the default is off)
     bank = torch.rand((16, E, 2), dtype=torch.float64, device="cuda") * 2 - 1
     b.reset()
     ev0 = torch.cuda.Event(enable_timing=True)
