@@ -134,6 +134,23 @@ def cpu_baseline(seconds: float):
                                   f"env-steps/s per core)"}}
 
 
+def hip_schedule_spin():
+    """hipSetDeviceFlags(hipDeviceScheduleSpin) on the process's HIP runtime (torch's), before
+    the device is initialised: a synchronise spins on the completion signal instead of yielding
+    the CPU (HIP's automatic choice on a host with more CPUs than HIP contexts), so the
+    barrier + synchronise that close a timed region return microseconds after the last kernel
+    rather than after a wake-up.  Returns the HIP status (0 = set), None if the runtime was not
+    found.  BENCH_HIP_SPIN=0 leaves HIP's default."""
+    import ctypes
+    for name in ("libamdhip64.so.7", "libamdhip64.so.6", "libamdhip64.so"):
+        try:
+            lib = ctypes.CDLL(name, mode=os.RTLD_NOLOAD | os.RTLD_GLOBAL)
+        except OSError:
+            continue
+        return int(lib.hipSetDeviceFlags(ctypes.c_uint(1)))
+    return None
+
+
 def load_profile(E):
     """Per-launch HBM bytes and VALU counts from the committed rocprofv3 PMC passes
     (tools/profile.sh -> profiles/traffic.json); None when absent or for another size."""
@@ -208,6 +225,7 @@ def main():
     import torch.distributed as dist
     from bluesky_gym.parallel import ShardedVectorEnv
     from bluesky_gym.vector import MergeVectorEnv
+    spin = hip_schedule_spin() if os.environ.get("BENCH_HIP_SPIN", "1") == "1" else None
 
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # BENCH_BACKEND=gloo rehearses the multi-rank path on fewer GPUs than ranks (test only)
@@ -372,6 +390,9 @@ def main():
                 "gather_transport_note": transport_note,
                 "rccl": comm,
                 "row_check": check,
+                # the HIP runtime's wait mode for the region's closing synchronise (bench.py
+                # hip_schedule_spin; BENCH_HIP_SPIN=0: HIP's default)
+                "hip_schedule": "spin" if spin == 0 else "default",
             },
             "roofline": {
                 # the binding limit is fp64 VALU dependency latency; `frac`
