@@ -134,23 +134,6 @@ def cpu_baseline(seconds: float):
                                   f"env-steps/s per core)"}}
 
 
-def hip_schedule_spin():
-    """hipSetDeviceFlags(hipDeviceScheduleSpin) on the process's HIP runtime (torch's), before
-    the device is initialised: a synchronise spins on the completion signal instead of yielding
-    the CPU (HIP's automatic choice on a host with more CPUs than HIP contexts), so the
-    barrier + synchronise that close a timed region return microseconds after the last kernel
-    rather than after a wake-up.  Returns the HIP status (0 = set), None if the runtime was not
-    found.  BENCH_HIP_SPIN=0 leaves HIP's default."""
-    import ctypes
-    for name in ("libamdhip64.so.7", "libamdhip64.so.6", "libamdhip64.so"):
-        try:
-            lib = ctypes.CDLL(name, mode=os.RTLD_NOLOAD | os.RTLD_GLOBAL)
-        except OSError:
-            continue
-        return int(lib.hipSetDeviceFlags(ctypes.c_uint(1)))
-    return None
-
-
 def load_profile(E):
     """Per-launch HBM bytes and VALU counts from the committed rocprofv3 PMC passes
     (tools/profile.sh -> profiles/traffic.json); None when absent or for another size."""
@@ -218,6 +201,10 @@ def main():
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    # the step kernel's ~1.1 KB of kernel arguments from device memory (AMD's launch-latency
+    # setting for MI300-class parts): -0.3..0.4 us per step at the driver's 20-step region,
+    # three runs each (profiles/r06/timed_region_ab.txt).  Read by HIP at initialisation.
+    os.environ.setdefault("HIP_FORCE_DEV_KERNARG", "1")
     # CPU baseline first, on rank 0 at N=1 only, before anything initialises the GPU
     cpu = None if (world > 1 or args.skip_cpu_baseline) else cpu_baseline(args.cpu_seconds)
 
@@ -225,7 +212,6 @@ def main():
     import torch.distributed as dist
     from bluesky_gym.parallel import ShardedVectorEnv
     from bluesky_gym.vector import MergeVectorEnv
-    spin = hip_schedule_spin() if os.environ.get("BENCH_HIP_SPIN", "1") == "1" else None
 
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # BENCH_BACKEND=gloo rehearses the multi-rank path on fewer GPUs than ranks (test only)
@@ -390,9 +376,9 @@ def main():
                 "gather_transport_note": transport_note,
                 "rccl": comm,
                 "row_check": check,
-                # the HIP runtime's wait mode for the region's closing synchronise (bench.py
-                # hip_schedule_spin; BENCH_HIP_SPIN=0: HIP's default)
-                "hip_schedule": "spin" if spin == 0 else "default",
+                # kernel arguments in device memory (HIP_FORCE_DEV_KERNARG, set in main unless
+                # the caller set it): the ~1.1 KB KParams per launch is fetched from HBM
+                "hip_force_dev_kernarg": os.environ.get("HIP_FORCE_DEV_KERNARG"),
             },
             "roofline": {
                 # the binding limit is fp64 VALU dependency latency; `frac`
