@@ -280,6 +280,10 @@ class ShardedVectorEnv:
         # liveness: gathers issued, and the last one that wrote each slot (Ready.valid)
         self._gseq = 0
         self._slot_seq = [0] * R
+        # the gather whose local rows a slot of self._rows holds now (-1 while a block is being
+        # rewritten: the kernel starts overwriting a slot at the block's first step, up to k - 1
+        # steps before the slot is gathered again; local_rows checks this)
+        self._rows_seq = [0] * R
         self.rows_valid_steps = R * self.k
         if self._fused:
             # per slot, made once: the row block the kernel writes, the gathered view step()
@@ -299,6 +303,7 @@ class ShardedVectorEnv:
                 self._work[blk] = None
             elif self._fused:
                 self._rccl.wait(blk)     # (a fused step's gather of this slot: no Work object)
+            self._rows_seq[blk] = -1
         self.local.batch.set_learner(self._rows[blk, i])
         return blk, i
 
@@ -332,7 +337,7 @@ class ShardedVectorEnv:
                                    self._gathered[blk], blk)
             self._blk = blk + 1 if blk + 1 < self._nslots else 0
             self._gseq += 1
-            self._slot_seq[blk] = self._gseq
+            self._slot_seq[blk] = self._rows_seq[blk] = self._gseq
             return self._views[blk], Ready(self._rwork[blk], self, blk, self._gseq)
         blk, i = self._slot()
         self.local.step_tensors(local_actions)
@@ -344,8 +349,10 @@ class ShardedVectorEnv:
     def local_rows(self, ready) -> torch.Tensor:
         """This rank's own learner rows behind a Ready ([n_local, obs+3] for k = 1, else
         [k, n_local, obs+3]): what every rank must find at this rank's place in the gathered
-        rows (bench.py's cross-rank row check).  Raises StaleRowsError once overwritten."""
-        if not ready.valid:
+        rows (bench.py's cross-rank row check).  Raises StaleRowsError once the kernel has
+        started rewriting them -- for k > 1 that is the first step of the slot's next block,
+        before the slot is gathered again (the gathered rows stay valid until that gather)."""
+        if not ready.valid or self._rows_seq[ready._slot] != ready._seq:
             raise StaleRowsError("the local rows of that gather were overwritten")
         blk = self._rows[ready._slot]
         return blk[0] if self.k == 1 else blk
@@ -375,7 +382,7 @@ class ShardedVectorEnv:
             all_gather_rows(out, src, self.group)
             work = None
         self._gseq += 1
-        self._slot_seq[blk] = self._gseq
+        self._slot_seq[blk] = self._rows_seq[blk] = self._gseq
         ready = Ready(work, self, blk, self._gseq)
         self._blk, self._i = (blk + 1) % self._nslots, 0
         if self.k == 1:

@@ -200,8 +200,15 @@ def _worker_stale(rank, world, port, k, overlap, q):
         ready.wait()
         first = rows.clone()
         n_ok = 0
+        local_ok = []                             # local_rows(ready) still answers
+        env.local_rows(ready)
         for _ in range(env.rows_valid_steps - 1):   # still inside the window
             env.step(None)
+            try:
+                env.local_rows(ready)
+                local_ok.append(True)
+            except StaleRowsError:
+                local_ok.append(False)
             assert ready.valid
             ready.wait()
             assert torch.equal(rows, first)
@@ -215,7 +222,7 @@ def _worker_stale(rank, world, port, k, overlap, q):
             raised = True
         env.flush()
         env.close()
-        q.put((rank, (env.rows_valid_steps, n_ok, raised, ready.valid), None))
+        q.put((rank, (env.rows_valid_steps, n_ok, raised, ready.valid, local_ok), None))
     except Exception as ex:  # pragma: no cover - reported to the parent
         q.put((rank, None, repr(ex)))
     finally:
@@ -235,8 +242,11 @@ def test_stale_rows_raise(k, overlap):
     for _ in range(world):
         r, got, err = q.get(timeout=120)
         assert err is None, f"rank {r}: {err}"
-        valid_steps, n_ok, raised, still_valid = got
+        valid_steps, n_ok, raised, still_valid, local_ok = got
         assert valid_steps == 2 * k and n_ok == valid_steps - 1
+        # this rank's own rows live until the kernel starts rewriting the slot: the first step
+        # of the slot's next block (k > 1), k - 1 steps before the gathered rows go stale
+        assert local_ok == [True] * k + [False] * (k - 1), local_ok
         assert raised and not still_valid
     for p in procs:
         p.join(timeout=30)
