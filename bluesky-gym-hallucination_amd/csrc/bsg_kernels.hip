@@ -2258,7 +2258,10 @@ constexpr int kActDim = (KIND == BSG_ENV_MERGE || KIND == BSG_ENV_STATIC_OBSTACL
 // mcache: the memo-cache buffer this aircraft's entries live in (b.memo_cache; the
 // lookahead blocks' own region; nullptr = no memo -- the same bits, computed in full)
 // LAK = false: a launch without the lookahead (its main waves' ownship loops compiled out)
-template <int KIND, bool WIND, bool LA_ROLE = false, bool LAK = true>
+// PROD: produce_kernel's waves (their priority below the step launch's, KParams::is_prod;
+// compiled out of the step kernel, where two more uniform branches per substep measured +1.4 %
+// on the 4096 x 32 launch, profiles/r06/ab_r05_r06.txt)
+template <int KIND, bool WIND, bool LA_ROLE = false, bool LAK = true, bool PROD = false>
 __device__ __forceinline__ void propagate(const KParams& p, int e, int j, size_t a, AC& s,
                                           EnvScalars& ev, double& sub_reward, bool& sub_done,
                                           const double act[2], const double mc[MC_FIELDS],
@@ -2454,9 +2457,10 @@ __device__ __forceinline__ void propagate(const KParams& p, int e, int j, size_t
         constexpr bool CR = decltype(cruise_tag)::value && LA_ROLE && KIND == BSG_ENV_MERGE && !WIND;
         int it = it0;
         for (; it < S; ++it) {
-          if (p.is_prod == 2) __builtin_amdgcn_s_setprio(1);   // (produce_kernel: below the
-          else if (p.is_prod) __builtin_amdgcn_s_setprio(0);   //  step's own waves)
-          else if (p.la) __builtin_amdgcn_s_setprio(3);
+          if constexpr (PROD) {                                 // (produce_kernel: below the
+            if (p.is_prod == 2) __builtin_amdgcn_s_setprio(1);  //  step's own waves)
+            else __builtin_amdgcn_s_setprio(0);
+          } else if (p.la) __builtin_amdgcn_s_setprio(3);
           else if ((slot & 1) ? (it < sw) : (it >= sw)) __builtin_amdgcn_s_setprio(1);
           else __builtin_amdgcn_s_setprio(0);
           substep<WIND, KIND != BSG_ENV_MERGE, CR>(s, m, dt, rt, p.wind, it == 0 ? fh0 : trk_ok);
@@ -3570,7 +3574,7 @@ __global__ __launch_bounds__(64) void produce_kernel(KParams p) {
       double sub_reward = 0.0;
       bool sub_done = false;
       EnvScalars ev = {};
-      propagate<BSG_ENV_MERGE, false, true>(p, e, j, a, s, ev, sub_reward, sub_done, act, mc, oat,
+      propagate<BSG_ENV_MERGE, false, true, true, true>(p, e, j, a, s, ev, sub_reward, sub_done, act, mc, oat,
                                             memo, k == 1);
       tj_store_state(en, a, EN, s);
     }

@@ -252,11 +252,23 @@ def test_fused_sac_update_matches_autograd_update(obs_dim, act_dim, gemm):
     for gx, gy in zip(*grads):
         scale = float(gx.abs().max())
         assert float((gx - gy).abs().max()) <= 1e-4 * scale + 1e-7, (gx - gy).abs().max().item()
-    # (1b) VERDICT r05 weak #6: the bar at one update, before Adam's moments amplify anything:
-    # Adam's first step is lr * g / (|g| + eps) -- sign(g) * lr wherever |g| >> eps -- so
-    # rounding-level gradient differences leave the parameters within 1e-6 (a thousandth of a step)
-    for x, y in zip(*first):
-        assert torch.allclose(x, y, rtol=1e-6, atol=1e-6), (x - y).abs().max().item()
+    # (1b) VERDICT r05 weak #6: the bar at one update, before Adam's moments build up.  Adam's
+    # first step is lr * g / (|g| + eps): where both gradients are well clear of zero and of
+    # their difference (min |g| > max(1e-6, 10 |gx - gy|)) it is lr * sign(g) on both paths to
+    # ~lr * eps / (10 |g|) <= 1e-9, so the parameters must agree to 1e-6; an entry whose
+    # gradient is within rounding of zero may step by up to 2 lr either way (measured 3.7e-5 on
+    # one such entry at Merge's shape, gpurun_out/r06/gpu_tests.log), and is counted instead:
+    # such entries must stay rare, or the gradients differ by more than rounding.
+    n_all = n_loose = 0
+    for x, y, gx, gy in zip(*first, *grads):
+        both0 = (gx == 0) & (gy == 0)
+        clear = torch.minimum(gx.abs(), gy.abs()) > torch.clamp(10 * (gx - gy).abs(), min=1e-6)
+        tight = clear | both0
+        assert torch.allclose(x[tight], y[tight], rtol=1e-6, atol=1e-6), \
+            (x[tight] - y[tight]).abs().max().item()
+        n_all += x.numel()
+        n_loose += int((~tight).sum())
+    assert n_loose <= 0.02 * n_all, (n_loose, n_all)
     for x, y in zip(*out):
         assert torch.allclose(x, y, rtol=1e-4, atol=1e-4), (x - y).abs().max().item()
     (lq0, la0), (lq1, la1) = losses
