@@ -140,6 +140,8 @@ hipError_t launch_step(const KParams& p, hipStream_t stream);
 
 // produce_kernel (Merge translation unit): the episodes prod_d0..prod_d1 ahead of each env's
 // running one into the trajectory store, on `stream`
+// the lookahead-free Merge launch (its own translation unit: bsg_kernels.hip BSG_MERGE_NL_TU)
+hipError_t launch_merge_nl(const KParams& p, int gs, int grid, hipStream_t st);
 hipError_t launch_produce(const KParams& p, hipStream_t stream);
 
 // Merge's creation-state constants (KParams::spawn_k) into out[0..7] (device; out[4] = 1.0

@@ -3480,7 +3480,12 @@ static hipError_t launch_kind_w(const KParams& p0, hipStream_t st) {
   } else if constexpr (KIND == BSG_ENV_SECTOR_CR) {
     switch (gs) { BSG_CASE(8) BSG_CASE(16) BSG_CASE(32) BSG_CASE(64) default: return hipErrorInvalidValue; }
   } else {
-    if constexpr ((KIND == BSG_ENV_MERGE || KIND == BSG_ENV_VERTICAL_CR) && !WIND) {
+    if constexpr (KIND == BSG_ENV_MERGE && !WIND) {
+      // the lookahead-free Merge launch (the 4,096 x 32 headline): its own translation unit,
+      // scheduled for ILP (launch_merge_nl below)
+      if (!p.la) return launch_merge_nl(p, gs, grid, st);
+    }
+    if constexpr (KIND == BSG_ENV_VERTICAL_CR && !WIND) {
       if (!p.la) {
 #define BSG_CASE_NL(G) \
   case G: hipLaunchKernelGGL((step_kernel<KIND, G, WIND, 1, false>), dim3(grid), dim3(64), p.lds_pad, st, p); break;
@@ -3506,7 +3511,7 @@ static hipError_t launch_kind(const KParams& p, hipStream_t st) {
   return p.wind.np > 0 ? launch_kind_w<KIND, true>(p, st) : launch_kind_w<KIND, false>(p, st);
 }
 
-#if !defined(BSG_KIND_TU) || BSG_KIND_TU == 0
+#if (!defined(BSG_KIND_TU) || BSG_KIND_TU == 0) && !defined(BSG_MERGE_NL_TU)
 // ---- produce_kernel: future episodes' intruders into the trajectory store -----------------
 // One wave per (group of 64/GS envs, episode d ahead of each env's running one).  For each env
 // the Philox counter episode - 1 + d (the episode word is read once, racing the step launches
@@ -3675,6 +3680,26 @@ hipError_t spawn_consts_merge(double spd, double alt, double* out, hipStream_t s
 // One translation unit per env kind (the Makefile compiles this file once per kind with
 // -DBSG_KIND_TU=<kind>, so the seven kinds build in parallel); launch_step dispatches
 // (bsg_dispatch.cpp).
+// The lookahead-free Merge instances (step_kernel<MERGE, G, false, 1, false>: MergeEnv without
+// the lookahead, the 4,096 x 32 headline) in a translation unit of their own
+// (-DBSG_MERGE_NL_TU=1), which the Makefile compiles with LLVM's max-ilp machine scheduler: the
+// launch is two waves per SIMD on latency-bound f64 chains, and that schedule measured -0.5 %
+// per launch at 4,096 x 32 (247 VGPRs, still two waves per SIMD) where it costs the
+// lookahead instances their occupancy (+70 % at 512 envs: profiles/r06/ab_sched_strategy.txt).
+// Scheduling only: the same instructions on the same operands, so the same bits.
+#if defined(BSG_MERGE_NL_TU)
+hipError_t launch_merge_nl(const KParams& p, int gs, int grid, hipStream_t st) {
+#define BSG_CASE_NL(G) \
+  case G: hipLaunchKernelGGL((step_kernel<BSG_ENV_MERGE, G, false, 1, false>), dim3(grid), dim3(64), p.lds_pad, st, p); break;
+  switch (gs) {
+    BSG_CASE_NL(2) BSG_CASE_NL(4) BSG_CASE_NL(8) BSG_CASE_NL(16) BSG_CASE_NL(32) BSG_CASE_NL(64)
+    default: return hipErrorInvalidValue;
+  }
+#undef BSG_CASE_NL
+  return hipGetLastError();
+}
+#endif
+
 #ifdef BSG_KIND_TU
 #define BSG_CAT2(a, b) a##b
 #define BSG_CAT(a, b) BSG_CAT2(a, b)
