@@ -2899,7 +2899,7 @@ __device__ __forceinline__ void lookahead_role(const KParams& p, LT& L, unsigned
 // the CD is a serial tail after the substeps of each wave.
 // BSG_WAVES_PER_EU: cap the registers for that many waves per SIMD (the compiler spills the
 // rest to scratch).  The Makefile sets 2 for MergeEnv's translation units, whose max-ilp
-// schedule would otherwise take the lookahead instances to one wave per SIMD (MERGE_FLAGS).
+// schedule would otherwise take the lookahead instances to one wave per SIMD (ILP_FLAGS).
 #if defined(BSG_WAVES_PER_EU)
 #define BSG_WPE __attribute__((amdgpu_waves_per_eu(BSG_WAVES_PER_EU, BSG_WAVES_PER_EU)))
 #else
