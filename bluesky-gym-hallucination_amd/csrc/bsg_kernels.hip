@@ -3428,8 +3428,13 @@ static hipError_t launch_kind_w(const KParams& p0, hipStream_t st) {
     if (!p.la) return hipSuccess;
     p.la_grid0 = 0;                          // every workgroup takes the lookahead role
   }
+#if defined(BSG_PRIO_SW_NUM)                // (experiment builds: the switch point's A/B)
+  p.prio_sw_num = BSG_PRIO_SW_NUM;
+  p.prio_sw_den = BSG_PRIO_SW_DEN;
+#else
   p.prio_sw_num = 3;                         // (the lookahead's waves: fixed priority)
   p.prio_sw_den = 4;
+#endif
   // Vertical: the lookahead waves also take the intruder pairs' CD (they end well before the
   // main waves there, whose phase 2 runs ~4 rounds of ~230 candidate pairs); Merge: not (its
   // lookahead waves are the critical path, profiles/r03/fastown/README.md)
